@@ -1,0 +1,256 @@
+"""Generate the golden vectors under tests/golden/ from the REFERENCE's own modules.
+
+Run in the build container only (the reference tree is absent on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it imports from /root/reference (read-only, by file path):
+  * cat_seg/third_party/model_vpt.py       -> CLIP (visual dense encoder + text encoder)
+  * cat_seg/modeling/transformer/model.py  -> Aggregator (needs `timm.layers`, absent here:
+    a stub module provides Mlp/DropPath/to_2tuple with timm 0.8 eval semantics —
+    fc1 -> act -> fc2, DropPath identity at eval)
+  * cat_seg/third_party/simple_tokenizer.py + clip.tokenize semantics (needs `ftfy`, absent:
+    stubbed as identity; exact for the ASCII class lists)
+The detectron2 glue (ImageList pad, sem_seg_postprocess, CATSeg.forward eval branches,
+cat_seg_model.py:147-229) cannot be imported (detectron2 is not installed) and is
+restated inline below, independently of oracle/catseg_oracle.py.
+
+Weights come from the build's deterministic synthesizer (cat_seg.weights), loaded into
+the reference modules with strict=True so every key name is checked.
+Outputs: small .npz fixtures (inputs + expected outputs).
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "cat-seg_amd"))
+
+from cat_seg.arch import TINY, VIT_B16  # noqa: E402
+from cat_seg.weights import synthesize_state_dict, CLIP as CLIP_P, AGG as AGG_P  # noqa: E402
+
+
+def _stub_timm():
+    class Mlp(nn.Module):
+        def __init__(self, in_features, hidden_features=None, out_features=None,
+                     act_layer=nn.GELU, drop=0.0, **_):
+            super().__init__()
+            out_features = out_features or in_features
+            hidden_features = hidden_features or in_features
+            self.fc1 = nn.Linear(in_features, hidden_features)
+            self.act = act_layer()
+            self.fc2 = nn.Linear(hidden_features, out_features)
+
+        def forward(self, x):
+            return self.fc2(self.act(self.fc1(x)))
+
+    class DropPath(nn.Module):
+        def __init__(self, p=0.0):
+            super().__init__()
+
+        def forward(self, x):
+            return x
+
+    layers = types.ModuleType("timm.layers")
+    layers.Mlp = Mlp
+    layers.DropPath = DropPath
+    layers.to_2tuple = lambda x: tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+    layers.to_ntuple = lambda n: (lambda x: tuple([x] * n))
+    layers.trunc_normal_ = lambda t, **k: t
+    layers.PatchEmbed = None
+    layers._assert = lambda c, m="": None
+    timm = types.ModuleType("timm")
+    timm.layers = layers
+    sys.modules["timm"] = timm
+    sys.modules["timm.layers"] = layers
+    ftfy = types.ModuleType("ftfy")
+    ftfy.fix_text = lambda s: s
+    sys.modules["ftfy"] = ftfy
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_stub_timm()
+model_vpt = _load("ref_model_vpt", f"{REF}/cat_seg/third_party/model_vpt.py")
+agg_mod = _load("ref_agg_model", f"{REF}/cat_seg/modeling/transformer/model.py")
+tok_mod = _load("ref_simple_tokenizer", f"{REF}/cat_seg/third_party/simple_tokenizer.py")
+
+
+# ---------------------------------------------------------------- tokens
+def tokenize(tok, texts, context_length=77):
+    # clip.tokenize semantics (cat_seg/third_party/clip.py:200-214)
+    sot, eot = tok.encoder["<|startoftext|>"], tok.encoder["<|endoftext|>"]
+    out = np.zeros((len(texts), context_length), dtype=np.int64)
+    for i, t in enumerate(texts):
+        ids = [sot] + tok.encode(t) + [eot]
+        assert len(ids) <= context_length
+        out[i, : len(ids)] = ids
+    return out
+
+
+def class_prompts(names):
+    # cat_seg_predictor.py:196-201: first alias before ", ", single template (:84-85)
+    return ["A photo of a {} in the scene".format(n.split(", ")[0] if ", " in n else n) for n in names]
+
+
+# ---------------------------------------------------------------- reference model build
+def build_reference(arch, sd, pad_len=256):
+    clip = model_vpt.CLIP(
+        arch.embed_dim, arch.vision_pretrain_res, arch.vision_layers, arch.vision_width,
+        arch.vision_patch, arch.context_length, arch.vocab_size, arch.text_width,
+        arch.text_heads, arch.text_layers)
+    clip_sd = {k[len(CLIP_P):]: v for k, v in sd.items() if k.startswith(CLIP_P)}
+    clip.load_state_dict(clip_sd, strict=True)
+    agg = agg_mod.Aggregator(
+        text_guidance_dim=arch.embed_dim, text_guidance_proj_dim=arch.text_guidance_proj_dim,
+        appearance_guidance_dim=arch.embed_dim,
+        appearance_guidance_proj_dim=arch.appearance_guidance_proj_dim,
+        decoder_dims=list(arch.decoder_dims), decoder_guidance_dims=list(arch.decoder_guidance_dims),
+        decoder_guidance_proj_dims=list(arch.decoder_guidance_proj_dims),
+        num_layers=arch.num_layers, nheads=arch.nheads, hidden_dim=arch.hidden_dim,
+        pooling_size=list(arch.pooling_size), feature_resolution=list(arch.feature_resolution),
+        window_size=arch.window_size, attention_type="linear", prompt_channel=1, pad_len=pad_len)
+    agg_sd = {k[len(AGG_P):]: v for k, v in sd.items() if k.startswith(AGG_P)}
+    missing, unexpected = agg.load_state_dict(agg_sd, strict=False)
+    # the only non-parameter entries are the SW-MSA mask buffers (model.py:183)
+    assert all(k.endswith("attn_mask") for k in missing), missing
+    assert not unexpected, unexpected
+    up1 = nn.ConvTranspose2d(arch.vision_width, arch.decoder_guidance_dims[0], 2, 2)
+    up2 = nn.ConvTranspose2d(arch.vision_width, arch.decoder_guidance_dims[1], 4, 4)
+    up1.load_state_dict({"weight": sd["upsample1.weight"], "bias": sd["upsample1.bias"]})
+    up2.load_state_dict({"weight": sd["upsample2.weight"], "bias": sd["upsample2.bias"]})
+    for m in (clip, agg, up1, up2):
+        m.eval()
+    return clip.float(), agg, up1, up2
+
+
+def ref_text(clip, tokens):
+    # cat_seg_predictor.py:214-219
+    with torch.no_grad():
+        e = clip.encode_text(torch.from_numpy(tokens))
+        e = e / e.norm(dim=-1, keepdim=True)
+    return e.unsqueeze(1)
+
+
+def ref_head(arch, clip, agg, up1, up2, clip_images, text):
+    """cat_seg_model.py:155,178-188 with the reference CLIP/Aggregator modules."""
+    layers = []
+    hs = [clip.visual.transformer.resblocks[l].register_forward_hook(lambda m, i, o: layers.append(o))
+          for l in arch.hook_layers]
+    with torch.no_grad():
+        feats = clip.encode_image(clip_images, dense=True)
+        g = arch.grid
+        img = feats[:, 1:, :]
+        B = img.shape[0]
+        res3 = img.reshape(B, g, g, -1).permute(0, 3, 1, 2)
+        res4 = layers[0][1:].permute(1, 2, 0).reshape(B, -1, g, g)
+        res5 = layers[1][1:].permute(1, 2, 0).reshape(B, -1, g, g)
+        vis = [res3, up1(res4), up2(res5)]
+        out = agg(res3, text.repeat(B, 1, 1, 1), vis)
+    for h in hs:
+        h.remove()
+    return out
+
+
+def glue_preprocess(arch, images):
+    """cat_seg_model.py:149-154 + detectron2 ImageList.from_tensors (pad /32, value 0)."""
+    mean = torch.tensor(arch.clip_pixel_mean).view(-1, 1, 1)
+    std = torch.tensor(arch.clip_pixel_std).view(-1, 1, 1)
+    norm = [(im - mean) / std for im in images]
+    H = max(x.shape[1] for x in norm)
+    W = max(x.shape[2] for x in norm)
+    d = arch.size_divisibility
+    H, W = -(-H // d) * d, -(-W // d) * d
+    pad = torch.zeros(len(norm), 3, H, W)
+    for i, x in enumerate(norm):
+        pad[i, :, : x.shape[1], : x.shape[2]] = x
+    R = arch.clip_resolution
+    return F.interpolate(pad, size=(R, R), mode="bilinear", align_corners=False)
+
+
+def glue_post(logits0, size, h, w):
+    """sigmoid + detectron2 sem_seg_postprocess (cat_seg_model.py:222-227)."""
+    r = logits0.sigmoid()[:, : size[0], : size[1]].unsqueeze(0)
+    return F.interpolate(r, size=(h, w), mode="bilinear", align_corners=False)[0]
+
+
+def rand_images(seed, shapes):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randint(0, 256, (3, h, w), generator=g, dtype=torch.uint8) for h, w in shapes]
+
+
+def rand_tokens(seed, T, ctx, vocab):
+    g = np.random.default_rng(seed)
+    toks = np.zeros((T, ctx), dtype=np.int64)
+    for t in range(T):
+        n = int(g.integers(3, ctx - 1))
+        toks[t, 0] = vocab - 2
+        toks[t, 1:n] = g.integers(1, vocab - 2, n - 1)
+        toks[t, n] = vocab - 1                           # EOT = highest id (argmax)
+    return toks
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: (v.numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in arrays.items()})
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def e2e_case(name, arch, T, shapes, seed, pad_len=256, tokens=None, sub=1):
+    sd = synthesize_state_dict(arch, seed=0)
+    clip, agg, up1, up2 = build_reference(arch, sd, pad_len=pad_len)
+    if tokens is None:
+        tokens = rand_tokens(seed, T, arch.context_length, arch.vocab_size)
+    text = ref_text(clip, tokens)
+    imgs = rand_images(seed, shapes)
+    clip_images = glue_preprocess(arch, [i.float() for i in imgs])
+    logits = ref_head(arch, clip, agg, up1, up2, clip_images, text)
+    out0 = glue_post(logits[0], shapes[0], shapes[0][0], shapes[0][1])
+    kw = dict(tokens=tokens, text=text, logits=logits[:, :, ::sub, ::sub] if sub > 1 else logits,
+              logits_sum=logits.double().sum(), logits_abs_sum=logits.double().abs().sum(),
+              sem_seg0_sub=out0[:, ::8, ::8], sem_seg0_sum=out0.double().sum(),
+              pad_len=pad_len, sub=sub)
+    for i, im in enumerate(imgs):
+        kw[f"image{i}"] = im
+    save(name, **kw)
+
+
+def main():
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    tok = tok_mod.SimpleTokenizer()
+    # class-name token ids for the reference datasets (the product takes token ids)
+    toks = {}
+    for ds in ("voc20", "ade150", "pc459", "ade847"):
+        names = json.load(open(f"{REF}/datasets/{ds}.json"))
+        toks[ds] = tokenize(tok, class_prompts(names)).astype(np.int32)
+    save("class_tokens", **toks)
+    # 1) tiny arch, T=10 < pad_len=16 (learned padding path), two ragged images (ImageList pad)
+    e2e_case("e2e_tiny_pad", TINY, 10, [(300, 352), (320, 256)], seed=1, pad_len=16)
+    # 2) tiny arch, T=24 > pad_len=16 (top-k + scatter -100), pooling (2,2)
+    e2e_case("e2e_tiny_topk_pool", TINY.replace(pooling_size=(2, 2)), 24, [(384, 384)], seed=2, pad_len=16)
+    # 3) tiny arch, default pad_len 256, T=20, pooling (1,1) (the eval protocol), B=2
+    e2e_case("e2e_tiny_eval", TINY, 20, [(384, 384), (384, 384)], seed=3)
+    # 4) config 1: ViT-B/16@384 (pos-embed bicubic resize), voc20 tokens, bs=1, POOLING (2,2)
+    e2e_case("e2e_b16_voc20", VIT_B16.replace(pooling_size=(2, 2)), 20, [(384, 384)], seed=4,
+             tokens=toks["voc20"].astype(np.int64), sub=2)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,46 @@
+"""Pin the CPU oracle (oracle/catseg_oracle.py) to the golden vectors produced by the
+reference's own modules (tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import catseg_oracle as O
+from cat_seg.arch import TINY, VIT_B16
+from cat_seg.weights import synthesize_state_dict
+
+from conftest import GOLDEN
+
+CASES = {
+    "e2e_tiny_pad": TINY,
+    "e2e_tiny_topk_pool": TINY.replace(pooling_size=(2, 2)),
+    "e2e_tiny_eval": TINY,
+    "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2)),
+}
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_oracle_matches_reference_golden(name):
+    if name == "e2e_b16_voc20" and os.environ.get("CATSEG_FAST_TESTS"):
+        pytest.skip("fast mode")
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = load(name)
+    arch = CASES[name].replace(pad_len=int(g["pad_len"]))
+    sd = synthesize_state_dict(arch, seed=0)
+    tokens = torch.from_numpy(g["tokens"]).long()
+    text = O.text_embeds(arch, sd, tokens)
+    np.testing.assert_allclose(text.numpy(), g["text"], atol=2e-6, rtol=0)
+    imgs = [torch.from_numpy(g[k]).float() for k in sorted(k for k in g if k.startswith("image"))]
+    clip_images, sizes = O.preprocess(arch, imgs)
+    logits = O.head_logits(arch, sd, clip_images, torch.from_numpy(g["text"]))
+    sub = int(g["sub"])
+    got = logits[:, :, ::sub, ::sub] if sub > 1 else logits
+    np.testing.assert_allclose(got.numpy(), g["logits"], atol=2e-5, rtol=0)
+    assert abs(logits.double().sum().item() - float(g["logits_sum"])) < 1e-2
+    out = O.catseg_forward(arch, sd, [{"image": i} for i in imgs], torch.from_numpy(g["text"]))
+    np.testing.assert_allclose(out[0]["sem_seg"][:, ::8, ::8].numpy(), g["sem_seg0_sub"], atol=1e-5, rtol=0)
