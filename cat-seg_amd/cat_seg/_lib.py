@@ -1,0 +1,147 @@
+"""ctypes binding of libcatseg_hip.so (include/catseg_hip.h).
+
+The library is the product: there is no fallback.  Loading fails loudly when the
+shared object is missing, and `require_gpu()` fails when no HIP device is
+visible, so nothing on the path can silently run elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CATSEG_HIP_LIB", os.path.join(_HERE, "libcatseg_hip.so"))
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_QUICKGELU, ACT_SIGMOID = 0, 1, 2, 3, 4
+BIG = 1 << 62
+
+i64, i32, f32, vp = C.c_int64, C.c_int, C.c_float, C.c_void_p
+
+
+class RowMap(C.Structure):
+    _fields_ = [(n, i64) for n in ("d1", "m1", "s1", "d2", "m2", "s2", "off")]
+
+
+def rowmap(d1=1, m1=BIG, s1=1, d2=1, m2=1, s2=0, off=0) -> RowMap:
+    return RowMap(d1, m1, s1, d2, m2, s2, off)
+
+
+IDENTITY = rowmap()
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("A", vp), ("lda", i64), ("amap", RowMap),
+        ("W", vp), ("ldw", i64),
+        ("M", i64), ("N", i64), ("K", i64),
+        ("bias", vp),
+        ("add", vp), ("ld_add", i64), ("addmap", RowMap), ("add_ncols", i64),
+        ("act", i32), ("alpha", f32),
+        ("res", vp), ("ld_res", i64),
+        ("res2", vp), ("ld_res2", i64),
+        ("out", vp), ("ldo", i64),
+        ("store_mode", i32), ("cvt_k", i32), ("cvt_hin", i32), ("cvt_win", i32), ("cvt_cout", i32),
+        ("dtype_a", i32), ("dtype_out", i32),
+    ]
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
+        ("out", vp), ("ld_out", i64),
+        ("n_seq", i64), ("seq_len", i32), ("n_heads", i32), ("head_dim", i32),
+        ("scale", f32), ("causal", i32),
+        ("mode", i32), ("img_h", i32), ("img_w", i32), ("window", i32), ("shift", i32),
+        ("dtype", i32),
+    ]
+
+
+class LinAttnArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
+        ("x", vp), ("y", vp), ("ld_xy", i64),
+        ("B", i64), ("T", i32), ("HW", i32), ("n_heads", i32), ("head_dim", i32),
+        ("n_pad", i32), ("k_pad", vp), ("v_pad", vp), ("eps", f32),
+        ("dtype", i32),
+    ]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [
+        ("src1", vp), ("s1_slice_stride", i64), ("s1_offset", i64), ("c1", i32),
+        ("src2", vp), ("s2_slice_stride", i64), ("s2_offset", i64), ("c2", i32), ("src2_div", i64),
+        ("S", i64), ("H", i32), ("W", i32),
+        ("weight", vp), ("c_out", i32),
+        ("bias", vp), ("act", i32),
+        ("gn_mean", vp), ("gn_rstd", vp), ("gn_gamma", vp), ("gn_beta", vp), ("gn_cpg", i32),
+        ("out", vp), ("stats", vp), ("stats_cpg", i32),
+        ("dtype", i32),
+    ]
+
+
+# name -> (argtypes); every entry returns int
+_SIGS = {
+    "catseg_gemm": [C.POINTER(GemmArgs), vp],
+    "catseg_layernorm": [vp, i64, RowMap, i32, vp, i64, i32, vp, vp, i64, i64, f32, vp],
+    "catseg_l2normalize": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, f32, vp],
+    "catseg_attention": [C.POINTER(AttnArgs), vp],
+    "catseg_linear_attention": [C.POINTER(LinAttnArgs), vp],
+    "catseg_conv3x3": [C.POINTER(ConvArgs), vp],
+    "catseg_conv_tile_rows": [],
+    "catseg_groupnorm_stats": [vp, i64, i32, i32, i64, f32, vp, vp, vp],
+    "catseg_groupnorm_relu": [vp, vp, i64, i64, i32, i32, vp, vp, vp, vp, i32, vp],
+    "catseg_conv3x3_head": [vp, i64, i32, i32, i32, i32, vp, f32, vp, i32, vp, i32, vp],
+    "catseg_conv3x3_head_gn": [vp, i64, i32, i32, i32, i32, vp, f32, vp, vp, vp, vp, i32, vp, i32, vp, i32, vp],
+    "catseg_corr_embed": [vp, i64, i64, vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, vp],
+    "catseg_topk_classes": [vp, i64, i64, i64, i32, i32, i32, vp, vp],
+    "catseg_gather_rows": [vp, i64, vp, i64, i64, vp, i64, i32, vp],
+    "catseg_convert": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, vp],
+    "catseg_fill_f32": [vp, i64, f32, vp],
+    "catseg_preprocess_im2col": [vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, i64, i32, vp],
+    "catseg_vit_embed": [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp],
+    "catseg_bicubic_resize": [vp, i32, i32, vp, i32, vp],
+    "catseg_postprocess": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
+    "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
+    "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
+    "catseg_abi_version": [],
+    "catseg_last_error": [],
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libcatseg_hip.so (raises if it is missing — there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libcatseg_hip.so not found at {LIB_PATH}: build it with "
+            "`make -C cat-seg_amd/csrc` (or __graft_entry__.build()); the CAT-Seg HIP path has no fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_char_p if name == "catseg_last_error" else C.c_int
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.catseg_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def require_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("the CAT-Seg HIP path needs a visible MI355X (torch.cuda.is_available() is False)")
+    load()

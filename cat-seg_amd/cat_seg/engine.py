@@ -1,0 +1,458 @@
+"""MI355X execution engine of the CAT-Seg dense-inference path.
+
+`CatSegEngine` owns the device-resident, kernel-ready weights and drives the HIP
+kernels of libcatseg_hip.so (through `ops`) for:
+
+  * the CLIP ViT dense image encoder + hooks        (model_vpt.py:288-314, cat_seg_model.py:84-87)
+  * the CLIP text encoder / cached class embeddings (model_vpt.py:421-438, cat_seg_predictor.py:190-224)
+  * the Aggregator: cost volume, top-k, corr_embed, Swin + class-attention layers,
+    guided upsampler                                 (model.py:683-725)
+  * pre/post-processing of CATSeg.forward (eval)     (cat_seg_model.py:147-155,220-229)
+
+Layouts (device, row-major, channels-last):
+  ViT residual stream x      fp32 [B*L][width]        (L = 1 + grid^2, token-major per image)
+  cost embedding X            act  [B*T*HW][128]       (image, class, pixel) rows
+  decoder maps                act  [B*T][h][w][c]      NHWC
+  logits                      fp32 [B][T0][96][96]
+`act` is bf16 (MFMA bf16, fp32 accumulate) or fp32 (exact-f32 MFMA) — the engine dtype.
+
+Algebraic savings taken (exact in real arithmetic):
+  * guidance halves of the Swin / class-attention q,k projections are computed once
+    per image / per class and added in the GEMM epilogue;
+  * class-attention padding rows: constant K/V contributions, their own rows skipped;
+  * forward_dense: the dead q/k projections of the last ViT block are skipped;
+  * the decoder guidance concat and repeat over classes are read in place by the conv.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+from . import _lib as L
+from ._lib import rowmap
+from .arch import CatSegArch
+from .weights import AGG, CLIP
+
+_f32 = torch.float32
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class _NS(dict):
+    __getattr__ = dict.__getitem__
+
+
+class CatSegEngine:
+    def __init__(self, arch: CatSegArch, state_dict: Dict[str, torch.Tensor], dtype=torch.bfloat16,
+                 device="cuda"):
+        L.require_gpu()
+        if tuple(arch.pooling_size) != (1, 1):
+            raise NotImplementedError("HIP path: class-attention pooling != (1, 1) is not implemented yet")
+        if arch.hidden_dim != 128 or arch.nheads != 4:
+            raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
+        self.arch = arch
+        self.dt = dtype
+        self.device = torch.device(device)
+        self._text = None
+        with torch.no_grad():
+            self.w = self._prepare(state_dict)
+
+    # ------------------------------------------------------------------ weights
+    def _W(self, t):
+        return t.detach().to(self.device, self.dt).contiguous()
+
+    def _F(self, t):
+        return t.detach().to(self.device, _f32).contiguous()
+
+    def _block(self, sd, p, dense=False):
+        width = sd[p + "attn.q_proj_weight"].shape[0]
+        b = sd[p + "attn.in_proj_bias"]
+        blk = _NS(
+            ln1w=self._F(sd[p + "ln_1.weight"]), ln1b=self._F(sd[p + "ln_1.bias"]),
+            wo=self._W(sd[p + "attn.out_proj.weight"]), bo=self._F(sd[p + "attn.out_proj.bias"]),
+            ln2w=self._F(sd[p + "ln_2.weight"]), ln2b=self._F(sd[p + "ln_2.bias"]),
+            wfc=self._W(sd[p + "mlp.c_fc.weight"]), bfc=self._F(sd[p + "mlp.c_fc.bias"]),
+            wpr=self._W(sd[p + "mlp.c_proj.weight"]), bpr=self._F(sd[p + "mlp.c_proj.bias"]),
+        )
+        if dense:   # forward_dense: v path only (model_vpt.py:219-240)
+            blk["wv"] = self._W(sd[p + "attn.v_proj_weight"])
+            blk["bv"] = self._F(b[2 * width:])
+        else:
+            blk["wqkv"] = self._W(torch.cat([sd[p + f"attn.{x}_proj_weight"] for x in "qkv"], 0))
+            blk["bqkv"] = self._F(b)
+        return blk
+
+    @staticmethod
+    def _conv_w(w):      # (co, ci, 3, 3) -> [co][ky][kx][ci] flattened K
+        return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+    @staticmethod
+    def _convt_w(w, b):  # ConvTranspose2d (ci, co, k, k) -> GEMM W [(ky, kx, co)][ci], bias per n
+        ci, co, k, _ = w.shape
+        return w.permute(2, 3, 1, 0).reshape(k * k * co, ci), b.repeat(k * k)
+
+    def _prepare(self, sd):
+        a = self.arch
+        w = _NS()
+        # ---------------- CLIP visual ----------------
+        p = CLIP + "visual."
+        W = a.vision_width
+        kc = 3 * a.vision_patch ** 2
+        kp = _round_up(kc, 32)
+        pw = torch.zeros(W, kp)
+        pw[:, :kc] = sd[p + "conv1.weight"].reshape(W, kc)
+        w.patch_w, w.patch_k = self._W(pw), kp
+        w.cls = self._F(sd[p + "class_embedding"])
+        pos = self._F(sd[p + "positional_embedding"])
+        if a.grid != a.pretrain_grid:   # resized_pos_embed (model_vpt.py:316-329), on device
+            out = torch.empty(a.grid * a.grid, W, device=self.device)
+            ops.bicubic_resize(pos[1:].contiguous(), a.pretrain_grid, W, out, a.grid)
+            pos = torch.cat([pos[:1], out], 0).contiguous()
+        w.pos = pos
+        w.ln_pre = (self._F(sd[p + "ln_pre.weight"]), self._F(sd[p + "ln_pre.bias"]))
+        w.vblocks = [self._block(sd, f"{p}transformer.resblocks.{i}.", dense=(i == a.vision_layers - 1))
+                     for i in range(a.vision_layers)]
+        w.ln_post = (self._F(sd[p + "ln_post.weight"]), self._F(sd[p + "ln_post.bias"]))
+        w.proj_t = self._W(sd[p + "proj"].t())
+        # ---------------- CLIP text ----------------
+        w.tok_emb = self._F(sd[CLIP + "token_embedding.weight"])
+        w.tpos = self._F(sd[CLIP + "positional_embedding"])
+        w.tblocks = [self._block(sd, f"{CLIP}transformer.resblocks.{i}.") for i in range(a.text_layers)]
+        w.ln_final = (self._F(sd[CLIP + "ln_final.weight"]), self._F(sd[CLIP + "ln_final.bias"]))
+        w.tproj_t = self._W(sd[CLIP + "text_projection"].t())
+        # ---------------- upsamplers (cat_seg_model.py:81-82) ----------------
+        for i in (1, 2):
+            ww, bb = self._convt_w(sd[f"upsample{i}.weight"], sd[f"upsample{i}.bias"])
+            w[f"up{i}_w"], w[f"up{i}_b"] = self._W(ww), self._F(bb)
+        # ---------------- Aggregator ----------------
+        D = a.hidden_dim
+        w.ce_w = self._F(sd[AGG + "conv1.weight"].reshape(D, 49))
+        w.ce_b = self._F(sd[AGG + "conv1.bias"])
+        w.gp_w = self._W(self._conv_w(sd[AGG + "guidance_projection.0.weight"]))
+        w.gp_b = self._F(sd[AGG + "guidance_projection.0.bias"])
+        w.dgp = [(self._W(self._conv_w(sd[f"{AGG}decoder_guidance_projection.{i}.0.weight"])),
+                  self._F(sd[f"{AGG}decoder_guidance_projection.{i}.0.bias"])) for i in range(2)]
+        w.tg_w = self._W(sd[AGG + "text_guidance_projection.0.weight"])
+        w.tg_b = self._F(sd[AGG + "text_guidance_projection.0.bias"])
+        w.layers = []
+        for l in range(a.num_layers):
+            sw = f"{AGG}layers.{l}.swin_block."
+            lay = _NS(gnw=self._F(sd[sw + "guidance_norm.weight"]), gnb=self._F(sd[sw + "guidance_norm.bias"]))
+            for name in ("block_1", "block_2"):
+                q = f"{sw}{name}."
+                wq, wk = sd[q + "attn.q.weight"], sd[q + "attn.k.weight"]
+                lay[name] = _NS(
+                    n1w=self._F(sd[q + "norm1.weight"]), n1b=self._F(sd[q + "norm1.bias"]),
+                    wqkv=self._W(torch.cat([wq[:, :D], wk[:, :D], sd[q + "attn.v.weight"]], 0)),
+                    bqkv=self._F(torch.cat([sd[q + "attn.q.bias"], sd[q + "attn.k.bias"], sd[q + "attn.v.bias"]])),
+                    wqk_g=self._W(torch.cat([wq[:, D:], wk[:, D:]], 0)),
+                    wproj=self._W(sd[q + "attn.proj.weight"]), bproj=self._F(sd[q + "attn.proj.bias"]),
+                    n2w=self._F(sd[q + "norm2.weight"]), n2b=self._F(sd[q + "norm2.bias"]),
+                    wfc1=self._W(sd[q + "mlp.fc1.weight"]), bfc1=self._F(sd[q + "mlp.fc1.bias"]),
+                    wfc2=self._W(sd[q + "mlp.fc2.weight"]), bfc2=self._F(sd[q + "mlp.fc2.bias"]),
+                )
+            c = f"{AGG}layers.{l}.attention."
+            wq, wk = sd[c + "attention.q.weight"], sd[c + "attention.k.weight"]
+            ca = _NS(
+                n1w=self._F(sd[c + "norm1.weight"]), n1b=self._F(sd[c + "norm1.bias"]),
+                wqkv=self._W(torch.cat([wq[:, :D], wk[:, :D], sd[c + "attention.v.weight"]], 0)),
+                bqkv=self._F(torch.cat([sd[c + "attention.q.bias"], sd[c + "attention.k.bias"],
+                                        sd[c + "attention.v.bias"]])),
+                wqk_t=self._W(torch.cat([wq[:, D:], wk[:, D:]], 0)),
+                n2w=self._F(sd[c + "norm2.weight"]), n2b=self._F(sd[c + "norm2.bias"]),
+                w0=self._W(sd[c + "MLP.0.weight"]), b0=self._F(sd[c + "MLP.0.bias"]),
+                w2=self._W(sd[c + "MLP.2.weight"]), b2=self._F(sd[c + "MLP.2.bias"]),
+            )
+            if a.pad_len > 0:
+                ca["kpad"], ca["vpad"] = self._pad_kv(ca, sd[c + "padding_tokens"].reshape(1, D),
+                                                      sd[c + "padding_guidance"].reshape(1, -1))
+            lay["ca"] = ca
+            w.layers.append(lay)
+        w.dec = []
+        for i in (1, 2):
+            q = f"{AGG}decoder{i}."
+            ww, bb = self._convt_w(sd[q + "up.weight"], sd[q + "up.bias"])
+            w.dec.append(_NS(
+                up_w=self._W(ww), up_b=self._F(bb), up_c=sd[q + "up.weight"].shape[1],
+                c0=self._W(self._conv_w(sd[q + "conv.double_conv.0.weight"])),
+                g0=(self._F(sd[q + "conv.double_conv.1.weight"]), self._F(sd[q + "conv.double_conv.1.bias"])),
+                c3=self._W(self._conv_w(sd[q + "conv.double_conv.3.weight"])),
+                g3=(self._F(sd[q + "conv.double_conv.4.weight"]), self._F(sd[q + "conv.double_conv.4.bias"])),
+            ))
+        hw = sd[AGG + "head.weight"]            # (1, C, 3, 3) -> [ky][kx][c]
+        w.head_w = self._F(hw[0].permute(1, 2, 0).reshape(-1))
+        w.head_b = float(sd[AGG + "head.bias"].reshape(-1)[0])
+        return w
+
+    def _pad_kv(self, ca, pad_tok, pad_guid):
+        """Constant K/V projections of the learned class padding (model.py:397-410)."""
+        dev, D = self.device, self.arch.hidden_dim
+        x = pad_tok.to(dev, _f32).contiguous()
+        h = torch.empty(1, D, device=dev, dtype=self.dt)
+        ops.layernorm(x, ca.n1w, ca.n1b, h)
+        g = pad_guid.to(dev, self.dt).contiguous()
+        tg = torch.empty(1, 2 * D, device=dev, dtype=_f32)
+        ops.gemm(g, ca.wqk_t, tg)
+        qkv = torch.empty(1, 3 * D, device=dev, dtype=_f32)
+        ops.gemm(h, ca.wqkv, qkv, bias=ca.bqkv, add=tg, add_ncols=2 * D)
+        return qkv[0, D:2 * D].contiguous(), qkv[0, 2 * D:].contiguous()
+
+    # ------------------------------------------------------------------ shared transformer block
+    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None):
+        """ResidualAttentionBlock.forward over a stack (model_vpt.py:208-217, 256-266)."""
+        M, width = x.shape
+        dt, dev = self.dt, self.device
+        h = torch.empty(M, width, device=dev, dtype=dt)
+        qkv = torch.empty(M, 3 * width, device=dev, dtype=dt)
+        o = torch.empty(M, width, device=dev, dtype=dt)
+        u = torch.empty(M, 4 * width, device=dev, dtype=dt)
+        fresh = False
+        for i, blk in enumerate(blocks):
+            ops.layernorm(x, blk.ln1w, blk.ln1b, h)
+            ops.gemm(h, blk.wqkv, qkv, bias=blk.bqkv)
+            ops.attention(qkv[:, :width], qkv[:, width:2 * width], qkv[:, 2 * width:], o,
+                          n_seq=n_seq, seq_len=seq_len, n_heads=n_heads, head_dim=width // n_heads,
+                          scale=(width // n_heads) ** -0.5, causal=causal)
+            x_new = torch.empty_like(x) if fresh else x
+            ops.gemm(o, blk.wo, x_new, bias=blk.bo, res=x)
+            x = x_new
+            ops.layernorm(x, blk.ln2w, blk.ln2b, h)
+            ops.gemm(h, blk.wfc, u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+            ops.gemm(u, blk.wpr, x, bias=blk.bpr, res=x)
+            fresh = i in hooks_at
+            if fresh:
+                hooks.append(x)
+        return x
+
+    # ------------------------------------------------------------------ text
+    def encode_text(self, tokens: torch.Tensor) -> torch.Tensor:
+        """CLIP.encode_text + L2 norm (cat_seg_predictor.py:214-216).  tokens (T, ctx) int."""
+        a, dev = self.arch, self.device
+        tokens = tokens.to(dev, torch.int32).contiguous()
+        n, ctx = tokens.shape
+        TW = a.text_width
+        x = torch.empty(n * ctx, TW, device=dev, dtype=_f32)
+        ops.token_embed(tokens, self.w.tok_emb, self.w.tpos[:ctx].contiguous(), x)
+        x = self._resblocks(x, self.w.tblocks, n, ctx, a.text_heads, causal=True)
+        e = torch.empty(n, TW, device=dev, dtype=_f32)
+        ops.eot_gather(x, tokens, e)
+        h = torch.empty(n, TW, device=dev, dtype=self.dt)
+        ops.layernorm(e, *self.w.ln_final, h)
+        t = torch.empty(n, a.embed_dim, device=dev, dtype=_f32)
+        ops.gemm(h, self.w.tproj_t, t)
+        out = torch.empty_like(t)
+        ops.l2normalize(t, out)
+        return out
+
+    def set_text(self, text: torch.Tensor):
+        """Cache the per-class-set terms (the predictor's eval cache, cat_seg_predictor.py:191-192,221-222).
+        text: (T, C_o) or (T, 1, C_o) L2-normalized class embeddings."""
+        dev, dt, D = self.device, self.dt, self.arch.hidden_dim
+        t = text.reshape(text.shape[0], -1).to(dev, _f32).contiguous()
+        T = t.shape[0]
+        txn = torch.empty(T, t.shape[1], device=dev, dtype=dt)
+        ops.l2normalize(t, txn)                           # correlation's F.normalize (model.py:650)
+        tg = torch.empty(T, D, device=dev, dtype=dt)       # text_guidance_projection (model.py:712-715)
+        ops.gemm(txn, self.w.tg_w, tg, bias=self.w.tg_b, act=L.ACT_RELU)
+        tgqk = []
+        for lay in self.w.layers:
+            o = torch.empty(T, 2 * D, device=dev, dtype=dt)
+            ops.gemm(tg, lay.ca.wqk_t, o)
+            tgqk.append(o)
+        self._text = _NS(T=T, txn=txn, tgqk=tgqk, src=text)
+
+    # ------------------------------------------------------------------ image encoder
+    def encode_image(self, raw: torch.Tensor, sizes: torch.Tensor):
+        """Pre-processing + CLIP dense encoder + hooks.  raw (B,3,Hp,Wp) fp32 0-255 on device,
+        sizes (B,2) int32 valid (h, w).  Returns feats fp32 (B*L, C_o), [hook0, hook1] fp32 (B*L, W)."""
+        a, dev, dt, w = self.arch, self.device, self.dt, self.w
+        B = raw.shape[0]
+        G2 = a.grid * a.grid
+        Lt = G2 + 1
+        W = a.vision_width
+        cols = torch.empty(B * G2, w.patch_k, device=dev, dtype=dt)
+        mean = torch.tensor(a.clip_pixel_mean, device=dev, dtype=_f32)
+        std = torch.tensor(a.clip_pixel_std, device=dev, dtype=_f32)
+        ops.preprocess_im2col(raw, sizes, mean=mean, std=std, res=a.clip_resolution, patch=a.vision_patch, out=cols)
+        patches = torch.empty(B * G2, W, device=dev, dtype=_f32)
+        ops.gemm(cols, w.patch_w, patches)
+        x = torch.empty(B * Lt, W, device=dev, dtype=_f32)
+        ops.vit_embed(patches, w.cls, w.pos, *w.ln_pre, x, B=B, G2=G2, width=W)
+        hooks: List[torch.Tensor] = []
+        x = self._resblocks(x, w.vblocks[:-1], B, Lt, a.vision_heads, False,
+                            hooks_at=set(a.hook_layers), hooks=hooks)
+        if a.vision_layers - 1 in a.hook_layers:
+            raise NotImplementedError("hook on the dense block")
+        # forward_dense (model_vpt.py:219-240)
+        blk = w.vblocks[-1]
+        M = B * Lt
+        h = torch.empty(M, W, device=dev, dtype=dt)
+        ops.layernorm(x, blk.ln1w, blk.ln1b, h)
+        v = torch.empty(M, W, device=dev, dtype=dt)
+        ops.gemm(h, blk.wv, v, bias=blk.bv)
+        vo = torch.empty(M, W, device=dev, dtype=_f32)
+        ops.gemm(v, blk.wo, vo, bias=blk.bo, add=x, addmap=rowmap(d1=Lt, s1=Lt))   # + x[:1] (CLS residual)
+        ops.layernorm(vo, blk.ln2w, blk.ln2b, h)
+        u = torch.empty(M, 4 * W, device=dev, dtype=dt)
+        ops.gemm(h, blk.wfc, u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+        ops.gemm(u, blk.wpr, vo, bias=blk.bpr, res=vo)
+        ops.layernorm(vo, *w.ln_post, h)                                        # ln_post (all tokens)
+        feats = torch.empty(M, a.embed_dim, device=dev, dtype=_f32)
+        ops.gemm(h, w.proj_t, feats)                                           # @ proj
+        return feats, hooks
+
+    # ------------------------------------------------------------------ head
+    def head_logits(self, raw: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+        """cat_seg_model.py:155-188 -> Aggregator.forward (model.py:683-725).
+        Returns fp32 logits (B, T0, 4*grid, 4*grid)."""
+        if self._text is None:
+            raise RuntimeError("set_text() / encode_text() must run before the image forward")
+        a, dev, dt, w, tx = self.arch, self.device, self.dt, self.w, self._text
+        B = raw.shape[0]
+        G = a.grid
+        HW = G * G
+        Lt = HW + 1
+        D = a.hidden_dim
+        Co = a.embed_dim
+        feats, hooks = self.encode_image(raw, sizes)
+        drop_cls = rowmap(d1=HW, s1=Lt, d2=1, m2=HW, s2=1, off=1)
+        # ---- guidance sources (cat_seg_model.py:178-186) ----
+        res3 = torch.empty(B * HW, Co, device=dev, dtype=dt)
+        ops.convert(feats, res3, inmap=drop_cls)
+        res45 = []
+        for i, (k, cout) in enumerate(((2, a.decoder_guidance_dims[0]), (4, a.decoder_guidance_dims[1]))):
+            hk = torch.empty(B * HW, a.vision_width, device=dev, dtype=dt)
+            ops.convert(hooks[i], hk, inmap=drop_cls)
+            r = torch.empty(B * HW * k * k, cout, device=dev, dtype=dt)
+            ops.gemm(hk, w[f"up{i + 1}_w"], r, bias=w[f"up{i + 1}_b"], store=(k, G, G, cout))
+            res45.append(r)
+        # ---- cost volume (model.py:648-652) ----
+        fn = torch.empty(B * HW, Co, device=dev, dtype=dt)
+        ops.l2normalize(feats, fn, inmap=drop_cls)
+        T0 = tx.T
+        corr = torch.empty(T0, B * HW, device=dev, dtype=_f32)
+        ops.gemm(tx.txn, fn, corr)                         # corr[t][b*HW + p]
+        classes = None
+        T = T0
+        if a.pad_len > 0 and T0 > a.pad_len:               # top-k truncation (model.py:694-702)
+            T = a.pad_len
+            classes = torch.empty(B, T, device=dev, dtype=torch.int32)
+            ops.topk_classes(corr, t_stride=B * HW, b_stride=HW, B=B, T=T0, HW=HW, k=T, out=classes)
+        S = B * T
+        R = S * HW
+        X = torch.empty(R, D, device=dev, dtype=dt)
+        ops.corr_embed(corr, t_stride=B * HW, b_stride=HW, B=B, T=T, H=G, W=G, weight=w.ce_w, bias=w.ce_b,
+                       out=X, classes=classes)
+        # ---- guidance projections (model.py:706-711) ----
+        G3 = torch.empty(B * HW, a.appearance_guidance_proj_dim, device=dev, dtype=dt)
+        ops.conv3x3(res3, w.gp_w, G3, S=B, H=G, W=G, c1=Co, bias=w.gp_b, act=L.ACT_RELU)
+        GD = []
+        for i, (src, cin) in enumerate(zip(res45, a.decoder_guidance_dims)):
+            k = 2 ** (i + 1)
+            g = torch.empty(B * HW * k * k, a.decoder_guidance_proj_dims[i], device=dev, dtype=dt)
+            ops.conv3x3(src, w.dgp[i][0], g, S=B, H=G * k, W=G * k, c1=cin, bias=w.dgp[i][1], act=L.ACT_RELU)
+            GD.append(g)
+        # ---- text guidance terms per class (gathered per image after top-k) ----
+        if classes is not None:
+            tgqk = []
+            idx = classes.reshape(-1).contiguous()
+            for t in tx.tgqk:
+                o = torch.empty(S, 2 * D, device=dev, dtype=dt)
+                ops.gather_rows(t, idx, o)
+                tgqk.append(o)
+            tmap = rowmap(d1=HW)
+        else:
+            tgqk = tx.tgqk
+            tmap = rowmap(d1=HW, m1=T)
+        # ---- aggregation layers (model.py:717-718) ----
+        h = torch.empty(R, D, device=dev, dtype=dt)
+        qkv = torch.empty(R, 3 * D, device=dev, dtype=dt)
+        o = torch.empty(R, D, device=dev, dtype=dt)
+        hid = torch.empty(R, 4 * D, device=dev, dtype=dt)
+        Y = torch.empty(R, D, device=dev, dtype=dt)
+        gn = torch.empty(B * HW, D, device=dev, dtype=dt)
+        gqk = torch.empty(B * HW, 2 * D, device=dev, dtype=dt)
+        ws = a.window_size
+        H_, W_ = a.feature_resolution
+        shift2 = ws // 2
+        if min(H_, W_) <= ws:   # model.py:146-149
+            ws, shift2 = min(H_, W_), 0
+        nwin = (H_ // ws) * (W_ // ws)
+        gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)     # (b, t, p) -> (b, p)
+        n_pad = a.pad_len - T if a.pad_len > 0 and T < a.pad_len else 0
+        for l, lay in enumerate(w.layers):
+            ops.layernorm(G3, lay.gnw, lay.gnb, gn)           # guidance_norm, once per image
+            for name, shift in (("block_1", 0), ("block_2", shift2)):
+                blk = lay[name]
+                ops.gemm(gn, blk.wqk_g, gqk)                   # W_g . LN(g): per image
+                ops.layernorm(X, blk.n1w, blk.n1b, h)
+                ops.gemm(h, blk.wqkv, qkv, bias=blk.bqkv, add=gqk, addmap=gmap, add_ncols=2 * D)
+                ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, n_seq=S * nwin, seq_len=ws * ws,
+                              n_heads=a.nheads, head_dim=D // a.nheads, scale=(D // a.nheads) ** -0.5, mode=1,
+                              img_hw=(H_, W_), window=ws, shift=shift)
+                ops.gemm(o, blk.wproj, X, bias=blk.bproj, res=X)
+                ops.layernorm(X, blk.n2w, blk.n2b, h)
+                ops.gemm(h, blk.wfc1, hid, bias=blk.bfc1, act=L.ACT_GELU)
+                ops.gemm(hid, blk.wfc2, X, bias=blk.bfc2, res=X)
+            ca = lay.ca
+            ops.layernorm(X, ca.n1w, ca.n1b, h)
+            ops.gemm(h, ca.wqkv, qkv, bias=ca.bqkv, add=tgqk[l], addmap=tmap, add_ncols=2 * D)
+            ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
+                                 n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                                 k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+            ops.layernorm(Y, ca.n2w, ca.n2b, h)
+            ops.gemm(h, ca.w0, hid, bias=ca.b0, act=L.ACT_RELU)
+            ops.gemm(hid, ca.w2, X, bias=ca.b2, res=Y, res2=X)   # x + (x_pool + MLP) (model.py:413,423)
+        del h, qkv, o, hid, Y, gn, gqk
+        # ---- guided upsampler (model.py:674-681, 540-555) ----
+        src, Hc = X, G
+        tile = ops.conv_tile_rows()
+        for i, dec in enumerate(w.dec):
+            cu = dec.up_c
+            Ho = Hc * 2
+            up = torch.empty(S * Ho * Ho, cu, device=dev, dtype=dt)
+            ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+            cout = dec.c0.shape[0]
+            groups = cout // 16
+            tiles = Ho * Ho // tile
+            c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
+            st = torch.empty(S * tiles * groups * 2, device=dev, dtype=_f32)
+            gd = GD[i]
+            ops.conv3x3(up, dec.c0, c1, S=S, H=Ho, W=Ho, c1=cu, src2=gd, c2=gd.shape[1], src2_div=T, stats=st)
+            m1 = torch.empty(S * groups, device=dev, dtype=_f32)
+            r1 = torch.empty_like(m1)
+            ops.groupnorm_stats(st, S, tiles, groups, tile * 16, m1, r1)
+            c2 = torch.empty_like(c1)
+            ops.conv3x3(c1, dec.c3, c2, S=S, H=Ho, W=Ho, c1=cout, gn=(m1, r1, *dec.g0, 16), stats=st)
+            m2 = torch.empty_like(m1)
+            r2 = torch.empty_like(m1)
+            ops.groupnorm_stats(st, S, tiles, groups, tile * 16, m2, r2)
+            if i == 0:
+                z = torch.empty_like(c2)
+                ops.groupnorm_relu(c2, z, S=S, HW=Ho * Ho, C=cout, cpg=16, mean=m2, rstd=r2,
+                                   gamma=dec.g3[0], beta=dec.g3[1])
+                src, Hc = z, Ho
+            else:
+                logits = torch.empty(B, T0, Ho, Ho, device=dev, dtype=_f32)
+                if classes is not None:
+                    ops.fill(logits, -100.0)
+                ops.conv3x3_head(c2, B=B, T=T, H=Ho, W=Ho, C=cout, weight=w.head_w, bias=w.head_b, out=logits,
+                                 T_out=T0, classes=classes, gn=(m2, r2, *dec.g3, 16))
+        return logits
+
+    # ------------------------------------------------------------------ full eval forward
+    def forward(self, raw: torch.Tensor, sizes: torch.Tensor, out_hw) -> torch.Tensor:
+        """Sigmoid probabilities upsampled to out_hw for every image (cat_seg_model.py:220-229)."""
+        logits = self.head_logits(raw, sizes)
+        B, T0, h, w = logits.shape
+        H, W = out_hw
+        out = torch.empty(B, T0, H, W, device=self.device, dtype=_f32)
+        ih, iw = [int(v) for v in sizes[0].tolist()] if sizes.is_cpu else (h, w)
+        ops.postprocess(logits, out, crop=(min(h, ih), min(w, iw)))
+        return out

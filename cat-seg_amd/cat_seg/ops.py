@@ -1,0 +1,232 @@
+"""Python mirror of the C ABI (include/catseg_hip.h): one thin wrapper per entry point.
+
+Every wrapper takes device tensors, derives pointers / strides / dtypes, launches on
+`torch.cuda.current_stream()` and raises RuntimeError on a non-zero status.  No
+wrapper has a fallback: a missing library or device raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import call, rowmap, IDENTITY
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return L.F32
+    if t.dtype == torch.bfloat16:
+        return L.BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld(t: torch.Tensor) -> int:
+    assert t.dim() >= 2 and t.stride(-1) == 1, "row-major rows expected"
+    return t.stride(-2)
+
+
+def gemm(A, W, out, *, M=None, K=None, bias=None, act=L.ACT_NONE, alpha=1.0,
+         add=None, addmap=None, add_ncols=None, res=None, res2=None, amap=None,
+         lda=None, ldo=None, store=None):
+    """out = act(A[amap(m)] . W^T + bias + add) * alpha + res + res2   (catseg_gemm)."""
+    N = W.shape[0]
+    K = K if K is not None else W.shape[1]
+    M = M if M is not None else A.shape[0]
+    a = L.GemmArgs()
+    a.A, a.lda, a.amap = A.data_ptr(), lda if lda is not None else _ld(A), amap or IDENTITY
+    a.W, a.ldw = W.data_ptr(), _ld(W)
+    a.M, a.N, a.K = M, N, K
+    a.bias = _p(bias)
+    if add is not None:
+        a.add, a.ld_add = add.data_ptr(), _ld(add)
+        a.addmap = addmap or IDENTITY
+        a.add_ncols = add_ncols if add_ncols is not None else N
+    else:
+        a.addmap = IDENTITY
+    a.act, a.alpha = act, alpha
+    if res is not None:
+        a.res, a.ld_res = res.data_ptr(), _ld(res)
+    if res2 is not None:
+        a.res2, a.ld_res2 = res2.data_ptr(), _ld(res2)
+    a.out = out.data_ptr()
+    a.ldo = ldo if ldo is not None else (_ld(out) if store is None else 0)
+    if store is not None:
+        a.store_mode = 1
+        a.cvt_k, a.cvt_hin, a.cvt_win, a.cvt_cout = store
+    a.dtype_a, a.dtype_out = _dt(A), _dt(out)
+    call("catseg_gemm", a, _stream())
+    return out
+
+
+def layernorm(x, gamma, beta, out, *, rows=None, inmap=None, eps=1e-5, cols=None):
+    cols = cols if cols is not None else gamma.shape[0]
+    rows = rows if rows is not None else out.shape[0]
+    call("catseg_layernorm", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
+         gamma.data_ptr(), beta.data_ptr(), rows, cols, eps, _stream())
+    return out
+
+
+def l2normalize(x, out, *, rows=None, cols=None, inmap=None, eps=1e-12):
+    cols = cols if cols is not None else out.shape[-1]
+    rows = rows if rows is not None else out.shape[0]
+    call("catseg_l2normalize", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
+         rows, cols, eps, _stream())
+    return out
+
+
+def convert(x, out, *, rows=None, cols=None, inmap=None):
+    cols = cols if cols is not None else out.shape[-1]
+    rows = rows if rows is not None else out.shape[0]
+    call("catseg_convert", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
+         rows, cols, _stream())
+    return out
+
+
+def attention(q, k, v, out, *, n_seq, seq_len, n_heads, head_dim, scale, causal=False,
+              mode=0, img_hw=(0, 0), window=0, shift=0):
+    a = L.AttnArgs()
+    a.q, a.k, a.v, a.ld_qkv = q.data_ptr(), k.data_ptr(), v.data_ptr(), _ld(q)
+    assert _ld(k) == a.ld_qkv and _ld(v) == a.ld_qkv
+    a.out, a.ld_out = out.data_ptr(), _ld(out)
+    a.n_seq, a.seq_len, a.n_heads, a.head_dim = n_seq, seq_len, n_heads, head_dim
+    a.scale, a.causal = scale, int(causal)
+    a.mode, a.img_h, a.img_w, a.window, a.shift = mode, img_hw[0], img_hw[1], window, shift
+    a.dtype = _dt(q)
+    call("catseg_attention", a, _stream())
+    return out
+
+
+def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_pad=None, v_pad=None, eps=1e-6):
+    a = L.LinAttnArgs()
+    a.q, a.k, a.v, a.ld_qkv = q.data_ptr(), k.data_ptr(), v.data_ptr(), _ld(q)
+    a.x, a.y, a.ld_xy = x.data_ptr(), y.data_ptr(), _ld(x)
+    assert _ld(y) == a.ld_xy
+    a.B, a.T, a.HW, a.n_heads, a.head_dim = B, T, HW, n_heads, head_dim
+    a.n_pad, a.k_pad, a.v_pad, a.eps = n_pad, _p(k_pad), _p(v_pad), eps
+    a.dtype = _dt(q)
+    call("catseg_linear_attention", a, _stream())
+    return y
+
+
+def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0,
+            src2=None, c2=0, s2_slice_stride=0, s2_offset=0, src2_div=1,
+            bias=None, act=L.ACT_NONE, gn=None, stats=None, stats_cpg=16):
+    a = L.ConvArgs()
+    a.src1, a.s1_slice_stride, a.s1_offset, a.c1 = (src1.data_ptr(),
+                                                   s1_slice_stride if s1_slice_stride is not None else H * W * c1,
+                                                   s1_offset, c1)
+    if src2 is not None:
+        a.src2, a.s2_slice_stride, a.s2_offset, a.c2, a.src2_div = (src2.data_ptr(), s2_slice_stride or H * W * c2,
+                                                                   s2_offset, c2, src2_div)
+    else:
+        a.src2_div = 1
+    a.S, a.H, a.W = S, H, W
+    a.weight, a.c_out = weight.data_ptr(), weight.shape[0]
+    a.bias, a.act = _p(bias), act
+    if gn is not None:
+        mean, rstd, gamma, beta, cpg = gn
+        a.gn_mean, a.gn_rstd, a.gn_gamma, a.gn_beta, a.gn_cpg = (mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+                                                                 beta.data_ptr(), cpg)
+    a.out = out.data_ptr()
+    a.stats, a.stats_cpg = _p(stats), stats_cpg
+    a.dtype = _dt(out)
+    call("catseg_conv3x3", a, _stream())
+    return out
+
+
+def conv_tile_rows() -> int:
+    return L.load().catseg_conv_tile_rows()
+
+
+def groupnorm_stats(partials, S, tiles, groups, tile_count, mean, rstd, eps=1e-5):
+    call("catseg_groupnorm_stats", partials.data_ptr(), S, tiles, groups, tile_count, eps, mean.data_ptr(),
+         rstd.data_ptr(), _stream())
+
+
+def groupnorm_relu(x, y, *, S, HW, C, cpg, mean, rstd, gamma, beta):
+    call("catseg_groupnorm_relu", x.data_ptr(), y.data_ptr(), S, HW, C, cpg, mean.data_ptr(), rstd.data_ptr(),
+         gamma.data_ptr(), beta.data_ptr(), _dt(x), _stream())
+    return y
+
+
+def conv3x3_head(x, *, B, T, H, W, C, weight, bias, out, T_out, classes=None, gn=None):
+    if gn is None:
+        call("catseg_conv3x3_head", x.data_ptr(), B, T, H, W, C, weight.data_ptr(), bias, _p(classes), T_out,
+             out.data_ptr(), _dt(x), _stream())
+    else:
+        mean, rstd, gamma, beta, cpg = gn
+        call("catseg_conv3x3_head_gn", x.data_ptr(), B, T, H, W, C, weight.data_ptr(), bias, mean.data_ptr(),
+             rstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), cpg, _p(classes), T_out, out.data_ptr(), _dt(x),
+             _stream())
+    return out
+
+
+def corr_embed(corr, *, t_stride, b_stride, B, T, H, W, weight, bias, out, classes=None):
+    call("catseg_corr_embed", corr.data_ptr(), t_stride, b_stride, _p(classes), B, T, H, W, weight.data_ptr(),
+         bias.data_ptr(), weight.shape[0], out.data_ptr(), _dt(out), _stream())
+    return out
+
+
+def topk_classes(corr, *, t_stride, b_stride, B, T, HW, k, out):
+    call("catseg_topk_classes", corr.data_ptr(), t_stride, b_stride, B, T, HW, k, out.data_ptr(), _stream())
+    return out
+
+
+def gather_rows(x, idx, out):
+    call("catseg_gather_rows", x.data_ptr(), _ld(x), idx.data_ptr(), idx.numel(), out.shape[-1], out.data_ptr(),
+         _ld(out), _dt(x), _stream())
+    return out
+
+
+def fill(out, value):
+    call("catseg_fill_f32", out.data_ptr(), out.numel(), value, _stream())
+    return out
+
+
+def preprocess_im2col(raw, sizes, *, mean, std, res, patch, out):
+    B, _, Hp, Wp = raw.shape
+    call("catseg_preprocess_im2col", raw.data_ptr(), sizes.data_ptr(), B, Hp, Wp, mean.data_ptr(), std.data_ptr(),
+         res, patch, out.data_ptr(), _ld(out), _dt(out), _stream())
+    return out
+
+
+def vit_embed(patches, cls, pos, gamma, beta, out, *, B, G2, width):
+    call("catseg_vit_embed", patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         B, G2, width, out.data_ptr(), _stream())
+    return out
+
+
+def bicubic_resize(grid, S_in, D, out, S_out):
+    call("catseg_bicubic_resize", grid.data_ptr(), S_in, D, out.data_ptr(), S_out, _stream())
+    return out
+
+
+def postprocess(logits, out, *, crop=None):
+    B, T, h, w = logits.shape
+    H, W = out.shape[-2:]
+    ch, cw = crop if crop is not None else (h, w)
+    call("catseg_postprocess", logits.data_ptr(), B, T, h, w, ch, cw, out.data_ptr(), H, W, _stream())
+    return out
+
+
+def token_embed(tokens, tok_emb, pos, out):
+    n, ctx = tokens.shape
+    call("catseg_token_embed", tokens.data_ptr(), n, ctx, tok_emb.data_ptr(), pos.data_ptr(), tok_emb.shape[1],
+         out.data_ptr(), _stream())
+    return out
+
+
+def eot_gather(x, tokens, out):
+    n, ctx = tokens.shape
+    call("catseg_eot_gather", x.data_ptr(), tokens.data_ptr(), n, ctx, out.shape[-1], out.data_ptr(), _stream())
+    return out

@@ -1,0 +1,257 @@
+// Flash-style softmax attention for gfx950 (MFMA, online softmax, LDS-staged K/V).
+//
+// One workgroup = NW waves = 16*NW queries of one (sequence, head).  Each wave owns
+// 16 queries and computes S^T = K . Q^T per 16-key tile, so the 16x16 C/D layout puts
+// ONE query per lane column (col = lane & 15) and 4 keys per register group
+// (row = 4*(lane>>4) + r): the per-query max / sum need only the two xor-16/32
+// shuffles, and the exponentiated tile is already the B operand of O^T = V^T . P^T
+// (k order permuted inside each 32-key step; V^T is read from LDS in the same
+// permuted order — cdna_hip_programming.md §3 "An accumulator tile as the next
+// MFMA's operand").  K tiles are stored [key][d], V tiles transposed [d][key].
+//
+// mode 0: dense sequences (CLIP ViT MHA, model_vpt.py:202-206; causal text encoder,
+//         model_vpt.py:400-406).
+// mode 1: Swin windows with cyclic shift + -100 region mask (model.py:86-114,
+//         161-216); the roll/partition/reverse are folded into the row index.
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int KB = 64;   // keys per LDS block
+
+struct AttnP {
+  const void* q; const void* k; const void* v; int64_t ld;
+  void* out; int64_t ldo;
+  int64_t n_seq; int L; int H; float scale; int causal;
+  int mode; int img_h, img_w, ws, shift;
+};
+
+DEV int64_t seq_row(const AttnP& p, int64_t s, int i) {
+  if (p.mode == 0) return s * p.L + i;
+  const int nwx = p.img_w / p.ws, nwin = (p.img_h / p.ws) * nwx;
+  const int64_t slice = s / nwin;
+  const int w = (int)(s % nwin);
+  const int Y = (w / nwx) * p.ws + i / p.ws, X = (w % nwx) * p.ws + i % p.ws;
+  const int y = (Y + p.shift) % p.img_h, x = (X + p.shift) % p.img_w;
+  return slice * (int64_t)p.img_h * p.img_w + (int64_t)y * p.img_w + x;
+}
+
+DEV int swin_region(const AttnP& p, int s_local_w, int i) {
+  const int nwx = p.img_w / p.ws;
+  const int Y = (s_local_w / nwx) * p.ws + i / p.ws, X = (s_local_w % nwx) * p.ws + i % p.ws;
+  const int hb = Y < p.img_h - p.ws ? 0 : (Y < p.img_h - p.shift ? 1 : 2);
+  const int wb = X < p.img_w - p.ws ? 0 : (X < p.img_w - p.shift ? 1 : 2);
+  return hb * 3 + wb;
+}
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
+  constexpr int NT = NW * 64;
+  constexpr int VN = Vec16<T>::N;
+  constexpr int KP = D + (sizeof(T) == 2 ? 8 : 4);     // K row stride (elements)
+  constexpr int VP = KB + 4;                            // V^T row stride
+  constexpr int DT = D / 16;                            // d tiles of O^T
+  __shared__ __attribute__((aligned(16))) T Ks[KB * KP];
+  __shared__ __attribute__((aligned(16))) T Vt[D * VP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t s = blockIdx.y / p.H;
+  const int h = blockIdx.y % p.H;
+  const int q0 = blockIdx.x * 16 * NW + wave * 16;
+  const int qi = q0 + (lane & 15);            // this lane's query (column)
+  const int g = lane >> 4;
+  const bool q_ok = qi < p.L;
+  const int64_t qrow = seq_row(p, s, q_ok ? qi : 0);
+  const T* Q = reinterpret_cast<const T*>(p.q) + qrow * p.ld + h * D;
+  const T* Kg = reinterpret_cast<const T*>(p.k);
+  const T* Vg = reinterpret_cast<const T*>(p.v);
+  const int nwin = p.mode == 1 ? (p.img_h / p.ws) * (p.img_w / p.ws) : 1;
+  const int wloc = p.mode == 1 ? (int)(s % nwin) : 0;
+  const bool swmask = p.mode == 1 && p.shift > 0;
+  const int qreg = swmask ? swin_region(p, wloc, q_ok ? qi : 0) : 0;
+
+  // Q fragments (B operand of S^T = K Q^T)
+  constexpr int QF = sizeof(T) == 2 ? D / 32 : D / 4;
+  typename std::conditional<sizeof(T) == 2, s16x8, float>::type qf[QF];
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int ks = 0; ks < QF; ++ks) {
+      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < QF; ++ks) qf[ks] = q_ok ? to_f<T>(Q[4 * ks + g]) : 0.f;
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+  const float sl2 = p.scale * 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
+
+  const int nblk = (p.L + KB - 1) / KB;
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int k0 = blk * KB;
+    // ---- stage K [key][d] and V^T [d][key] ----
+    constexpr int CPK = D / VN;
+    for (int c = tid; c < KB * CPK; c += NT) {
+      const int kk = c / CPK, d0 = (c % CPK) * VN;
+      const int key = k0 + kk;
+      uint4 ku = make_uint4(0, 0, 0, 0), vu = make_uint4(0, 0, 0, 0);
+      if (key < p.L) {
+        const int64_t r = seq_row(p, s, key);
+        ku = ld16(Kg + r * p.ld + h * D + d0);
+        vu = ld16(Vg + r * p.ld + h * D + d0);
+      }
+      st16(&Ks[kk * KP + d0], ku);
+      const T* ve = reinterpret_cast<const T*>(&vu);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
+    }
+    __syncthreads();
+
+    // ---- S^T tiles ----
+    f32x4 st[KB / 16];
+#pragma unroll
+    for (int kt = 0; kt < KB / 16; ++kt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      const int kr = kt * 16 + (lane & 15);
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int ks = 0; ks < QF; ++ks) {
+          s16x8 kf = *reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]);
+          a = mfma_bf16(kf, qf[ks], a);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < QF; ++ks) a = mfma_f32(to_f<T>(Ks[kr * KP + 4 * ks + g]), qf[ks], a);
+      }
+      st[kt] = a;
+    }
+    // ---- mask + online softmax (per query column) ----
+    float bmax = -1e30f;
+#pragma unroll
+    for (int kt = 0; kt < KB / 16; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + kt * 16 + 4 * g + r;
+        float x = st[kt][r] * sl2;
+        if (key >= p.L || (p.causal && key > qi)) x = -INFINITY;
+        else if (swmask && swin_region(p, wloc, key) != qreg) x += -100.f * 1.4426950408889634f;
+        st[kt][r] = x;
+        bmax = fmaxf(bmax, x);
+      }
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float m_new = fmaxf(m_run, bmax);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KB / 16; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(st[kt][r] - m_new);
+        st[kt][r] = e;
+        psum += e;
+      }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < DT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[i][r] *= alpha;
+
+    // ---- O^T += V^T . P^T ----
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int u = 0; u < KB / 32; ++u) {
+        s16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (short)f2bf(st[2 * u][j]);
+          pb[4 + j] = (short)f2bf(st[2 * u + 1][j]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const T* vr = &Vt[(dt * 16 + (lane & 15)) * VP + 32 * u + 4 * g];
+          uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < KB / 16; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const float va = to_f<T>(Vt[(dt * 16 + (lane & 15)) * VP + kt * 16 + 4 * g + r]);
+            o[dt] = mfma_f32(va, st[kt][r], o[dt]);
+          }
+    }
+    __syncthreads();
+  }
+
+  // ---- normalize + store: lane holds O^T[d = dt*16 + 4g + r][q] ----
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (!q_ok) return;
+  const float inv = 1.f / l_run;
+  T* O = reinterpret_cast<T*>(p.out) + qrow * p.ldo + h * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
+    store4<T>(O + dt * 16 + 4 * g, v);
+  }
+}
+
+template <typename T, int D, int NW>
+void launch(const AttnP& p, hipStream_t st) {
+  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
+  hipLaunchKernelGGL((attn_kernel<T, D, NW>), grid, dim3(NW * 64), 0, st, p);
+}
+
+template <typename T>
+int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
+  if (p.mode == 1) {
+    if (head_dim == 32) { launch<T, 32, 3>(p, st); return 0; }
+  } else {
+    if (head_dim == 64) { launch<T, 64, 4>(p, st); return 0; }
+    if (head_dim == 32) { launch<T, 32, 4>(p, st); return 0; }
+  }
+  return -1;
+}
+
+}  // namespace
+
+extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");
+  CATSEG_CHECK(a->n_seq > 0 && a->seq_len > 0 && a->n_heads > 0, "attention: empty shape");
+  const int vn = a->dtype == CATSEG_BF16 ? 8 : 4;
+  CATSEG_CHECK(a->ld_qkv % vn == 0 && a->ld_out % 4 == 0, "attention: row strides must allow 16B loads");
+  CATSEG_CHECK(((uintptr_t)a->q % 16) == 0 && ((uintptr_t)a->k % 16) == 0 && ((uintptr_t)a->v % 16) == 0,
+               "attention: q/k/v must be 16B aligned");
+  AttnP p;
+  p.q = a->q; p.k = a->k; p.v = a->v; p.ld = a->ld_qkv; p.out = a->out; p.ldo = a->ld_out;
+  p.n_seq = a->n_seq; p.L = a->seq_len; p.H = a->n_heads; p.scale = a->scale; p.causal = a->causal;
+  p.mode = a->mode; p.img_h = a->img_h; p.img_w = a->img_w; p.ws = a->window; p.shift = a->shift;
+  if (a->mode == 1) {
+    CATSEG_CHECK(a->window > 0 && a->img_h % a->window == 0 && a->img_w % a->window == 0,
+                 "attention: image must tile into windows");
+    CATSEG_CHECK(a->seq_len == a->window * a->window, "attention: seq_len must be window^2");
+    CATSEG_CHECK(a->shift >= 0 && a->shift < a->window, "attention: bad shift");
+    CATSEG_CHECK(!a->causal, "attention: causal not supported for windows");
+  } else {
+    CATSEG_CHECK(a->mode == 0, "attention: bad mode");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  int rc = a->dtype == CATSEG_BF16 ? dispatch<bf16>(p, a->head_dim, st)
+                                   : dispatch<float>(p, a->head_dim, st);
+  CATSEG_CHECK(rc == 0, "attention: unsupported head_dim/mode combination");
+  return catseg_launch_status("attention");
+}

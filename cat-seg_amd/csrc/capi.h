@@ -1,0 +1,30 @@
+// Internal helpers for the extern "C" entry points (error state, checks).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include "catseg_hip.h"
+
+void catseg_set_error(const char* fmt, ...);
+
+#define CATSEG_CHECK(cond, msg)                      \
+  do {                                               \
+    if (!(cond)) {                                   \
+      catseg_set_error("%s", msg);                   \
+      return CATSEG_ERR_ARG;                         \
+    }                                                \
+  } while (0)
+
+#define CATSEG_FAIL(msg)        \
+  do {                          \
+    catseg_set_error("%s", msg);\
+    return CATSEG_ERR_ARG;      \
+  } while (0)
+
+static inline int catseg_launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    catseg_set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return CATSEG_ERR_HIP;
+  }
+  return CATSEG_OK;
+}

@@ -1,0 +1,107 @@
+// Common device helpers for the CAT-Seg gfx950 kernels.
+//
+// Element types: activations are either fp32 or bf16 (raw ushort storage,
+// round-to-nearest-even conversion).  MFMA: bf16 uses
+// v_mfma_f32_16x16x32_bf16, fp32 uses the exact-f32 v_mfma_f32_16x16x4_f32
+// (gfx950 has no xf32).  Both share the 16x16 C/D layout
+// (col = lane & 15, row = 4 * (lane >> 4) + reg), see
+// /opt/skills/guides/cdna_hip_programming.md §3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include <type_traits>
+
+typedef unsigned short bf16;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define DEV __device__ __forceinline__
+
+DEV float bf2f(bf16 v) { return __uint_as_float(((unsigned)v) << 16); }
+DEV bf16 f2bf(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));  // inf/nan
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16)(u >> 16);
+}
+
+template <typename T> DEV float to_f(T v);
+template <> DEV float to_f<float>(float v) { return v; }
+template <> DEV float to_f<bf16>(bf16 v) { return bf2f(v); }
+template <typename T> DEV T from_f(float v);
+template <> DEV float from_f<float>(float v) { return v; }
+template <> DEV bf16 from_f<bf16>(float v) { return f2bf(v); }
+
+// 16-byte vector of T: 4 floats or 8 bf16
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { static constexpr int N = 4; };
+template <> struct Vec16<bf16> { static constexpr int N = 8; };
+
+DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+DEV void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+// load 4 consecutive elements as floats
+template <typename T> DEV void load4(const T* p, float out[4]);
+template <> DEV void load4<float>(const float* p, float out[4]) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+}
+template <> DEV void load4<bf16>(const bf16* p, float out[4]) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  out[0] = __uint_as_float(v.x << 16); out[1] = __uint_as_float(v.x & 0xffff0000u);
+  out[2] = __uint_as_float(v.y << 16); out[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <typename T> DEV void store4(T* p, const float v[4]);
+template <> DEV void store4<float>(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> DEV void store4<bf16>(bf16* p, const float v[4]) {
+  uint2 o;
+  o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+  o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = o;
+}
+
+DEV f32x4 mfma_bf16(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+DEV f32x4 mfma_f32(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Activations (epilogues).  GELU is the exact erf form (nn.GELU default, timm Mlp);
+// QuickGELU is CLIP's x*sigmoid(1.702x) (model_vpt.py:165-167).
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_QUICKGELU = 3, ACT_SIGMOID = 4 };
+DEV float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case ACT_QUICKGELU: return v / (1.f + __expf(-1.702f * v));
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+// Row map: r(m) = ((m / d1) % m1) * s1 + ((m / d2) % m2) * s2 + off.
+// Identity = {1, INT64 big, 1, 1, 1, 0, 0}.  Used to gather A rows (hook tokens
+// without CLS) and to broadcast per-image / per-class guidance terms.
+struct RowMap {
+  int64_t d1, m1, s1, d2, m2, s2, off;
+};
+DEV int64_t rowmap(const RowMap& r, int64_t m) {
+  return ((m / r.d1) % r.m1) * r.s1 + ((m / r.d2) % r.m2) * r.s2 + r.off;
+}

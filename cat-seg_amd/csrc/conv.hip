@@ -1,0 +1,422 @@
+// 3x3 / pad 1 convolution over NHWC as an MFMA implicit GEMM (gfx950), plus the
+// GroupNorm statistics / apply kernels and the 1-channel head conv of the guided
+// upsampler (reference cat_seg/modeling/transformer/model.py:520-555,616,627,634).
+//
+// GEMM view: D[co][m] = sum_k Wt[co][k] * A[m][k], m = (slice, y, x), k = (ky, kx, ci).
+// The A loader gathers 16-byte channel chunks of the 3x3 neighbourhood straight from
+// the NHWC sources (zero outside the image), reading channels [0, c1) from the per-
+// slice tensor and [c1, c1+c2) from the per-image guidance tensor, so the channel
+// concatenation of Up.forward (model.py:551-554) and its repeat over classes are
+// never materialised.  An optional GroupNorm+ReLU prologue normalises src1 on load
+// (DoubleConv's second conv consumes relu(GN(conv1))).  The epilogue adds bias,
+// applies the activation and, for GroupNorm consumers, emits per-(tile, group)
+// mean/M2 partials that catseg_groupnorm_stats combines deterministically.
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int BK = 32, NT = 256, BM = 128;
+
+struct ConvP {
+  const void* s1; int64_t s1_ss, s1_off; int c1;
+  const void* s2; int64_t s2_ss, s2_off; int c2; int64_t s2_div;
+  int64_t S; int H, W;
+  const void* w; int cout;
+  const float* bias; int act;
+  const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
+  void* out; float* stats; int scpg;
+};
+
+template <typename T>
+DEV uint4 gn_chunk(uint4 u, const ConvP& p, int64_t s, int ci) {
+  constexpr int VN = Vec16<T>::N;
+  T* e = reinterpret_cast<T*>(&u);
+  const int grp = ci / p.gcpg;
+  const int ngroups = p.c1 / p.gcpg;
+  const float mu = p.gmean[s * ngroups + grp], rs = p.grstd[s * ngroups + grp];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) {
+    float v = (to_f<T>(e[j]) - mu) * rs * p.ggamma[ci + j] + p.gbeta[ci + j];
+    e[j] = from_f<T>(fmaxf(v, 0.f));
+  }
+  return u;
+}
+
+template <typename T, int BN>
+__global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
+  constexpr int VN = Vec16<T>::N;
+  constexpr int CPR = BK / VN;
+  constexpr int LDR = BK + (sizeof(T) == 2 ? 8 : 4);
+  constexpr int A_CH = BM * CPR / NT;
+  constexpr int W_TOT = BN * CPR, W_CH = (W_TOT + NT - 1) / NT;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) T sA[2][BM * LDR];
+  __shared__ __attribute__((aligned(16))) T sW[2][BN * LDR];
+  __shared__ float red[4][8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t HW = (int64_t)p.H * p.W;
+  const int64_t M = p.S * HW;
+  const int cin = p.c1 + p.c2;
+  const int64_t K = 9LL * cin;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int wm = (wave & 1) * WM, wn = (wave >> 1) * WN;
+
+  int a_lrow[A_CH], a_col[A_CH], a_y[A_CH], a_x[A_CH];
+  int64_t a_s[A_CH]; bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    int c = tid + i * NT;
+    a_lrow[i] = c / CPR; a_col[i] = (c % CPR) * VN;
+    int64_t m = m0 + a_lrow[i];
+    a_ok[i] = m < M;
+    int64_t mm = a_ok[i] ? m : 0;
+    a_s[i] = mm / HW;
+    int pix = (int)(mm % HW);
+    a_y[i] = pix / p.W; a_x[i] = pix % p.W;
+  }
+  const T* S1 = reinterpret_cast<const T*>(p.s1);
+  const T* S2 = reinterpret_cast<const T*>(p.s2);
+  const T* Wt = reinterpret_cast<const T*>(p.w);
+
+  uint4 ra[A_CH], rw[W_CH];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int64_t k = k0 + a_col[i];
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (a_ok[i] && k < K) {
+        const int tap = (int)(k / cin), ci = (int)(k % cin);
+        const int yy = a_y[i] + tap / 3 - 1, xx = a_x[i] + tap % 3 - 1;
+        if (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+          const int64_t pix = (int64_t)yy * p.W + xx;
+          if (ci < p.c1) {
+            u = ld16(S1 + a_s[i] * p.s1_ss + p.s1_off + pix * p.c1 + ci);
+            if (p.gmean) u = gn_chunk<T>(u, p, a_s[i], ci);
+          } else {
+            u = ld16(S2 + (a_s[i] / p.s2_div) * p.s2_ss + p.s2_off + pix * p.c2 + (ci - p.c1));
+          }
+        }
+      }
+      ra[i] = u;
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int c = tid + i * NT;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (c < W_TOT) {
+        const int n = n0 + c / CPR;
+        const int64_t k = k0 + (c % CPR) * VN;
+        if (n < p.cout && k < K) u = ld16(Wt + (int64_t)n * K + k);
+      }
+      rw[i] = u;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], ra[i]);
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int c = tid + i * NT;
+      if (c < W_TOT) st16(&sW[buf][(c / CPR) * LDR + (c % CPR) * VN], rw[i]);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = (int)((K + BK - 1) / BK);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BK);
+    const T* As = sA[buf];
+    const T* Ws = sW[buf];
+    if constexpr (sizeof(T) == 2) {
+      const int r = lane & 15, kc = (lane >> 4) * 8;
+      s16x8 bfrag[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j + r) * LDR + kc]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        s16x8 afrag = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i + r) * LDR + kc]);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag, bfrag[j], acc[i][j]);
+      }
+    } else {
+      const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int s = 0; s < BK / 4; ++s) {
+        float bv[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) bv[j] = As[(wm + 16 * j + r) * LDR + 4 * s + kq];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          float av = Ws[(wn + 16 * i + r) * LDR + 4 * s + kq];
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma_f32(av, bv[j], acc[i][j]);
+        }
+      }
+    }
+    if (kt + 1 < ktiles) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias, act, store, GroupNorm partials ----
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  T* O = reinterpret_cast<T*>(p.out);
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = n0 + wn + 16 * i + rq;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int64_t m = m0 + wm + 16 * j + col;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + ((p.bias && n + r < p.cout) ? p.bias[n + r] : 0.f);
+        acc[i][j][r] = apply_act(v, p.act);
+      }
+      if (m < M && n < p.cout) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        store4<T>(O + m * p.cout + n, v);
+      }
+    }
+  }
+  if (p.stats) {
+    // tile = BM rows of ONE slice (host checks HW % BM == 0), columns = all groups
+    // (host checks BN >= cout, scpg == 16).  Two passes: tile mean, then M2.
+    const int64_t s = m0 / HW;
+    const int tile = (int)((m0 % HW) / BM);
+    const int ntiles = (int)(HW / BM);
+    const int ngroups = p.cout / p.scpg;
+    float gsum[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a += acc[i][j][r];
+      gsum[i] = warp_sum(a);
+    }
+    // each wave covers groups (wn/16 + i) over its WM rows; combine the two row-halves
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) red[wave][i] = gsum[i];
+    __syncthreads();
+    float gmean[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int wpair = wave ^ 1;   // same wn, other wm
+      gmean[i] = (red[wave][i] + red[wpair][i]) / (float)(BM * 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[i][j][r] - gmean[i];
+          a += d * d;
+        }
+      gsum[i] = warp_sum(a);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) red[wave][i] = gsum[i];
+    __syncthreads();
+    if ((wave & 1) == 0 && lane == 0) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int grp = (n0 + wn) / 16 + i;
+        if (grp < ngroups) {
+          float* o = p.stats + ((s * ntiles + tile) * ngroups + grp) * 2;
+          o[0] = gmean[i];
+          o[1] = red[wave][i] + red[wave ^ 1][i];
+        }
+      }
+    }
+  }
+}
+
+template <typename T>
+int launch_conv(const ConvP& p, hipStream_t st) {
+  const int64_t M = p.S * p.H * p.W;
+  const unsigned gx = (unsigned)((M + BM - 1) / BM);
+  if (p.cout <= 32) {
+    hipLaunchKernelGGL((conv3x3_kernel<T, 32>), dim3(gx, 1), dim3(NT), 0, st, p);
+  } else if (p.cout <= 64) {
+    hipLaunchKernelGGL((conv3x3_kernel<T, 64>), dim3(gx, 1), dim3(NT), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((conv3x3_kernel<T, 128>), dim3(gx, (unsigned)((p.cout + 127) / 128)), dim3(NT), 0, st, p);
+  }
+  return 0;
+}
+
+// ---------------- GroupNorm stats combine (Chan et al. pairwise, fixed order) ----
+__global__ void gn_stats_kernel(const float* part, int64_t S, int tiles, int groups, float tile_n,
+                                float eps, float* mean, float* rstd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S * groups) return;
+  const int64_t s = i / groups;
+  const int g = (int)(i % groups);
+  double n = 0, mu = 0, m2 = 0;
+  for (int t = 0; t < tiles; ++t) {
+    const float* q = part + ((s * tiles + t) * groups + g) * 2;
+    const double nb = tile_n, mb = q[0], m2b = q[1];
+    const double nn = n + nb, d = mb - mu;
+    mu += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  mean[i] = (float)mu;
+  rstd[i] = (float)(1.0 / sqrt(m2 / n + (double)eps));
+}
+
+template <typename T>
+__global__ void gn_relu_kernel(const T* x, T* y, int64_t total4, int C, int cpg, int64_t HW,
+                               const float* mean, const float* rstd, const float* gamma, const float* beta) {
+  const int groups = C / cpg;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % C);
+    const int64_t s = e / ((int64_t)C * HW);
+    const int g = c / cpg;
+    const float mu = mean[s * groups + g], rs = rstd[s * groups + g];
+    float v[4];
+    load4<T>(x + e, v);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf((v[r] - mu) * rs * gamma[c + r] + beta[c + r], 0.f);
+    store4<T>(y + e, v);
+  }
+}
+
+// ---------------- head conv3x3 C -> 1 (+bias), GN+ReLU applied on load -----------
+template <typename T>
+__global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, const float* w, float bias,
+                            const float* mean, const float* rstd, const float* gamma, const float* beta, int cpg,
+                            const int32_t* classes, int Tout, float* out) {
+  extern __shared__ float sw[];   // [9][C] weights, then gamma, beta
+  for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) sw[i] = w[i];
+  __syncthreads();
+  const int64_t HW = (int64_t)H * W;
+  const int64_t total = B * Tn * HW;
+  const int groups = C / cpg;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i / HW;
+    const int pix = (int)(i % HW), y = pix / W, xx = pix % W;
+    float acc = bias;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yy = y + tap / 3 - 1, x2 = xx + tap % 3 - 1;
+      if (yy < 0 || yy >= H || x2 < 0 || x2 >= W) continue;
+      const T* src = x + (s * HW + (int64_t)yy * W + x2) * C;
+      for (int c = 0; c < C; c += 4) {
+        float v[4];
+        load4<T>(src + c, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float u = v[r];
+          if (mean) {
+            const int g = (c + r) / cpg;
+            u = fmaxf((u - mean[s * groups + g]) * rstd[s * groups + g] * gamma[c + r] + beta[c + r], 0.f);
+          }
+          acc += u * sw[tap * C + c + r];
+        }
+      }
+    }
+    const int64_t b = s / Tn;
+    const int t = (int)(s % Tn);
+    const int cls = classes ? classes[b * Tn + t] : t;
+    out[(b * Tout + cls) * HW + pix] = acc;
+  }
+}
+
+}  // namespace
+
+extern "C" int catseg_conv_tile_rows(void) { return BM; }
+
+extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->src1 && a->weight && a->out, "conv3x3: null pointer");
+  CATSEG_CHECK(a->S > 0 && a->H > 0 && a->W > 0 && a->c1 > 0 && a->c_out > 0, "conv3x3: empty shape");
+  const int vn = a->dtype == CATSEG_BF16 ? 8 : 4;
+  CATSEG_CHECK(a->c1 % vn == 0 && a->c2 % vn == 0, "conv3x3: channel counts must be multiples of 16 bytes");
+  CATSEG_CHECK(a->c2 == 0 || (a->src2 && a->src2_div > 0), "conv3x3: src2 missing");
+  CATSEG_CHECK(a->c_out % 4 == 0, "conv3x3: c_out must be a multiple of 4");
+  CATSEG_CHECK(a->s1_slice_stride % vn == 0 && a->s1_offset % vn == 0, "conv3x3: src1 stride alignment");
+  CATSEG_CHECK(!a->gn_mean || (a->gn_rstd && a->gn_gamma && a->gn_beta && a->gn_cpg > 0 && a->c1 % a->gn_cpg == 0 &&
+                               a->gn_cpg % vn == 0),
+               "conv3x3: bad GroupNorm prologue");
+  if (a->stats) {
+    CATSEG_CHECK(((int64_t)a->H * a->W) % BM == 0, "conv3x3: GN stats need H*W % 128 == 0");
+    CATSEG_CHECK(a->c_out <= 64 && a->stats_cpg == 16 && a->c_out % 16 == 0, "conv3x3: GN stats need cout<=64, 16/group");
+  }
+  ConvP p;
+  p.s1 = a->src1; p.s1_ss = a->s1_slice_stride; p.s1_off = a->s1_offset; p.c1 = a->c1;
+  p.s2 = a->src2; p.s2_ss = a->s2_slice_stride; p.s2_off = a->s2_offset; p.c2 = a->c2; p.s2_div = a->src2_div > 0 ? a->src2_div : 1;
+  p.S = a->S; p.H = a->H; p.W = a->W; p.w = a->weight; p.cout = a->c_out; p.bias = a->bias; p.act = a->act;
+  p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
+  p.out = a->out; p.stats = a->stats; p.scpg = a->stats_cpg;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->dtype == CATSEG_BF16) launch_conv<bf16>(p, st);
+  else launch_conv<float>(p, st);
+  return catseg_launch_status("conv3x3");
+}
+
+extern "C" int catseg_groupnorm_stats(const float* partials, int64_t S, int tiles, int groups, int64_t tile_count,
+                                      float eps, float* mean, float* rstd, void* stream) {
+  CATSEG_CHECK(partials && mean && rstd && S > 0 && tiles > 0 && groups > 0, "groupnorm_stats: bad args");
+  const int64_t n = S * groups;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     partials, S, tiles, groups, (float)tile_count, eps, mean, rstd);
+  return catseg_launch_status("groupnorm_stats");
+}
+
+extern "C" int catseg_groupnorm_relu(const void* x, void* y, int64_t S, int64_t HW, int C, int cpg,
+                                     const float* mean, const float* rstd, const float* gamma,
+                                     const float* beta, int dtype, void* stream) {
+  CATSEG_CHECK(x && y && mean && rstd && gamma && beta && C % 4 == 0 && cpg > 0 && C % cpg == 0 && cpg % 4 == 0,
+               "groupnorm_relu: bad args");
+  const int64_t total4 = S * HW * C / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>((total4 + 255) / 256, 8192);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(gn_relu_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y,
+                       total4, C, cpg, HW, mean, rstd, gamma, beta);
+  else
+    hipLaunchKernelGGL(gn_relu_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       (float*)y, total4, C, cpg, HW, mean, rstd, gamma, beta);
+  return catseg_launch_status("groupnorm_relu");
+}
+
+extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, int W, int C, const float* weight,
+                                      float bias, const float* mean, const float* rstd, const float* gamma,
+                                      const float* beta, int cpg, const int32_t* classes, int T_out, float* out,
+                                      int dtype, void* stream) {
+  CATSEG_CHECK(x && weight && out && C % 4 == 0 && B > 0 && T > 0, "conv3x3_head: bad args");
+  CATSEG_CHECK(!mean || (rstd && gamma && beta && cpg > 0 && C % cpg == 0), "conv3x3_head: bad GN args");
+  const int64_t total = B * T * (int64_t)H * W;
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 16384);
+  const size_t sh = 9 * C * sizeof(float);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(head_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const bf16*)x, B, T, H, W,
+                       C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
+  else
+    hipLaunchKernelGGL(head_kernel<float>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const float*)x, B, T, H,
+                       W, C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
+  return catseg_launch_status("conv3x3_head");
+}
+
+extern "C" int catseg_conv3x3_head(const void* x, int64_t B, int T, int H, int W, int C, const float* weight,
+                                   float bias, const int32_t* classes, int T_out, float* out, int dtype,
+                                   void* stream) {
+  return catseg_conv3x3_head_gn(x, B, T, H, W, C, weight, bias, nullptr, nullptr, nullptr, nullptr, 1, classes,
+                                T_out, out, dtype, stream);
+}

@@ -1,0 +1,254 @@
+// MFMA GEMM with fused epilogue:  out[m, n] = act(alpha-free) ...
+//
+//   v = sum_k A[amap(m), k] * W[n, k]            (fp32 accumulate)
+//   v += bias[n]                                 (optional, fp32)
+//   v += add[addmap(m), n]   for n < add_ncols   (optional: per-image / per-class
+//                                                 guidance terms, CLS broadcast)
+//   v = act(v) * alpha
+//   v += res[m, n] + res2[m, n]                  (optional residual streams)
+//   out[store(m, n)] = v                          (row-major or ConvTranspose scatter)
+//
+// W is in nn.Linear layout [N, K] (K contiguous), as are A's rows, so both MFMA
+// operands are K-contiguous 16-byte fragments.  The product is computed as
+// D = W_tile . A_tile^T, so each lane ends with 4 CONSECUTIVE output columns of one
+// row (C/D layout row = 4*(lane>>4)+r -> n, col = lane&15 -> m): one 8/16-byte
+// vector store per fragment, and bias/residual loads are vectors too.
+//
+// This serves every GEMM-shaped op on the path: ViT QKV / out-proj / MLP,
+// ln_post@proj, patch-embed (im2col), Swin and class-attention projections and
+// MLPs, the cost volume, ConvTranspose2d (store mode 1) and the guidance terms.
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int NT = 256;   // 4 waves
+
+template <typename TA> struct Lds;
+template <> struct Lds<bf16> { static constexpr int PAD = 8; };   // row = 40 bf16 = 80 B
+template <> struct Lds<float> { static constexpr int PAD = 4; };  // row = 36 f32 = 144 B
+
+struct EpiArgs {
+  const float* bias;
+  const void* add; int64_t ld_add; RowMap addmap; int64_t add_ncols;
+  int act; float alpha;
+  const void* res; int64_t ld_res;
+  const void* res2; int64_t ld_res2;
+  void* out; int64_t ldo;
+  int store_mode; int cvt_k, cvt_hin, cvt_win, cvt_cout;
+};
+
+template <typename TO>
+DEV void epilogue4(const EpiArgs& e, int64_t m, int64_t n, f32x4 acc) {
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  if (e.bias) {
+    float4 b = *reinterpret_cast<const float4*>(e.bias + n);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+  if (e.add && n < e.add_ncols) {
+    float a[4];
+    load4<TO>(reinterpret_cast<const TO*>(e.add) + rowmap(e.addmap, m) * e.ld_add + n, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += a[r];
+  }
+  if (e.act != ACT_NONE || e.alpha != 1.f) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], e.act) * e.alpha;
+  }
+  if (e.res) {
+    float a[4];
+    load4<TO>(reinterpret_cast<const TO*>(e.res) + m * e.ld_res + n, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += a[r];
+  }
+  if (e.res2) {
+    float a[4];
+    load4<TO>(reinterpret_cast<const TO*>(e.res2) + m * e.ld_res2 + n, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += a[r];
+  }
+  int64_t off;
+  if (e.store_mode == 0) {
+    off = m * e.ldo + n;
+  } else {   // ConvTranspose2d(k, stride k) scatter: m = (s, y, x), n = (ky, kx, co)
+    const int64_t k = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
+    const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
+    const int64_t ky = n / (k * cout), kx = (n / cout) % k, co = n % cout;
+    off = ((s * hin * k + y * k + ky) * (win * k) + x * k + kx) * cout + co;
+  }
+  store4<TO>(reinterpret_cast<TO*>(e.out) + off, v);
+}
+
+template <typename TA, typename TO, int BM, int BN>
+__global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int64_t lda, RowMap amap,
+                                                  const TA* __restrict__ W, int64_t ldw,
+                                                  int64_t M, int64_t N, int64_t K, EpiArgs e) {
+  constexpr int VN = Vec16<TA>::N;           // elements per 16-byte chunk
+  constexpr int CPR = BK / VN;               // chunks per tile row
+  constexpr int LDR = BK + Lds<TA>::PAD;     // LDS row stride (elements)
+  constexpr int A_CH = BM * CPR / NT;        // chunks per thread
+  constexpr int W_CH = BN * CPR / NT;
+  static_assert(A_CH >= 1 && W_CH >= 1, "tile too small");
+  constexpr int WM = BM / 2, WN = BN / 2;    // wave tile (2x2 waves)
+  constexpr int FM = WM / 16, FN = WN / 16;
+
+  __shared__ __attribute__((aligned(16))) TA sA[2][BM * LDR];
+  __shared__ __attribute__((aligned(16))) TA sW[2][BN * LDR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+  const int wm = (wave & 1) * WM, wn = (wave >> 1) * WN;
+
+  // per-thread staging rows (fixed over the K loop)
+  const TA* a_ptr[A_CH]; int a_lrow[A_CH], a_col[A_CH]; bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    int c = tid + i * NT;
+    a_lrow[i] = c / CPR; a_col[i] = (c % CPR) * VN;
+    int64_t m = m0 + a_lrow[i];
+    a_ok[i] = m < M;
+    a_ptr[i] = A + (a_ok[i] ? rowmap(amap, m) : 0) * lda;
+  }
+  const TA* w_ptr[W_CH]; int w_lrow[W_CH], w_col[W_CH]; bool w_ok[W_CH];
+#pragma unroll
+  for (int i = 0; i < W_CH; ++i) {
+    int c = tid + i * NT;
+    w_lrow[i] = c / CPR; w_col[i] = (c % CPR) * VN;
+    int64_t n = n0 + w_lrow[i];
+    w_ok[i] = n < N;
+    w_ptr[i] = W + (w_ok[i] ? n : 0) * ldw;
+  }
+
+  uint4 ra[A_CH], rw[W_CH];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int64_t k = k0 + a_col[i];
+      ra[i] = (a_ok[i] && k < K) ? ld16(a_ptr[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      int64_t k = k0 + w_col[i];
+      rw[i] = (w_ok[i] && k < K) ? ld16(w_ptr[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], ra[i]);
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) st16(&sW[buf][w_lrow[i] * LDR + w_col[i]], rw[i]);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = (int)((K + BK - 1) / BK);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BK);
+    const TA* As = sA[buf];
+    const TA* Ws = sW[buf];
+    if constexpr (sizeof(TA) == 2) {
+      const int r = lane & 15, kc = (lane >> 4) * 8;
+      s16x8 bfrag[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j + r) * LDR + kc]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        s16x8 afrag = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i + r) * LDR + kc]);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag, bfrag[j], acc[i][j]);
+      }
+    } else {
+      const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int s = 0; s < BK / 4; ++s) {
+        float bv[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) bv[j] = As[(wm + 16 * j + r) * LDR + 4 * s + kq];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          float av = Ws[(wn + 16 * i + r) * LDR + 4 * s + kq];
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma_f32(av, bv[j], acc[i][j]);
+        }
+      }
+    }
+    if (kt + 1 < ktiles) {
+      sstore(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // epilogue
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int64_t n = n0 + wn + 16 * i + rq;
+    if (n >= N) continue;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int64_t m = m0 + wm + 16 * j + col;
+      if (m < M) epilogue4<TO>(e, m, n, acc[i][j]);
+    }
+  }
+}
+
+template <typename TA, typename TO, int BM, int BN>
+void launch(const CatsegGemmArgs* g, hipStream_t st) {
+  EpiArgs e;
+  e.bias = g->bias;
+  e.add = g->add; e.ld_add = g->ld_add; e.add_ncols = g->add_ncols;
+  e.addmap = RowMap{g->addmap.d1, g->addmap.m1, g->addmap.s1, g->addmap.d2, g->addmap.m2, g->addmap.s2, g->addmap.off};
+  e.act = g->act; e.alpha = g->alpha;
+  e.res = g->res; e.ld_res = g->ld_res; e.res2 = g->res2; e.ld_res2 = g->ld_res2;
+  e.out = g->out; e.ldo = g->ldo;
+  e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
+  e.cvt_cout = g->cvt_cout;
+  RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
+  dim3 grid((unsigned)((g->M + BM - 1) / BM), (unsigned)((g->N + BN - 1) / BN));
+  hipLaunchKernelGGL((gemm_kernel<TA, TO, BM, BN>), grid, dim3(NT), 0, st,
+                     (const TA*)g->A, g->lda, am, (const TA*)g->W, g->ldw, g->M, g->N, g->K, e);
+}
+
+template <typename TA, typename TO>
+void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->N <= 64) launch<TA, TO, 128, 64>(g, st);
+  else launch<TA, TO, 128, 128>(g, st);
+}
+
+}  // namespace
+
+extern "C" int catseg_gemm(const CatsegGemmArgs* g, void* stream) {
+  CATSEG_CHECK(g && g->A && g->W && g->out, "gemm: null pointer");
+  CATSEG_CHECK(g->M > 0 && g->N > 0 && g->K > 0, "gemm: empty shape");
+  CATSEG_CHECK(g->N % 4 == 0, "gemm: N must be a multiple of 4");
+  const int va = g->dtype_a == CATSEG_BF16 ? 8 : 4;
+  CATSEG_CHECK(g->K % va == 0 && g->lda % va == 0 && g->ldw % va == 0,
+               "gemm: K/lda/ldw must be multiples of 16 bytes");
+  CATSEG_CHECK(((uintptr_t)g->A % 16) == 0 && ((uintptr_t)g->W % 16) == 0, "gemm: A/W must be 16B aligned");
+  CATSEG_CHECK(g->ldo % 4 == 0, "gemm: ldo must be a multiple of 4");
+  CATSEG_CHECK(!g->add || g->ld_add % 4 == 0, "gemm: ld_add must be a multiple of 4");
+  CATSEG_CHECK(g->store_mode == 0 || (g->cvt_cout % 4 == 0 && g->cvt_k > 0 && g->cvt_hin > 0 && g->cvt_win > 0),
+               "gemm: bad ConvTranspose scatter geometry");
+  CATSEG_CHECK(g->store_mode == 0 || g->N == (int64_t)g->cvt_k * g->cvt_k * g->cvt_cout,
+               "gemm: ConvTranspose N must be k*k*cout");
+  CATSEG_CHECK(g->amap.d1 > 0 && g->amap.m1 > 0 && g->amap.d2 > 0 && g->amap.m2 > 0, "gemm: bad amap");
+  CATSEG_CHECK(!g->add || (g->addmap.d1 > 0 && g->addmap.m1 > 0 && g->addmap.d2 > 0 && g->addmap.m2 > 0),
+               "gemm: bad addmap");
+  hipStream_t st = (hipStream_t)stream;
+  if (g->dtype_a == CATSEG_BF16 && g->dtype_out == CATSEG_BF16) launch_tiles<bf16, bf16>(g, st);
+  else if (g->dtype_a == CATSEG_BF16 && g->dtype_out == CATSEG_F32) launch_tiles<bf16, float>(g, st);
+  else if (g->dtype_a == CATSEG_F32 && g->dtype_out == CATSEG_F32) launch_tiles<float, float>(g, st);
+  else if (g->dtype_a == CATSEG_F32 && g->dtype_out == CATSEG_BF16) launch_tiles<float, bf16>(g, st);
+  else CATSEG_FAIL("gemm: unsupported dtype combination");
+  return catseg_launch_status("gemm");
+}

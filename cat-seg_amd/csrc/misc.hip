@@ -1,0 +1,521 @@
+// Row-wise and data-movement kernels of the CAT-Seg path (HBM-bound; vectorised,
+// one wave per row where a row reduction is needed) and the C-ABI error state.
+#include <stdarg.h>
+#include <string.h>
+#include "common.h"
+#include "capi.h"
+
+static thread_local char g_err[512] = "";
+
+void catseg_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char* catseg_last_error(void) { return g_err; }
+extern "C" int catseg_abi_version(void) { return 1; }
+
+namespace {
+
+constexpr int MAXV = 8;   // <= 8 float4 per lane -> cols <= 2048
+
+// ---------------- LayerNorm / L2 normalise (one wave per row) -------------------
+template <typename TI, typename TO, bool LN>
+__global__ void rownorm_kernel(const TI* __restrict__ in, int64_t ld_in, RowMap inmap, TO* __restrict__ out,
+                               int64_t ld_out, const float* gamma, const float* beta, int64_t rows, int cols,
+                               float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* x = in + rowmap(inmap, row) * ld_in;
+  float v[MAXV][4];
+  float s = 0.f;
+  int nv = 0;
+#pragma unroll
+  for (int it = 0; it < MAXV; ++it) {
+    const int c = (it * 64 + lane) * 4;
+    if (c < cols) {
+      load4<TI>(x + c, v[it]);
+      s += v[it][0] + v[it][1] + v[it][2] + v[it][3];
+      nv = it + 1;
+    }
+  }
+  (void)nv;
+  if (LN) {
+    const float mean = warp_sum(s) / cols;
+    float q = 0.f;
+#pragma unroll
+    for (int it = 0; it < MAXV; ++it) {
+      const int c = (it * 64 + lane) * 4;
+      if (c < cols)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[it][r] -= mean;
+          q += v[it][r] * v[it][r];
+        }
+    }
+    const float rstd = rsqrtf(warp_sum(q) / cols + eps);
+#pragma unroll
+    for (int it = 0; it < MAXV; ++it) {
+      const int c = (it * 64 + lane) * 4;
+      if (c < cols) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = v[it][r] * rstd * gamma[c + r] + beta[c + r];
+        store4<TO>(out + row * ld_out + c, o);
+      }
+    }
+  } else {
+    float q = 0.f;
+#pragma unroll
+    for (int it = 0; it < MAXV; ++it) {
+      const int c = (it * 64 + lane) * 4;
+      if (c < cols)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q += v[it][r] * v[it][r];
+    }
+    const float inv = 1.f / fmaxf(sqrtf(warp_sum(q)), eps);
+#pragma unroll
+    for (int it = 0; it < MAXV; ++it) {
+      const int c = (it * 64 + lane) * 4;
+      if (c < cols) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = v[it][r] * inv;
+        store4<TO>(out + row * ld_out + c, o);
+      }
+    }
+  }
+}
+
+template <bool LN>
+int rownorm(const void* in, int64_t ld_in, CatsegRowMap m, int dti, void* out, int64_t ld_out, int dto,
+            const float* gamma, const float* beta, int64_t rows, int64_t cols, float eps, void* stream) {
+  CATSEG_CHECK(in && out && rows > 0 && cols > 0, "rownorm: bad args");
+  CATSEG_CHECK(cols % 4 == 0 && cols <= 64 * 4 * MAXV, "rownorm: cols must be a multiple of 4 and <= 2048");
+  CATSEG_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, "rownorm: strides must be multiples of 4");
+  CATSEG_CHECK(!LN || (gamma && beta), "layernorm: gamma/beta missing");
+  CATSEG_CHECK(m.d1 > 0 && m.m1 > 0 && m.d2 > 0 && m.m2 > 0, "rownorm: bad row map");
+  RowMap rm{m.d1, m.m1, m.s1, m.d2, m.m2, m.s2, m.off};
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+#define RN_LAUNCH(TI, TO)                                                                                   \
+  hipLaunchKernelGGL((rownorm_kernel<TI, TO, LN>), grid, block, 0, st, (const TI*)in, ld_in, rm, (TO*)out, \
+                     ld_out, gamma, beta, rows, (int)cols, eps)
+  if (dti == CATSEG_F32 && dto == CATSEG_F32) RN_LAUNCH(float, float);
+  else if (dti == CATSEG_F32 && dto == CATSEG_BF16) RN_LAUNCH(float, bf16);
+  else if (dti == CATSEG_BF16 && dto == CATSEG_BF16) RN_LAUNCH(bf16, bf16);
+  else RN_LAUNCH(bf16, float);
+#undef RN_LAUNCH
+  return catseg_launch_status(LN ? "layernorm" : "l2normalize");
+}
+
+// ---------------- corr_embed: Conv2d(1, hidden, 7, pad 3) per cost slice ------------
+template <typename TO>
+__global__ void corr_embed_kernel(const float* corr, int64_t ts, int64_t bs, const int32_t* classes, int Tn, int H,
+                                  int W, const float* w, const float* bias, int hidden, TO* out) {
+  extern __shared__ float sm[];
+  const int PW = W + 6, PH = H + 6;
+  float* sin = sm;                     // [PH][PW]
+  float* sw = sm + PH * PW;            // [49][hidden]
+  const int64_t s = blockIdx.x;
+  const int64_t b = s / Tn;
+  const int t = (int)(s % Tn);
+  const int cls = classes ? classes[s] : t;
+  const float* src = corr + (int64_t)cls * ts + b * bs;
+  for (int i = threadIdx.x; i < PH * PW; i += blockDim.x) {
+    const int y = i / PW - 3, x = i % PW - 3;
+    sin[i] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 49 * hidden; i += blockDim.x) {
+    const int tap = i / hidden, c = i % hidden;
+    sw[i] = w[c * 49 + tap];
+  }
+  __syncthreads();
+  const int c = threadIdx.x % hidden;
+  const int step = blockDim.x / hidden;
+  const float bc = bias[c];
+  for (int pix = threadIdx.x / hidden; pix < H * W; pix += step) {
+    const int y = pix / W, x = pix % W;
+    float acc = bc;
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) acc += sin[(y + ky) * PW + x + kx] * sw[(ky * 7 + kx) * hidden + c];
+    out[(s * H * W + pix) * hidden + c] = from_f<TO>(acc);
+  }
+}
+
+// ---------------- top-k classes per image (bitonic sort of (max corr, idx)) ---------
+__global__ void topk_kernel(const float* corr, int64_t ts, int64_t bs, int Tn, int HW, int k, int32_t* classes) {
+  __shared__ float sv[2048];
+  __shared__ int si[2048];
+  const int64_t b = blockIdx.x;
+  int n = 1;
+  while (n < Tn) n <<= 1;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    float m = -INFINITY;
+    if (t < Tn) {
+      const float* src = corr + (int64_t)t * ts + b * bs;
+      for (int p = 0; p < HW; ++p) m = fmaxf(m, src[p]);
+    }
+    sv[t] = m;
+    si[t] = t < Tn ? t : 0x7fffffff;
+  }
+  __syncthreads();
+  // sort descending by value, ascending by index on ties
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const float a = sv[i], c = sv[j];
+          const int ia = si[i], ic = si[j];
+          const bool a_first = (a > c) || (a == c && ia < ic);
+          if (desc != a_first) {
+            sv[i] = c; sv[j] = a; si[i] = ic; si[j] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < k; i += blockDim.x) classes[b * k + i] = si[i];
+}
+
+template <typename E>
+__global__ void gather_rows_kernel(const E* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols, E* out,
+                                   int64_t ld_out) {
+  const int64_t total = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols, c = i % cols;
+    out[r * ld_out + c] = in[(int64_t)idx[r] * ld_in + c];
+  }
+}
+
+__global__ void fill_kernel(float* out, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = v;
+}
+
+// ---------------- preprocess + im2col --------------------------------------------
+// torch bilinear, align_corners=False: src = max(scale*(dst+0.5)-0.5, 0), scale = in/out
+DEV void lin_idx(int dst, int in_size, float scale, int& i0, int& i1, float& l1) {
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  src = fmaxf(src, 0.f);
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in_size - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+template <typename TO>
+__global__ void pre_im2col_kernel(const float* raw, const int32_t* sizes, int64_t B, int Hp, int Wp, const float* mean,
+                                  const float* stdv, int res, int patch, TO* out, int64_t ld_out) {
+  const int G = res / patch;
+  const int Kc = 3 * patch * patch;
+  const int64_t total = B * (int64_t)G * G * ld_out;
+  const float sy = (float)Hp / (float)res, sx = (float)Wp / (float)res;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int kcol = (int)(i % ld_out);
+    const int64_t m = i / ld_out;
+    float v = 0.f;
+    if (kcol < Kc) {
+      const int64_t b = m / (G * G);
+      const int gp = (int)(m % (G * G)), gy = gp / G, gx = gp % G;
+      const int c = kcol / (patch * patch), kk = kcol % (patch * patch), ky = kk / patch, kx = kk % patch;
+      const int oy = gy * patch + ky, ox = gx * patch + kx;
+      int y0, y1, x0, x1;
+      float ly, lx;
+      lin_idx(oy, Hp, sy, y0, y1, ly);
+      lin_idx(ox, Wp, sx, x0, x1, lx);
+      const int h = sizes[2 * b], w = sizes[2 * b + 1];
+      const float* img = raw + (b * 3 + c) * (int64_t)Hp * Wp;
+      const float mu = mean[c], inv = 1.f / stdv[c];
+      auto px = [&](int y, int x) -> float { return (y < h && x < w) ? (img[(int64_t)y * Wp + x] - mu) * inv : 0.f; };
+      v = (1.f - ly) * ((1.f - lx) * px(y0, x0) + lx * px(y0, x1)) + ly * ((1.f - lx) * px(y1, x0) + lx * px(y1, x1));
+    }
+    out[i] = from_f<TO>(v);
+  }
+}
+
+// ---------------- ViT embed: [cls; patches] + pos -> ln_pre ------------------------
+__global__ void vit_embed_kernel(const float* patches, const float* cls, const float* pos, const float* gamma,
+                                 const float* beta, int64_t B, int G2, int width, float* x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int L = G2 + 1;
+  if (row >= B * L) return;
+  const int64_t b = row / L;
+  const int tok = (int)(row % L);
+  const float* src = tok == 0 ? cls : patches + (b * G2 + tok - 1) * width;
+  const float* pp = pos + (int64_t)tok * width;
+  float v[MAXV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXV; ++it) {
+    const int c = (it * 64 + lane) * 4;
+    if (c < width) {
+      float a[4], q[4];
+      load4<float>(src + c, a);
+      load4<float>(pp + c, q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[it][r] = a[r] + q[r]; s += v[it][r]; }
+    }
+  }
+  const float mean = warp_sum(s) / width;
+  float q2 = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXV; ++it) {
+    const int c = (it * 64 + lane) * 4;
+    if (c < width)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[it][r] -= mean; q2 += v[it][r] * v[it][r]; }
+  }
+  const float rstd = rsqrtf(warp_sum(q2) / width + 1e-5f);
+#pragma unroll
+  for (int it = 0; it < MAXV; ++it) {
+    const int c = (it * 64 + lane) * 4;
+    if (c < width) {
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = v[it][r] * rstd * gamma[c + r] + beta[c + r];
+      store4<float>(x + row * width + c, o);
+    }
+  }
+}
+
+// ---------------- bicubic (torch upsample_bicubic2d, A = -0.75, align_corners=False) ----
+DEV float cc1(float x, float A) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; }
+DEV float cc2(float x, float A) { return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A; }
+
+__global__ void bicubic_kernel(const float* in, int Si, int D, float* out, int So) {
+  const int64_t total = (int64_t)So * So * D;
+  const float scale = (float)Si / (float)So;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int op = (int)(i / D), oy = op / So, ox = op % So;
+    const float ry = scale * (oy + 0.5f) - 0.5f, rx = scale * (ox + 0.5f) - 0.5f;
+    const int iy = (int)floorf(ry), ix = (int)floorf(rx);
+    const float ty = ry - iy, tx = rx - ix;
+    const float A = -0.75f;
+    const float wy[4] = {cc2(ty + 1.f, A), cc1(ty, A), cc1(1.f - ty, A), cc2(2.f - ty, A)};
+    const float wx[4] = {cc2(tx + 1.f, A), cc1(tx, A), cc1(1.f - tx, A), cc2(2.f - tx, A)};
+    float acc = 0.f;
+    for (int a = 0; a < 4; ++a) {
+      const int yy = min(max(iy - 1 + a, 0), Si - 1);
+      float row = 0.f;
+      for (int c = 0; c < 4; ++c) {
+        const int xx = min(max(ix - 1 + c, 0), Si - 1);
+        row += in[((int64_t)yy * Si + xx) * D + d] * wx[c];
+      }
+      acc += row * wy[a];
+    }
+    out[i] = acc;
+  }
+}
+
+// ---------------- postprocess: sigmoid + bilinear resize -----------------------------
+__global__ void post_kernel(const float* lg, int64_t planes, int h, int w, int ch, int cw, float* out, int H, int W) {
+  const int64_t total = planes * (int64_t)H * W;
+  const float sy = (float)ch / (float)H, sx = (float)cw / (float)W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % W);
+    const int y = (int)((i / W) % H);
+    const int64_t pl = i / ((int64_t)H * W);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    lin_idx(y, ch, sy, y0, y1, ly);
+    lin_idx(x, cw, sx, x0, x1, lx);
+    const float* src = lg + pl * (int64_t)h * w;
+    auto sg = [&](int yy, int xx) -> float { return 1.f / (1.f + expf(-src[yy * w + xx])); };
+    out[i] = (1.f - ly) * ((1.f - lx) * sg(y0, x0) + lx * sg(y0, x1)) + ly * ((1.f - lx) * sg(y1, x0) + lx * sg(y1, x1));
+  }
+}
+
+// ---------------- text: token embedding + EOT gather ------------------------------
+__global__ void token_embed_kernel(const int32_t* tok, int64_t n, int ctx, const float* emb, const float* pos, int width,
+                                   float* x) {
+  const int64_t total = n * ctx * (int64_t)width;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % width);
+    const int64_t r = i / width;
+    const int pi = (int)(r % ctx);
+    x[i] = emb[(int64_t)tok[r] * width + c] + pos[(int64_t)pi * width + c];
+  }
+}
+
+__global__ void eot_kernel(const float* x, const int32_t* tok, int64_t n, int ctx, int width, float* out) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  __shared__ int arg;
+  if (threadIdx.x == 0) {
+    int best = 0, bv = tok[r * ctx];
+    for (int i = 1; i < ctx; ++i)
+      if (tok[r * ctx + i] > bv) { bv = tok[r * ctx + i]; best = i; }
+    arg = best;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < width; c += blockDim.x) out[r * width + c] = x[(r * ctx + arg) * width + c];
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap = 16384) {
+  int64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+
+}  // namespace
+
+extern "C" int catseg_layernorm(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in, void* out,
+                                int64_t ld_out, int dtype_out, const float* gamma, const float* beta, int64_t rows,
+                                int64_t cols, float eps, void* stream) {
+  return rownorm<true>(in, ld_in, inmap, dtype_in, out, ld_out, dtype_out, gamma, beta, rows, cols, eps, stream);
+}
+
+extern "C" int catseg_l2normalize(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in, void* out,
+                                  int64_t ld_out, int dtype_out, int64_t rows, int64_t cols, float eps, void* stream) {
+  return rownorm<false>(in, ld_in, inmap, dtype_in, out, ld_out, dtype_out, nullptr, nullptr, rows, cols, eps, stream);
+}
+
+extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
+                                 const int32_t* classes, int64_t B, int T, int H, int W, const float* weight,
+                                 const float* bias, int hidden, void* out, int dtype, void* stream) {
+  CATSEG_CHECK(corr && weight && bias && out && B > 0 && T > 0 && H > 0 && W > 0, "corr_embed: bad args");
+  CATSEG_CHECK(hidden > 0 && 256 % hidden == 0, "corr_embed: hidden must divide 256");
+  const size_t sh = ((H + 6) * (W + 6) + 49 * hidden) * sizeof(float);
+  CATSEG_CHECK(sh <= 64 * 1024, "corr_embed: slice too large for LDS");
+  const unsigned grid = (unsigned)(B * T);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(corr_embed_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, corr, corr_t_stride,
+                       corr_b_stride, classes, T, H, W, weight, bias, hidden, (bf16*)out);
+  else
+    hipLaunchKernelGGL(corr_embed_kernel<float>, dim3(grid), dim3(256), sh, (hipStream_t)stream, corr, corr_t_stride,
+                       corr_b_stride, classes, T, H, W, weight, bias, hidden, (float*)out);
+  return catseg_launch_status("corr_embed");
+}
+
+extern "C" int catseg_topk_classes(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride, int64_t B, int T,
+                                   int HW, int k, int32_t* classes, void* stream) {
+  CATSEG_CHECK(corr && classes && B > 0 && T > 0 && HW > 0, "topk: bad args");
+  CATSEG_CHECK(T <= 2048 && k > 0 && k <= T, "topk: need 0 < k <= T <= 2048");
+  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
+                     corr_b_stride, T, HW, k, classes);
+  return catseg_launch_status("topk");
+}
+
+extern "C" int catseg_gather_rows(const void* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols,
+                                  void* out, int64_t ld_out, int dtype, void* stream) {
+  CATSEG_CHECK(in && idx && out && rows > 0 && cols > 0, "gather_rows: bad args");
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(gather_rows_kernel<bf16>, dim3(grid_for(rows * cols)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)in, ld_in, idx, rows, cols, (bf16*)out, ld_out);
+  else
+    hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(grid_for(rows * cols)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)in, ld_in, idx, rows, cols, (float*)out, ld_out);
+  return catseg_launch_status("gather_rows");
+}
+
+extern "C" int catseg_fill_f32(float* out, int64_t n, float value, void* stream) {
+  CATSEG_CHECK(out && n > 0, "fill: bad args");
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, value);
+  return catseg_launch_status("fill");
+}
+
+extern "C" int catseg_preprocess_im2col(const float* raw, const int32_t* sizes, int64_t B, int Hp, int Wp,
+                                        const float* mean, const float* stdv, int res, int patch, void* out,
+                                        int64_t ld_out, int dtype, void* stream) {
+  CATSEG_CHECK(raw && sizes && mean && stdv && out && B > 0 && Hp > 0 && Wp > 0, "preprocess: bad args");
+  CATSEG_CHECK(patch > 0 && res % patch == 0 && ld_out >= 3 * patch * patch, "preprocess: bad geometry");
+  const int G = res / patch;
+  const int64_t total = B * (int64_t)G * G * ld_out;
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(pre_im2col_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, raw, sizes, B,
+                       Hp, Wp, mean, stdv, res, patch, (bf16*)out, ld_out);
+  else
+    hipLaunchKernelGGL(pre_im2col_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, raw, sizes,
+                       B, Hp, Wp, mean, stdv, res, patch, (float*)out, ld_out);
+  return catseg_launch_status("preprocess_im2col");
+}
+
+extern "C" int catseg_vit_embed(const float* patches, const float* cls, const float* pos, const float* gamma,
+                                const float* beta, int64_t B, int G2, int width, float* x, void* stream) {
+  CATSEG_CHECK(patches && cls && pos && gamma && beta && x && B > 0 && G2 > 0, "vit_embed: bad args");
+  CATSEG_CHECK(width % 4 == 0 && width <= 64 * 4 * MAXV, "vit_embed: bad width");
+  const int64_t rows = B * (G2 + 1);
+  hipLaunchKernelGGL(vit_embed_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, patches,
+                     cls, pos, gamma, beta, B, G2, width, x);
+  return catseg_launch_status("vit_embed");
+}
+
+extern "C" int catseg_bicubic_resize(const float* in, int S_in, int D, float* out, int S_out, void* stream) {
+  CATSEG_CHECK(in && out && S_in > 0 && S_out > 0 && D > 0, "bicubic: bad args");
+  const int64_t total = (int64_t)S_out * S_out * D;
+  hipLaunchKernelGGL(bicubic_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in, S_in, D, out, S_out);
+  return catseg_launch_status("bicubic");
+}
+
+extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                                  float* out, int H, int W, void* stream) {
+  CATSEG_CHECK(logits && out && B > 0 && T > 0 && H > 0 && W > 0, "postprocess: bad args");
+  CATSEG_CHECK(crop_h > 0 && crop_h <= h && crop_w > 0 && crop_w <= w, "postprocess: bad crop");
+  const int64_t total = B * T * (int64_t)H * W;
+  hipLaunchKernelGGL(post_kernel, dim3(grid_for(total, 65536)), dim3(256), 0, (hipStream_t)stream, logits, B * T, h, w,
+                     crop_h, crop_w, out, H, W);
+  return catseg_launch_status("postprocess");
+}
+
+extern "C" int catseg_token_embed(const int32_t* tokens, int64_t n, int ctx, const float* tok_emb, const float* pos,
+                                  int width, float* x, void* stream) {
+  CATSEG_CHECK(tokens && tok_emb && pos && x && n > 0 && ctx > 0 && width > 0, "token_embed: bad args");
+  hipLaunchKernelGGL(token_embed_kernel, dim3(grid_for(n * ctx * width)), dim3(256), 0, (hipStream_t)stream, tokens,
+                     n, ctx, tok_emb, pos, width, x);
+  return catseg_launch_status("token_embed");
+}
+
+extern "C" int catseg_eot_gather(const float* x, const int32_t* tokens, int64_t n, int ctx, int width, float* out,
+                                 void* stream) {
+  CATSEG_CHECK(x && tokens && out && n > 0, "eot_gather: bad args");
+  hipLaunchKernelGGL(eot_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, x, tokens, n, ctx, width, out);
+  return catseg_launch_status("eot_gather");
+}
+
+// ---------------- dtype conversion with a row map (hook / feature casts) ------------
+namespace {
+template <typename TI, typename TO>
+__global__ void convert_kernel(const TI* in, int64_t ld_in, RowMap m, TO* out, int64_t ld_out, int64_t rows,
+                               int64_t cols4) {
+  const int64_t total = rows * cols4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols4, c = (i % cols4) * 4;
+    float v[4];
+    load4<TI>(in + rowmap(m, r) * ld_in + c, v);
+    store4<TO>(out + r * ld_out + c, v);
+  }
+}
+}  // namespace
+
+extern "C" int catseg_convert(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in, void* out,
+                              int64_t ld_out, int dtype_out, int64_t rows, int64_t cols, void* stream) {
+  CATSEG_CHECK(in && out && rows > 0 && cols > 0 && cols % 4 == 0 && ld_in % 4 == 0 && ld_out % 4 == 0,
+               "convert: bad args");
+  CATSEG_CHECK(inmap.d1 > 0 && inmap.m1 > 0 && inmap.d2 > 0 && inmap.m2 > 0, "convert: bad row map");
+  RowMap rm{inmap.d1, inmap.m1, inmap.s1, inmap.d2, inmap.m2, inmap.s2, inmap.off};
+  const unsigned grid = grid_for(rows * cols / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype_in == CATSEG_F32 && dtype_out == CATSEG_BF16)
+    hipLaunchKernelGGL((convert_kernel<float, bf16>), dim3(grid), dim3(256), 0, st, (const float*)in, ld_in, rm,
+                       (bf16*)out, ld_out, rows, cols / 4);
+  else if (dtype_in == CATSEG_F32 && dtype_out == CATSEG_F32)
+    hipLaunchKernelGGL((convert_kernel<float, float>), dim3(grid), dim3(256), 0, st, (const float*)in, ld_in, rm,
+                       (float*)out, ld_out, rows, cols / 4);
+  else if (dtype_in == CATSEG_BF16 && dtype_out == CATSEG_F32)
+    hipLaunchKernelGGL((convert_kernel<bf16, float>), dim3(grid), dim3(256), 0, st, (const bf16*)in, ld_in, rm,
+                       (float*)out, ld_out, rows, cols / 4);
+  else
+    hipLaunchKernelGGL((convert_kernel<bf16, bf16>), dim3(grid), dim3(256), 0, st, (const bf16*)in, ld_in, rm,
+                       (bf16*)out, ld_out, rows, cols / 4);
+  return catseg_launch_status("convert");
+}

@@ -1,0 +1,241 @@
+/*
+ * catseg_hip.h — C ABI of libcatseg_hip.so, the MI355X (gfx950) kernels of the
+ * CAT-Seg dense-inference hot path.
+ *
+ * Conventions
+ *   - Plain pointers to DEVICE memory, int64 sizes/strides in ELEMENTS, a dtype
+ *     enum, and the HIP stream as `void*` (a hipStream_t; NULL = default stream).
+ *   - Caller-allocated outputs and workspaces; no entry point allocates,
+ *     synchronises or copies to the host, so every one is hipGraph-capturable.
+ *   - Return 0 on success, < 0 on error; catseg_last_error() then holds a
+ *     thread-local message.  Arguments are validated on the host before launch.
+ *   - Row-major, channels-last layouts.  The aggregation cost tensor is
+ *     X[b][t][h][w][c] (the reference's B C T H W, model.py:683-725, with C moved
+ *     innermost), i.e. rows of `hidden` channels ordered (image, class, pixel).
+ *
+ * Each entry names the reference function(s) it replaces (paths relative to the
+ * reference repo root).  The Python host mirror is cat-seg_amd/cat_seg/ops.py.
+ */
+#ifndef CATSEG_HIP_H
+#define CATSEG_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CATSEG_OK = 0, CATSEG_ERR_ARG = -1, CATSEG_ERR_HIP = -2 };
+enum { CATSEG_F32 = 0, CATSEG_BF16 = 1 };
+enum { CATSEG_ACT_NONE = 0, CATSEG_ACT_RELU = 1, CATSEG_ACT_GELU = 2, CATSEG_ACT_QUICKGELU = 3,
+       CATSEG_ACT_SIGMOID = 4 };
+
+const char* catseg_last_error(void);
+int catseg_abi_version(void);
+
+/* r(m) = ((m / d1) % m1) * s1 + ((m / d2) % m2) * s2 + off   (identity: {1,BIG,1,1,1,0,0}) */
+typedef struct {
+  int64_t d1, m1, s1, d2, m2, s2, off;
+} CatsegRowMap;
+
+/* ---------------------------------------------------------------------------
+ * catseg_gemm — every dense contraction on the path.  Replaces nn.Linear /
+ * F.linear calls of model_vpt.py:193-236 (ViT q/k/v, out_proj, c_fc+QuickGELU,
+ * c_proj), model_vpt.py:312 (ln_post @ proj), model_vpt.py:289 (patch conv as
+ * im2col GEMM), model.py:77-112 + 159 (Swin q/k/v/proj/Mlp), model.py:327-366
+ * (class-attention q/k/v/MLP), model.py:648-652 (cost-volume einsum),
+ * model.py:546 / cat_seg_model.py:81-82 (ConvTranspose2d k=s via store_mode 1).
+ *   out[store(m,n)] = act(A[amap(m),:] . W[n,:] + bias[n] + add[addmap(m), n<add_ncols]) * alpha
+ *                     + res[m,n] + res2[m,n]
+ * W: [N][K] (nn.Linear layout).  bias: fp32 [N] or NULL.  add/res/res2/out share
+ * dtype_out.  store_mode 1: m = (s, y, x) over (cvt_hin, cvt_win), n = (ky, kx, co),
+ * out NHWC [s][y*k+ky][x*k+kx][co].
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const void* A; int64_t lda; CatsegRowMap amap;
+  const void* W; int64_t ldw;
+  int64_t M, N, K;
+  const float* bias;
+  const void* add; int64_t ld_add; CatsegRowMap addmap; int64_t add_ncols;
+  int act; float alpha;
+  const void* res; int64_t ld_res;
+  const void* res2; int64_t ld_res2;
+  void* out; int64_t ldo;
+  int store_mode; int cvt_k, cvt_hin, cvt_win, cvt_cout;
+  int dtype_a, dtype_out;
+} CatsegGemmArgs;
+int catseg_gemm(const CatsegGemmArgs* args, void* stream);
+
+/* catseg_layernorm — LayerNorm over the last dim (fp32 math).  Replaces
+ * model_vpt.py:156-162 (ln_pre/ln_1/ln_2/ln_post/ln_final) and the nn.LayerNorm of
+ * model.py:152,158,233,368-369.  in rows use `inmap`. */
+int catseg_layernorm(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in,
+                     void* out, int64_t ld_out, int dtype_out,
+                     const float* gamma, const float* beta, int64_t rows, int64_t cols,
+                     float eps, void* stream);
+
+/* catseg_l2normalize — x / max(||x||, eps) per row (F.normalize, model.py:649-650,
+ * cat_seg_predictor.py:216, model.py:714). */
+int catseg_l2normalize(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in,
+                       void* out, int64_t ld_out, int dtype_out, int64_t rows, int64_t cols,
+                       float eps, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * catseg_attention — softmax attention, flash-style (online softmax, K/V tiles
+ * staged in LDS, MFMA for QK^T and PV).
+ *   mode 0 (dense sequences): nn.MultiheadAttention of model_vpt.py:202-206
+ *     (ViT, 16/12 heads x 64) and the causal text encoder (:400-406).
+ *     Sequence s, token i lives at row s*seq_len + i.
+ *   mode 1 (Swin windows): WindowAttention of model.py:86-114 with the cyclic
+ *     shift and -100 region mask of model.py:161-216.  Sequence s = (slice,
+ *     window); token i maps to pixel ((wy*ws + i/ws + shift) % H, ...) of slice.
+ *   q/k/v: row pointers (columns of one head at + h*head_dim), row stride ld_qkv.
+ *   out:   row stride ld_out, head h at columns h*head_dim.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const void* q; const void* k; const void* v; int64_t ld_qkv;
+  void* out; int64_t ld_out;
+  int64_t n_seq; int seq_len; int n_heads; int head_dim;
+  float scale; int causal;
+  int mode; int img_h, img_w, window, shift;
+  int dtype;
+} CatsegAttnArgs;
+int catseg_attention(const CatsegAttnArgs* args, void* stream);
+
+/* catseg_linear_attention — class aggregation attention (LinearAttention,
+ * model.py:256-286, inside AttentionLayer model.py:338-354 and the padding of
+ * ClassTransformerLayer model.py:397-410).  For every pixel (b, p) the sequence is
+ * the T classes, rows (b*T + t)*HW + p of q/k/v (heads x head_dim columns).
+ * n_pad learned padding tokens with constant projections k_pad/v_pad (fp32,
+ * heads*head_dim) join the K/V sums; S = T + n_pad is the reference's v_length.
+ *   y[row] = x[row] + LinearAttn(q, k, v)[row]            (x/y: ld_xy, may alias) */
+typedef struct {
+  const void* q; const void* k; const void* v; int64_t ld_qkv;
+  const void* x; void* y; int64_t ld_xy;
+  int64_t B; int T; int HW; int n_heads; int head_dim;
+  int n_pad; const float* k_pad; const float* v_pad; float eps;
+  int dtype;
+} CatsegLinAttnArgs;
+int catseg_linear_attention(const CatsegLinAttnArgs* args, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * catseg_conv3x3 — 3x3 / pad 1 convolution as an MFMA implicit GEMM over NHWC.
+ * Replaces nn.Conv2d of model.py:528,531 (DoubleConv), 616, 627 (guidance
+ * projections).  Input channels are the concatenation [src1 (c1) || src2 (c2)]
+ * without materialising it (model.py:551-554): src1 per slice s, src2 per image
+ * s / src2_div (the decoder guidance repeated over T).  Optional GroupNorm+ReLU
+ * prologue on src1 (gn_mean/gn_rstd per (s, group of gn_cpg channels), gamma/
+ * beta per channel).  Epilogue: + bias, act, optional GroupNorm partial stats
+ * (per (s, tile, group): count-weighted mean and M2) for catseg_groupnorm_stats.
+ *   weight: [c_out][3][3][c1+c2] (K contiguous).  out: [S][H][W][c_out].
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const void* src1; int64_t s1_slice_stride; int64_t s1_offset; int c1;
+  const void* src2; int64_t s2_slice_stride; int64_t s2_offset; int c2; int64_t src2_div;
+  int64_t S; int H; int W;
+  const void* weight; int c_out;
+  const float* bias; int act;
+  const float* gn_mean; const float* gn_rstd; const float* gn_gamma; const float* gn_beta; int gn_cpg;
+  void* out; float* stats; int stats_cpg;
+  int dtype;
+} CatsegConvArgs;
+int catseg_conv3x3(const CatsegConvArgs* args, void* stream);
+/* Rows per conv tile (the `tile` axis of the stats buffer): stats is
+ * [S][H*W/catseg_conv_tile_rows()][c_out/stats_cpg][2]. */
+int catseg_conv_tile_rows(void);
+
+/* catseg_groupnorm_stats — combine the conv partials into mean / rstd per
+ * (slice, group) (nn.GroupNorm statistics, model.py:529,532; eps 1e-5). */
+int catseg_groupnorm_stats(const float* partials, int64_t S, int tiles, int groups, int64_t tile_count,
+                           float eps, float* mean, float* rstd, void* stream);
+
+/* catseg_groupnorm_relu — y = relu((x - mean[s,g]) * rstd[s,g] * gamma[c] + beta[c]) over
+ * NHWC [S][HW][C] (GroupNorm + ReLU of model.py:529-533). */
+int catseg_groupnorm_relu(const void* x, void* y, int64_t S, int64_t HW, int C, int cpg,
+                          const float* mean, const float* rstd, const float* gamma,
+                          const float* beta, int dtype, void* stream);
+
+/* catseg_conv3x3_head — the final head conv3x3 c_in -> 1 with bias (model.py:634,679)
+ * writing fp32 logits into out[b][cls(b, t)][H][W], cls = classes[b*T + t] (or t if
+ * classes == NULL); out has T_out class planes (the top-k scatter of model.py:721-724). */
+int catseg_conv3x3_head(const void* x, int64_t B, int T, int H, int W, int C,
+                        const float* weight, float bias, const int32_t* classes, int T_out,
+                        float* out, int dtype, void* stream);
+/* Same, with the preceding GroupNorm+ReLU (mean/rstd per (slice, group of cpg
+ * channels), gamma/beta per channel) applied to x on load.  weight: [9][C]. */
+int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, int W, int C,
+                           const float* weight, float bias, const float* mean, const float* rstd,
+                           const float* gamma, const float* beta, int cpg,
+                           const int32_t* classes, int T_out, float* out, int dtype, void* stream);
+
+/* catseg_corr_embed — Conv2d(1, hidden, 7, pad 3) on every cost slice
+ * (Aggregator.corr_embed, model.py:654-659).  corr: fp32, slice (b, t) read from
+ * corr + cls(b,t)*corr_t_stride + b*corr_b_stride (cls = classes[b*T+t] or t),
+ * H*W contiguous.  out: X rows [(b*T + t)*H*W + p][hidden]. */
+int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
+                      const int32_t* classes, int64_t B, int T, int H, int W,
+                      const float* weight, const float* bias, int hidden,
+                      void* out, int dtype, void* stream);
+
+/* catseg_topk_classes — per image, the top-k classes by max-over-pixels cosine
+ * (model.py:694-696; ties broken by lower class index).  corr fp32 laid out as
+ * corr[t*corr_t_stride + b*corr_b_stride + p]. */
+int catseg_topk_classes(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
+                        int64_t B, int T, int HW, int k, int32_t* classes, void* stream);
+
+/* catseg_gather_rows — out[r] = in[idx[r]] for fp32/bf16 rows (text guidance gather
+ * of model.py:697-698). */
+int catseg_gather_rows(const void* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols,
+                       void* out, int64_t ld_out, int dtype, void* stream);
+
+/* catseg_convert — out[r] = (dtype_out) in[inmap(r)] (hook / feature casts, CLS drop of
+ * cat_seg_model.py:178-183). */
+int catseg_convert(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtype_in,
+                   void* out, int64_t ld_out, int dtype_out, int64_t rows, int64_t cols, void* stream);
+
+/* catseg_fill_f32 — out[i] = value (the -100 canvas of model.py:722). */
+int catseg_fill_f32(float* out, int64_t n, float value, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Image side
+ * ------------------------------------------------------------------------- */
+/* catseg_preprocess_im2col — cat_seg_model.py:149-154 + the patch conv's im2col:
+ * normalize (mean/std), ImageList zero-pad (value 0 after normalization) to the
+ * padded canvas (Hp, Wp), bilinear resize (align_corners=False) to res x res, then
+ * unfold res/patch x res/patch patches into rows (b, gy, gx) of K = 3*patch*patch
+ * columns ordered (c, ky, kx), zero-padded to ld_out.  raw: fp32 [B][3][Hp][Wp]
+ * (0..255), sizes: int32 [B][2] valid (h, w) per image. */
+int catseg_preprocess_im2col(const float* raw, const int32_t* sizes, int64_t B, int Hp, int Wp,
+                             const float* mean, const float* std, int res, int patch,
+                             void* out, int64_t ld_out, int dtype, void* stream);
+
+/* catseg_vit_embed — VisualTransformer.forward head (model_vpt.py:290-300):
+ * x[b, 0] = cls + pos[0]; x[b, 1+p] = patches[b*G2 + p] + pos[1+p]; then ln_pre.
+ * patches fp32 [B*G2][width]; x fp32 [B*(G2+1)][width]. */
+int catseg_vit_embed(const float* patches, const float* cls, const float* pos,
+                     const float* gamma, const float* beta, int64_t B, int G2, int width,
+                     float* x, void* stream);
+
+/* catseg_bicubic_resize — VisualTransformer.resized_pos_embed (model_vpt.py:316-329),
+ * bicubic (A = -0.75) align_corners=False on a [S_in][S_in][D] grid -> [S_out][S_out][D]. */
+int catseg_bicubic_resize(const float* in, int S_in, int D, float* out, int S_out, void* stream);
+
+/* catseg_postprocess — sigmoid then bilinear (align_corners=False) of fp32 logits
+ * [B][T][h][w] cropped to (crop_h, crop_w) to [B][T][H][W] fp32
+ * (cat_seg_model.py:222-227 + detectron2 sem_seg_postprocess). */
+int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                       float* out, int H, int W, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Text side (CLIP.encode_text, model_vpt.py:421-438)
+ * ------------------------------------------------------------------------- */
+/* catseg_token_embed — x[n, i] = tok_emb[tokens[n, i]] + pos[i]  (fp32 out). */
+int catseg_token_embed(const int32_t* tokens, int64_t n, int ctx, const float* tok_emb,
+                       const float* pos, int width, float* x, void* stream);
+/* catseg_eot_gather — out[n] = x[n*ctx + argmax_i tokens[n, i]] (first max). */
+int catseg_eot_gather(const float* x, const int32_t* tokens, int64_t n, int ctx, int width,
+                      float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CATSEG_HIP_H */

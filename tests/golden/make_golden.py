@@ -245,6 +245,8 @@ def main():
     e2e_case("e2e_tiny_pad", TINY, 10, [(300, 352), (320, 256)], seed=1, pad_len=16)
     # 2) tiny arch, T=24 > pad_len=16 (top-k + scatter -100), pooling (2,2)
     e2e_case("e2e_tiny_topk_pool", TINY.replace(pooling_size=(2, 2)), 24, [(384, 384)], seed=2, pad_len=16)
+    # 2b) tiny arch, T=24 > pad_len=16 (top-k + scatter -100), eval pooling (1,1), B=2
+    e2e_case("e2e_tiny_topk", TINY, 24, [(384, 384), (352, 384)], seed=5, pad_len=16)
     # 3) tiny arch, default pad_len 256, T=20, pooling (1,1) (the eval protocol), B=2
     e2e_case("e2e_tiny_eval", TINY, 20, [(384, 384), (384, 384)], seed=3)
     # 4) config 1: ViT-B/16@384 (pos-embed bicubic resize), voc20 tokens, bs=1, POOLING (2,2)

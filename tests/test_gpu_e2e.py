@@ -1,0 +1,80 @@
+"""End-to-end parity of the HIP engine against the golden vectors of the reference
+(tests/golden, made by importing the reference modules) and against the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cat_seg.arch import TINY, VIT_B16, VIT_L14_336
+from cat_seg.engine import CatSegEngine
+from cat_seg.weights import synthesize_state_dict
+from oracle import catseg_oracle as O
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def batch_raw(imgs, div=32):
+    H = max(i.shape[1] for i in imgs)
+    W = max(i.shape[2] for i in imgs)
+    H, W = -(-H // div) * div, -(-W // div) * div
+    raw = torch.zeros(len(imgs), 3, H, W)
+    for k, im in enumerate(imgs):
+        raw[k, :, : im.shape[1], : im.shape[2]] = im
+    sizes = torch.tensor([[i.shape[1], i.shape[2]] for i in imgs], dtype=torch.int32)
+    return raw.cuda(), sizes.cuda()
+
+
+# fp32 gate: 1e-3 (BASELINE.md parity gates); bf16 gate: max-abs 5e-2, mean-abs 5e-3
+@pytest.mark.parametrize("name", ["e2e_tiny_pad", "e2e_tiny_eval", "e2e_tiny_topk"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_engine_vs_reference_golden(name, dtype):
+    g = load(name)
+    arch = TINY.replace(pad_len=int(g["pad_len"]))
+    sd = synthesize_state_dict(arch, seed=0)
+    eng = CatSegEngine(arch, sd, dtype=dtype)
+    text = eng.encode_text(torch.from_numpy(g["tokens"]).int())
+    t_err = (text.cpu() - torch.from_numpy(g["text"][:, 0])).abs().max().item()
+    assert t_err < (1e-4 if dtype == torch.float32 else 2e-2), t_err
+    eng.set_text(torch.from_numpy(g["text"]).cuda())      # the cached reference embeddings
+    imgs = [torch.from_numpy(g[k]).float() for k in sorted(k for k in g if k.startswith("image"))]
+    raw, sizes = batch_raw(imgs)
+    logits = eng.head_logits(raw, sizes).cpu()
+    ref = torch.from_numpy(g["logits"])
+    err = (logits - ref).abs()
+    if dtype == torch.float32:
+        assert err.max().item() < 1e-3, err.max().item()
+    else:
+        assert err.max().item() < 5e-2 and err.mean().item() < 5e-3, (err.max().item(), err.mean().item())
+    if (ref < -99).any():   # top-k scatter: untouched classes are exactly -100
+        assert torch.equal(logits[ref < -99], ref[ref < -99])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_engine_b16_config2_vs_oracle(dtype):
+    """Config 2 geometry (ViT-B/16 @384, pos-embed resize, 150 classes), bs=2 here to keep
+    the CPU oracle fast; fp32 gate 1e-3."""
+    arch = VIT_B16
+    sd = synthesize_state_dict(arch, seed=0)
+    gen = torch.Generator().manual_seed(7)
+    text = torch.nn.functional.normalize(torch.randn(150, arch.embed_dim, generator=gen), dim=-1)
+    imgs = [torch.randint(0, 256, (3, 384, 384), generator=gen).float() for _ in range(2)]
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    clip_images, _ = O.preprocess(arch, imgs)
+    ref = O.head_logits(arch, sd, clip_images, text.unsqueeze(1))
+    eng = CatSegEngine(arch, sd, dtype=dtype)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    err = (got - ref).abs()
+    print(f"B/16 {dtype}: max {err.max().item():.3e} mean {err.mean().item():.3e}")
+    if dtype == torch.float32:
+        assert err.max().item() < 1e-3
+    else:
+        assert err.max().item() < 5e-2 and err.mean().item() < 5e-3

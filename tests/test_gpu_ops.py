@@ -1,0 +1,305 @@
+"""Per-kernel parity of the HIP C-ABI entry points against fp32/fp64 PyTorch and the
+oracle's functions, on seeded inputs.  Marked gpu: runs on the MI355X box only."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cat_seg import ops
+from cat_seg import _lib as L
+from cat_seg._lib import rowmap
+from oracle import catseg_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+
+
+def close(got, ref, atol, rtol=0.0, what=""):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    err = (got - ref).abs().max().item()
+    tol = atol + rtol * ref.abs().max().item()
+    assert err <= tol, f"{what}: max abs err {err:.3e} > {tol:.3e}"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    L.require_gpu()
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(300, 384, 128), (577, 1024, 1024), (33, 64, 96), (130, 32, 288), (1, 384, 128)])
+def test_gemm_plain(dt, M, N, K):
+    A = rnd(M, K, seed=1)
+    W = rnd(N, K, seed=2) / math.sqrt(K)
+    b = rnd(N, seed=3)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(A.to(dev, dt), W.to(dev, dt), out, bias=b.to(dev))
+    ref = A.to(dt).double() @ W.to(dt).double().T + b.double()
+    close(out, ref, atol=2e-5 if dt == torch.float32 else 1e-3, what="gemm")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dt):
+    M, N, K = 2 * 3 * 20, 384, 128      # rows (b=2, t=3, p=20)
+    A = rnd(M, K, seed=4)
+    W = rnd(N, K, seed=5) / math.sqrt(K)
+    b = rnd(N, seed=6)
+    add = rnd(2 * 20, 256, seed=7)       # per (b, p), first 256 columns
+    res = rnd(M, N, seed=8)
+    res2 = rnd(M, N, seed=9)
+    amap = rowmap(d1=1, m1=M, s1=1)
+    gmap = rowmap(d1=3 * 20, s1=20, d2=1, m2=20, s2=1)
+    outs = {}
+    for act in (L.ACT_NONE, L.ACT_RELU, L.ACT_GELU, L.ACT_QUICKGELU):
+        out = torch.empty(M, N, device=dev, dtype=dt)
+        ops.gemm(A.to(dev, dt), W.to(dev, dt), out, bias=b.to(dev), act=act, add=add.to(dev, dt), addmap=gmap,
+                 add_ncols=256, res=res.to(dev, dt), res2=res2.to(dev, dt), amap=amap)
+        v = A.to(dt).double() @ W.to(dt).double().T + b.double()
+        rows = torch.arange(M)
+        arow = (rows // 60) * 20 + rows % 20
+        v[:, :256] += add.to(dt).double()[arow]
+        fn = {L.ACT_NONE: lambda x: x, L.ACT_RELU: F.relu, L.ACT_GELU: F.gelu,
+              L.ACT_QUICKGELU: lambda x: x * torch.sigmoid(1.702 * x)}[act]
+        ref = fn(v) + res.to(dt).double() + res2.to(dt).double()
+        close(out, ref, atol=2e-5 if dt == torch.float32 else 3e-2, rtol=0 if dt == torch.float32 else 1e-2,
+              what=f"gemm act {act}")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_convtranspose_store(dt):
+    S, H, Wd, cin, cout, k = 3, 6, 5, 64, 48, 2
+    x = rnd(S, cin, H, Wd, seed=10)
+    w = rnd(cin, cout, k, k, seed=11) / 8
+    b = rnd(cout, seed=12)
+    ref = F.conv_transpose2d(x.to(dt).double(), w.to(dt).double(), b.double(), stride=k)   # (S, cout, kH, kW)
+    A = x.permute(0, 2, 3, 1).reshape(S * H * Wd, cin)
+    Wg = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)
+    out = torch.empty(S * H * k * Wd * k, cout, device=dev, dtype=dt)
+    ops.gemm(A.to(dev, dt).contiguous(), Wg.to(dev, dt).contiguous(), out, bias=b.repeat(k * k).to(dev),
+             store=(k, H, Wd, cout))
+    got = out.reshape(S, H * k, Wd * k, cout).permute(0, 3, 1, 2)
+    close(got, ref, atol=1e-5 if dt == torch.float32 else 2e-2, what="convT")
+
+
+def test_gemm_amap_cls_drop():
+    B, L_, C = 2, 5, 16
+    A = rnd(B * L_, C, seed=13)
+    W = rnd(8, C, seed=14)
+    out = torch.empty(B * (L_ - 1), 8, device=dev)
+    ops.gemm(A.to(dev), W.to(dev), out, M=B * (L_ - 1), amap=rowmap(d1=L_ - 1, s1=L_, d2=1, m2=L_ - 1, s2=1, off=1))
+    ref = A.reshape(B, L_, C)[:, 1:].reshape(-1, C).double() @ W.double().T
+    close(out, ref, atol=1e-5, what="amap")
+
+
+# ----------------------------------------------------------------------------- norms
+@pytest.mark.parametrize("cols", [128, 768, 1024, 96])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_l2(cols, dt):
+    x = rnd(77, cols, seed=15) * 3 + 0.5
+    g, b = rnd(cols, seed=16) + 1, rnd(cols, seed=17)
+    out = torch.empty(77, cols, device=dev, dtype=dt)
+    ops.layernorm(x.to(dev), g.to(dev), b.to(dev), out)
+    close(out, F.layer_norm(x.double(), (cols,), g.double(), b.double(), 1e-5),
+          atol=2e-5 if dt == torch.float32 else 2e-2, what="LN")
+    ops.l2normalize(x.to(dev), out)
+    close(out, F.normalize(x.double(), dim=-1), atol=1e-6 if dt == torch.float32 else 4e-3, what="l2")
+
+
+# ----------------------------------------------------------------------------- attention
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("L_,H,causal", [(577, 4, False), (77, 2, True), (50, 3, False)])
+def test_attention_dense(dt, L_, H, causal):
+    B, d = 2, 64
+    qkv = rnd(B * L_, 3 * H * d, seed=18) * 2
+    out = torch.empty(B * L_, H * d, device=dev, dtype=dt)
+    q = qkv.to(dev, dt)
+    ops.attention(q[:, :H * d], q[:, H * d:2 * H * d], q[:, 2 * H * d:], out, n_seq=B, seq_len=L_, n_heads=H,
+                  head_dim=d, scale=d ** -0.5, causal=causal)
+    x = qkv.to(dt).double().reshape(B, L_, 3, H, d).permute(2, 0, 3, 1, 4)
+    s = (x[0] @ x[1].transpose(-1, -2)) * d ** -0.5
+    if causal:
+        s = s + torch.full((L_, L_), float("-inf")).triu(1).double()
+    ref = (torch.softmax(s, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B * L_, H * d)
+    close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shift", [0, 6])
+def test_attention_swin_windows(dt, shift):
+    S, Hh, Ww, ws, nh, hd = 3, 24, 24, 12, 4, 32
+    D = nh * hd
+    qkv = rnd(S * Hh * Ww, 3 * D, seed=19) * 2
+    out = torch.empty(S * Hh * Ww, D, device=dev, dtype=dt)
+    q = qkv.to(dev, dt)
+    ops.attention(q[:, :D], q[:, D:2 * D], q[:, 2 * D:], out, n_seq=S * 4, seq_len=ws * ws, n_heads=nh,
+                  head_dim=hd, scale=hd ** -0.5, mode=1, img_hw=(Hh, Ww), window=ws, shift=shift)
+    # reference: roll -> partition -> masked softmax attention -> reverse -> roll back (model.py:185-219)
+    x = qkv.to(dt).double().reshape(S, Hh, Ww, 3 * D)
+    if shift:
+        x = torch.roll(x, (-shift, -shift), (1, 2))
+    xw = O.window_partition(x, ws).reshape(-1, ws * ws, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    a = (xw[0] * hd ** -0.5) @ xw[1].transpose(-1, -2)
+    if shift:
+        m = O.shift_mask(Hh, Ww, ws, shift).double()
+        a = (a.view(S, 4, nh, ws * ws, ws * ws) + m.unsqueeze(1).unsqueeze(0)).view(-1, nh, ws * ws, ws * ws)
+    o = (torch.softmax(a, -1) @ xw[2]).transpose(1, 2).reshape(-1, ws, ws, D)
+    o = O.window_reverse(o, ws, Hh, Ww)
+    if shift:
+        o = torch.roll(o, (shift, shift), (1, 2))
+    close(out, o.reshape(S * Hh * Ww, D), atol=2e-5 if dt == torch.float32 else 1.5e-2, what="swin attn")
+
+
+# ----------------------------------------------------------------------------- linear attention
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T,n_pad", [(20, 236), (150, 106), (256, 0), (37, 0)])
+def test_linear_attention(dt, T, n_pad):
+    B, HW, D = 2, 9, 128
+    qkv = rnd(B * T * HW, 3 * D, seed=20)
+    x = rnd(B * T * HW, D, seed=21)
+    kp, vp = rnd(D, seed=22), rnd(D, seed=23)
+    qd, xd = qkv.to(dev, dt), x.to(dev, dt)
+    y = torch.empty_like(xd)
+    ops.linear_attention(qd[:, :D], qd[:, D:2 * D], qd[:, 2 * D:], xd, y, B=B, T=T, HW=HW, n_heads=4, head_dim=32,
+                         n_pad=n_pad, k_pad=kp.to(dev), v_pad=vp.to(dev))
+    z = qkv.to(dt).double().reshape(B, T, HW, 3, 4, 32).permute(3, 0, 2, 1, 4, 5).reshape(3, B * HW, T, 4, 32)
+    q, k, v = z[0], z[1], z[2]
+    if n_pad:
+        k = torch.cat([k, kp.double().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+        v = torch.cat([v, vp.double().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+    o = O.linear_attention(q, k, v).reshape(B, HW, T, D).permute(0, 2, 1, 3).reshape(-1, D)
+    close(y, x.to(dt).double() + o, atol=2e-5 if dt == torch.float32 else 3e-2, what="linattn")
+
+
+# ----------------------------------------------------------------------------- conv + GN
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_dual_source_gn(dt):
+    B, T, H, W, c1, c2, co = 2, 3, 16, 16, 48, 16, 32
+    S = B * T
+    x1 = rnd(S, c1, H, W, seed=24)
+    x2 = rnd(B, c2, H, W, seed=25)
+    w = rnd(co, c1 + c2, 3, 3, seed=26) / 8
+    xin = torch.cat([x1, x2.repeat_interleave(T, 0)], 1)
+    ref = F.conv2d(xin.to(dt).double(), w.to(dt).double(), padding=1)
+    a1 = x1.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    a2 = x2.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    wk = w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+    out = torch.empty(S * H * W, co, device=dev, dtype=dt)
+    tiles = H * W // ops.conv_tile_rows()
+    st = torch.empty(S * tiles * (co // 16) * 2, device=dev)
+    ops.conv3x3(a1, wk, out, S=S, H=H, W=W, c1=c1, src2=a2, c2=c2, src2_div=T, stats=st)
+    got = out.reshape(S, H, W, co).permute(0, 3, 1, 2)
+    tol = 1e-5 if dt == torch.float32 else 3e-2
+    close(got, ref, atol=tol, what="conv")
+    mean = torch.empty(S * (co // 16), device=dev)
+    rstd = torch.empty_like(mean)
+    ops.groupnorm_stats(st, S, tiles, co // 16, ops.conv_tile_rows() * 16, mean, rstd)
+    g = ref.reshape(S, co // 16, -1)
+    close(mean, g.mean(-1).reshape(-1), atol=1e-5 if dt == torch.float32 else 1e-3, what="gn mean")
+    close(rstd, (1 / torch.sqrt(g.var(-1, unbiased=False) + 1e-5)).reshape(-1), atol=0, rtol=1e-4 if dt == torch.float32 else 2e-2,
+          what="gn rstd")
+    # GN+ReLU prologue feeding a second conv, and the head conv with GN on load
+    gam, bet = rnd(co, seed=27) + 1, rnd(co, seed=28)
+    w2 = rnd(co, co, 3, 3, seed=29) / 8
+    y1 = F.relu(F.group_norm(ref, co // 16, gam.double(), bet.double(), 1e-5))
+    ref2 = F.conv2d(y1, w2.to(dt).double(), padding=1)
+    out2 = torch.empty_like(out)
+    ops.conv3x3(out, w2.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt), out2, S=S, H=H, W=W, c1=co,
+                gn=(mean, rstd, gam.to(dev), bet.to(dev), 16))
+    close(out2.reshape(S, H, W, co).permute(0, 3, 1, 2), ref2, atol=1e-4 if dt == torch.float32 else 8e-2,
+          what="conv gn prologue")
+    z = torch.empty_like(out)
+    ops.groupnorm_relu(out, z, S=S, HW=H * W, C=co, cpg=16, mean=mean, rstd=rstd, gamma=gam.to(dev), beta=bet.to(dev))
+    close(z.reshape(S, H, W, co).permute(0, 3, 1, 2), y1, atol=1e-4 if dt == torch.float32 else 2e-2,
+          rtol=0 if dt == torch.float32 else 1e-2, what="gn relu")
+    hw_ = rnd(1, co, 3, 3, seed=30) / 8
+    logits = torch.full((B, T + 2, H, W), 7.0, device=dev)
+    cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32)
+    ops.conv3x3_head(out, B=B, T=T, H=H, W=W, C=co, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
+                     bias=0.25, out=logits, T_out=T + 2, classes=cls.to(dev), gn=(mean, rstd, gam.to(dev), bet.to(dev), 16))
+    rh = F.conv2d(y1, hw_.double(), torch.tensor([0.25]).double(), padding=1).reshape(B, T, H, W)
+    for bi in range(B):
+        for t in range(T):
+            close(logits[bi, cls[bi, t]], rh[bi, t], atol=1e-4 if dt == torch.float32 else 5e-2, what="head")
+
+
+# ----------------------------------------------------------------------------- small ops
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_corr_embed_topk(dt):
+    B, T, H, W, hid = 2, 40, 24, 24, 128
+    corr = rnd(T, B * H * W, seed=31) * 0.2
+    w = rnd(hid, 1, 7, 7, seed=32) / 7
+    b = rnd(hid, seed=33)
+    k = 16
+    cls = torch.empty(B, k, device=dev, dtype=torch.int32)
+    cd = corr.to(dev)
+    ops.topk_classes(cd, t_stride=B * H * W, b_stride=H * W, B=B, T=T, HW=H * W, k=k, out=cls)
+    m = corr.reshape(T, B, H * W).max(-1)[0].T   # (B, T)
+    ref_cls = m.topk(k, -1)[1]
+    assert torch.equal(torch.sort(cls.cpu().long(), -1)[0], torch.sort(ref_cls, -1)[0])
+    X = torch.empty(B * k * H * W, hid, device=dev, dtype=dt)
+    ops.corr_embed(cd, t_stride=B * H * W, b_stride=H * W, B=B, T=k, H=H, W=W, weight=w.reshape(hid, 49).to(dev),
+                   bias=b.to(dev), out=X, classes=cls)
+    c = corr.reshape(T, B, H, W).permute(1, 0, 2, 3)
+    sel = torch.stack([c[bi, cls[bi].cpu().long()] for bi in range(B)])   # (B, k, H, W)
+    ref = F.conv2d(sel.reshape(B * k, 1, H, W).double(), w.double(), b.double(), padding=3)
+    close(X.reshape(B * k, H, W, hid).permute(0, 3, 1, 2), ref, atol=1e-5 if dt == torch.float32 else 2e-2,
+          what="corr_embed")
+
+
+def test_preprocess_im2col():
+    arch_mean = torch.tensor([122.7709383, 116.7460125, 104.09373615])
+    arch_std = torch.tensor([68.5005327, 66.6321579, 70.3231630])
+    imgs = [torch.randint(0, 256, (3, 300, 352), generator=torch.Generator().manual_seed(1)).float(),
+            torch.randint(0, 256, (3, 320, 256), generator=torch.Generator().manual_seed(2)).float()]
+
+    class A:
+        clip_pixel_mean, clip_pixel_std, size_divisibility, clip_resolution = arch_mean.tolist(), arch_std.tolist(), 32, 384
+    ref, sizes = O.preprocess(A, imgs)
+    Hp, Wp = 320, 352
+    raw = torch.zeros(2, 3, Hp, Wp)
+    for i, im in enumerate(imgs):
+        raw[i, :, :im.shape[1], :im.shape[2]] = im
+    p = 16
+    out = torch.empty(2 * 24 * 24, 3 * p * p + 32, device=dev)
+    ops.preprocess_im2col(raw.to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), mean=arch_mean.to(dev),
+                          std=arch_std.to(dev), res=384, patch=p, out=out)
+    cols = F.unfold(ref, p, stride=p).transpose(1, 2).reshape(-1, 3 * p * p)
+    close(out[:, :3 * p * p], cols, atol=2e-5, what="preprocess")
+    assert out[:, 3 * p * p:].abs().max().item() == 0
+
+
+def test_bicubic_postprocess():
+    S_in, S_out, D = 14, 24, 8
+    g = rnd(S_in * S_in, D, seed=34)
+    out = torch.empty(S_out * S_out, D, device=dev)
+    ops.bicubic_resize(g.to(dev), S_in, D, out, S_out)
+    pos = torch.cat([torch.zeros(1, D), g], 0)
+    ref = O.resized_pos_embed(pos, S_in, S_out)[1:]
+    close(out, ref, atol=2e-6, what="bicubic")
+    lg = rnd(2, 3, 96, 96, seed=35) * 4
+    o = torch.empty(2, 3, 333, 250, device=dev)
+    ops.postprocess(lg.to(dev), o)
+    ref = F.interpolate(lg.sigmoid(), size=(333, 250), mode="bilinear", align_corners=False)
+    close(o, ref, atol=2e-6, what="postprocess")
+
+
+def test_text_helpers():
+    n, ctx, Wd, vocab = 3, 16, 64, 50
+    tok = torch.randint(0, vocab, (n, ctx), generator=torch.Generator().manual_seed(3)).int()
+    emb, pos = rnd(vocab, Wd, seed=36), rnd(ctx, Wd, seed=37)
+    x = torch.empty(n * ctx, Wd, device=dev)
+    ops.token_embed(tok.to(dev), emb.to(dev), pos.to(dev), x)
+    ref = emb[tok.long()] + pos
+    close(x, ref.reshape(-1, Wd), atol=1e-6, what="token_embed")
+    e = torch.empty(n, Wd, device=dev)
+    ops.eot_gather(x, tok.to(dev), e)
+    close(e, ref[torch.arange(n), tok.long().argmax(-1)], atol=1e-6, what="eot")

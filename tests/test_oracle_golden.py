@@ -16,6 +16,7 @@ CASES = {
     "e2e_tiny_pad": TINY,
     "e2e_tiny_topk_pool": TINY.replace(pooling_size=(2, 2)),
     "e2e_tiny_eval": TINY,
+    "e2e_tiny_topk": TINY,
     "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2)),
 }
 
