@@ -1,0 +1,232 @@
+"""Benchmark: CAT-Seg dense inference, images/sec @ ViT-L/14 336², 150 classes, bs=8 per GPU.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = the full eval forward of one batch of 8 synthetic images already resident in
+HBM: CLIP-normalize / pad / resize -> CLIP ViT-L/14 dense encoder -> cost volume ->
+2 aggregation layers -> guided upsampler -> sigmoid logits bilinearly upsampled to
+336² (cat_seg_model.py:147-229).  Class embeddings of the 150 ade150 prompts are
+encoded once on the GPU before timing (the predictor's eval cache,
+cat_seg_predictor.py:191-192).  With N > 1 each rank runs its own 8 images and the
+(8, 150, 96, 96) logits are all-gathered over RCCL (weak scaling).
+
+Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant
+kernel (HIP-event timed per launch on the launch stream, algorithmic FLOPs from the
+launch shapes) and the CPU baseline (the oracle, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cat-seg_amd"))
+sys.path.insert(0, ROOT)
+
+from cat_seg import ops  # noqa: E402
+from cat_seg.arch import VIT_L14_336  # noqa: E402
+from cat_seg.engine import CatSegEngine  # noqa: E402
+from cat_seg.weights import synthesize_state_dict  # noqa: E402
+
+GF_PER_IMAGE = 875.7          # reference eval forward FLOPs, L/14@336, T=150
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--classes", type=int, default=150)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
+    ap.add_argument("--cpu-images", type=int, default=2, help="oracle sample size for cpu_baseline (0 = skip)")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def class_tokens(T):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "class_tokens.npz"))
+    tok = g["ade150"] if T <= 150 else g["ade847"]
+    return torch.from_numpy(tok[:T].astype(np.int32))
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    arch = VIT_L14_336
+    B, T = args.batch, args.classes
+    R = arch.clip_resolution
+
+    sd = synthesize_state_dict(arch, seed=0)
+    eng = CatSegEngine(arch, sd, dtype=dtype, device=dev)
+    with torch.no_grad():
+        text = eng.encode_text(class_tokens(T))
+        eng.set_text(text)
+    gen = torch.Generator().manual_seed(1234 + rank)
+    pad = (R + 31) // 32 * 32
+    raw = torch.zeros(B, 3, pad, pad)
+    raw[:, :, :R, :R] = torch.rand(B, 3, R, R, generator=gen) * 255
+    raw = raw.to(dev)
+    sizes = torch.tensor([[R, R]] * B, dtype=torch.int32, device=dev)
+    out = torch.empty(B, T, R, R, device=dev)
+    gathered = torch.empty(world * B, T, 4 * arch.grid, 4 * arch.grid, device=dev) if world > 1 else None
+
+    def step():
+        logits = eng.head_logits(raw, sizes)
+        ops.postprocess(logits, out, crop=(min(logits.shape[-2], R), min(logits.shape[-1], R)))
+        return logits
+
+    stream = torch.cuda.Stream(device=dev)
+    graph = None
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        if not args.no_graph:
+            with torch.cuda.stream(stream):
+                step()            # allocate / warm the caching allocator outside capture
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                g_logits = step()
+
+        def run():
+            if graph is not None:
+                graph.replay()
+                lg = g_logits
+            else:
+                with torch.cuda.stream(stream):
+                    lg = step()
+            if world > 1:
+                with torch.cuda.stream(stream):
+                    dist.all_gather_into_tensor(gathered, lg.contiguous())
+            return lg
+
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    images = world * B * args.steps
+    value = images / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    roofline, kernels = None, None
+    if rank == 0 and not args.no_roofline:
+        roofline, kernels = roofline_pass(step, stream, dtype)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_images > 0:
+        cpu = cpu_baseline(arch, sd, text.cpu(), args.cpu_images)
+    if rank == 0:
+        path_tflops = GF_PER_IMAGE * value / 1e3
+        line = {
+            "metric": "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling",
+            "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, ade150 prompt tokens)",
+            "config": {"workload": f"CATSeg eval forward ViT-L/14@336, T={T} classes, bs={B}/GPU, "
+                                   "POOLING [1,1], sigmoid upsampled to 336x336",
+                       "global_batch": world * B, "classes": T, "resolution": R,
+                       "parallelism": f"batch-shard x{world} + RCCL all-gather of logits" if world > 1 else "1 GPU",
+                       "hipgraph": graph is not None},
+            "roofline": roofline,
+            "path_roofline": {"bound": "mfma", "achieved": round(path_tflops, 2),
+                              "peak": PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS,
+                              "unit": "TFLOP/s", "gf_per_image": GF_PER_IMAGE,
+                              "frac": round(path_tflops / (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
+                                                           else PEAK_F32_TFLOPS), 4)},
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def roofline_pass(step, stream, dtype):
+    """One eager pass with HIP events around every wrapped launch (on the launch stream)."""
+    ops.PROFILE = []
+    with torch.no_grad(), torch.cuda.stream(stream):
+        step()
+    torch.cuda.synchronize()
+    recs, ops.PROFILE = ops.PROFILE, None
+    agg = {}
+    for r in recs:
+        ms = r["start"].elapsed_time(r["end"])
+        a = agg.setdefault(r["kernel"], {"launches": 0, "ms": 0.0, "flops": 0, "bytes": 0})
+        a["launches"] += 1
+        a["ms"] += ms
+        a["flops"] += r["flops"]
+        a["bytes"] += r["bytes"]
+    top = max(agg, key=lambda k: agg[k]["ms"])
+    a = agg[top]
+    avg_s = a["ms"] / a["launches"] / 1e3
+    if a["flops"] > 0:
+        achieved = a["flops"] / a["launches"] / avg_s / 1e12
+        peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+        roof = {"bound": "mfma", "kernel": top, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2),
+                "flops_per_launch": a["flops"] // a["launches"]}
+    else:
+        achieved = a["bytes"] / a["launches"] / avg_s / 1e9
+        roof = {"bound": "hbm", "kernel": top, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2)}
+    kern = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                "tflops": round(v["flops"] / (v["ms"] / 1e3) / 1e12, 2) if v["flops"] else None}
+            for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])}
+    return roof, kern
+
+
+def cpu_baseline(arch, sd, text, n_images):
+    """The oracle (CPU fp32 restatement of the reference path) on a bounded sample."""
+    from oracle import catseg_oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(99)
+    R = arch.clip_resolution
+    inputs = [{"image": torch.rand(3, R, R, generator=gen) * 255} for _ in range(n_images)]
+    O.catseg_forward(arch, sd, inputs[:1], text.unsqueeze(1))     # warm-up
+    t0 = time.perf_counter()
+    O.catseg_forward(arch, sd, inputs, text.unsqueeze(1), all_images=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_images / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_images} images of the same workload (L/14@336, T={text.shape[0]}, fp32, one batch) "
+                      f"through oracle/catseg_oracle.py on {threads} host threads, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -108,6 +108,8 @@ class CatSegEngine:
         pw = torch.zeros(W, kp)
         pw[:, :kc] = sd[p + "conv1.weight"].reshape(W, kc)
         w.patch_w, w.patch_k = self._W(pw), kp
+        w.pix_mean = self._F(torch.tensor(a.clip_pixel_mean))
+        w.pix_std = self._F(torch.tensor(a.clip_pixel_std))
         w.cls = self._F(sd[p + "class_embedding"])
         pos = self._F(sd[p + "positional_embedding"])
         if a.grid != a.pretrain_grid:   # resized_pos_embed (model_vpt.py:316-329), on device
@@ -277,9 +279,8 @@ class CatSegEngine:
         Lt = G2 + 1
         W = a.vision_width
         cols = torch.empty(B * G2, w.patch_k, device=dev, dtype=dt)
-        mean = torch.tensor(a.clip_pixel_mean, device=dev, dtype=_f32)
-        std = torch.tensor(a.clip_pixel_std, device=dev, dtype=_f32)
-        ops.preprocess_im2col(raw, sizes, mean=mean, std=std, res=a.clip_resolution, patch=a.vision_patch, out=cols)
+        ops.preprocess_im2col(raw, sizes, mean=w.pix_mean, std=w.pix_std, res=a.clip_resolution,
+                              patch=a.vision_patch, out=cols)
         patches = torch.empty(B * G2, W, device=dev, dtype=_f32)
         ops.gemm(cols, w.patch_w, patches)
         x = torch.empty(B * Lt, W, device=dev, dtype=_f32)

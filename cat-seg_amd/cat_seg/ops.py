@@ -18,6 +18,31 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+# Optional launch recorder (bench.py's roofline pass): when a list, every wrapped launch
+# appends {"kernel", "flops", "bytes", "start", "end"} with HIP events recorded on the
+# launch stream around it.
+PROFILE: Optional[list] = None
+
+
+class _rec:
+    def __init__(self, kernel, flops=0, nbytes=0):
+        self.kernel, self.flops, self.nbytes = kernel, flops, nbytes
+
+    def __enter__(self):
+        if PROFILE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record(torch.cuda.current_stream())
+        return self
+
+    def __exit__(self, *exc):
+        if PROFILE is not None and exc[0] is None:
+            self.e1.record(torch.cuda.current_stream())
+            PROFILE.append({"kernel": self.kernel, "flops": self.flops, "bytes": self.nbytes,
+                            "start": self.e0, "end": self.e1})
+        return False
+
+
 def _dt(t: torch.Tensor) -> int:
     if t.dtype == torch.float32:
         return L.F32
@@ -64,14 +89,17 @@ def gemm(A, W, out, *, M=None, K=None, bias=None, act=L.ACT_NONE, alpha=1.0,
         a.store_mode = 1
         a.cvt_k, a.cvt_hin, a.cvt_win, a.cvt_cout = store
     a.dtype_a, a.dtype_out = _dt(A), _dt(out)
-    call("catseg_gemm", a, _stream())
+    kname = "gemm_bf16" if a.dtype_a == L.BF16 else "gemm_f32"
+    with _rec(kname, 2 * M * N * K, A.element_size() * (M * K + N * K) + out.element_size() * M * N):
+        call("catseg_gemm", a, _stream())
     return out
 
 
 def layernorm(x, gamma, beta, out, *, rows=None, inmap=None, eps=1e-5, cols=None):
     cols = cols if cols is not None else gamma.shape[0]
     rows = rows if rows is not None else out.shape[0]
-    call("catseg_layernorm", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
+    with _rec("layernorm", 0, rows * cols * (x.element_size() + out.element_size())):
+      call("catseg_layernorm", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
          gamma.data_ptr(), beta.data_ptr(), rows, cols, eps, _stream())
     return out
 
@@ -102,7 +130,8 @@ def attention(q, k, v, out, *, n_seq, seq_len, n_heads, head_dim, scale, causal=
     a.scale, a.causal = scale, int(causal)
     a.mode, a.img_h, a.img_w, a.window, a.shift = mode, img_hw[0], img_hw[1], window, shift
     a.dtype = _dt(q)
-    call("catseg_attention", a, _stream())
+    with _rec("attention_window" if mode == 1 else "attention", 4 * n_seq * n_heads * seq_len * seq_len * head_dim):
+        call("catseg_attention", a, _stream())
     return out
 
 
@@ -114,7 +143,8 @@ def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_p
     a.B, a.T, a.HW, a.n_heads, a.head_dim = B, T, HW, n_heads, head_dim
     a.n_pad, a.k_pad, a.v_pad, a.eps = n_pad, _p(k_pad), _p(v_pad), eps
     a.dtype = _dt(q)
-    call("catseg_linear_attention", a, _stream())
+    with _rec("linear_attention", 4 * B * HW * T * n_heads * head_dim * head_dim):
+        call("catseg_linear_attention", a, _stream())
     return y
 
 
@@ -140,7 +170,8 @@ def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0
     a.out = out.data_ptr()
     a.stats, a.stats_cpg = _p(stats), stats_cpg
     a.dtype = _dt(out)
-    call("catseg_conv3x3", a, _stream())
+    with _rec("conv3x3", 2 * S * H * W * weight.shape[0] * weight.shape[1]):
+        call("catseg_conv3x3", a, _stream())
     return out
 
 
