@@ -1,0 +1,176 @@
+"""CATSeg meta-architecture — the drop-in boundary of the MI355X path (reference
+cat_seg/cat_seg_model.py:18-229).
+
+`@META_ARCH_REGISTRY.register() class CATSeg`, built by `build_model(cfg)` from the
+same config keys, with `forward(batched_inputs: list[dict]) -> list[dict]`:
+  input  {"image": (3, H, W) uint8/float 0-255 (CPU or device), optional "height", "width"}
+  output {"sem_seg": (T, height, width) fp32 sigmoid probabilities on the model device}
+The reference returns results for batched_inputs[0] only (cat_seg_model.py:227-229);
+this boundary returns one result per input image by default
+(MODEL.CATSEG_HIP.RETURN_ALL_IMAGES; set False for the reference's exact behaviour).
+
+Everything between the input copy and the returned tensors runs in the HIP kernels of
+libcatseg_hip.so through `CatSegEngine`; there is no CPU or PyTorch-op fallback.
+Parameters live under the reference checkpoint keys (`state_dict()` /
+`load_state_dict()`, detectron2 `{"model": ...}` files accepted), synthesized
+deterministically when no checkpoint is given.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+from torch import nn
+
+from . import ops
+from .arch import CatSegArch, arch_from_cfg
+from .engine import CatSegEngine
+from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401  (registers the head)
+from .registry import META_ARCH_REGISTRY, build_sem_seg_head, configurable
+from .weights import synthesize_state_dict
+
+_DTYPES = {"bf16": torch.bfloat16, "f32": torch.float32, "fp32": torch.float32}
+
+
+def convert_openai_clip_keys(sd: Dict[str, torch.Tensor], prefix: str = "") -> Dict[str, torch.Tensor]:
+    """OpenAI CLIP `attn.in_proj_weight` -> q/k/v_proj_weight split (model_vpt.py:520-528)."""
+    out = {}
+    for k, v in sd.items():
+        if k.endswith("attn.in_proj_weight"):
+            q, kk, vv = v.chunk(3, dim=0)
+            out[prefix + k.replace("in_proj", "q_proj")] = q
+            out[prefix + k.replace("in_proj", "k_proj")] = kk
+            out[prefix + k.replace("in_proj", "v_proj")] = vv
+        elif k not in ("input_resolution", "context_length", "vocab_size"):
+            out[prefix + k] = v
+    return out
+
+
+@META_ARCH_REGISTRY.register()
+class CATSeg(nn.Module):
+    @configurable
+    def __init__(self, *, backbone, sem_seg_head: nn.Module, size_divisibility: int, pixel_mean: Tuple[float],
+                 pixel_std: Tuple[float], clip_pixel_mean: Tuple[float], clip_pixel_std: Tuple[float],
+                 train_class_json: str, test_class_json: str, sliding_window: bool, clip_finetune: str,
+                 backbone_multiplier: float, clip_pretrained: str, arch: Optional[CatSegArch] = None,
+                 dtype: str = "bf16", return_all_images: bool = True, synthetic_seed: int = 0):
+        super().__init__()
+        self.backbone = backbone
+        self.sem_seg_head = sem_seg_head
+        self.size_divisibility = size_divisibility
+        self.register_buffer("pixel_mean", torch.Tensor(pixel_mean).view(-1, 1, 1), False)
+        self.register_buffer("pixel_std", torch.Tensor(pixel_std).view(-1, 1, 1), False)
+        self.register_buffer("clip_pixel_mean", torch.Tensor(clip_pixel_mean).view(-1, 1, 1), False)
+        self.register_buffer("clip_pixel_std", torch.Tensor(clip_pixel_std).view(-1, 1, 1), False)
+        self.train_class_json, self.test_class_json = train_class_json, test_class_json
+        self.clip_finetune = clip_finetune
+        self.sliding_window = sliding_window
+        arch = arch or arch_from_cfg_defaults(clip_pretrained)
+        # cat_seg_model.py:78 (384 for ViT-B/16, else 336); non-reference presets keep their own
+        self.clip_resolution = ((384, 384) if clip_pretrained == "ViT-B/16" else
+                                (336, 336) if clip_pretrained.startswith("ViT-") else (arch.clip_resolution,) * 2)
+        self.arch = arch.replace(
+            clip_resolution=self.clip_resolution[0], size_divisibility=size_divisibility,
+            clip_pixel_mean=tuple(clip_pixel_mean), clip_pixel_std=tuple(clip_pixel_std))
+        self.compute_dtype = _DTYPES[dtype]
+        self.return_all_images = return_all_images
+        self._sd = synthesize_state_dict(self.arch, seed=synthetic_seed)
+        self._engine: Optional[CatSegEngine] = None
+
+    @classmethod
+    def from_config(cls, cfg):
+        hip = cfg.MODEL.get("CATSEG_HIP", {}) if hasattr(cfg.MODEL, "get") else {}
+        return {
+            "backbone": None,
+            "sem_seg_head": build_sem_seg_head(cfg, None),
+            "size_divisibility": cfg.MODEL.MASK_FORMER.SIZE_DIVISIBILITY,
+            "pixel_mean": cfg.MODEL.PIXEL_MEAN,
+            "pixel_std": cfg.MODEL.PIXEL_STD,
+            "clip_pixel_mean": cfg.MODEL.CLIP_PIXEL_MEAN,
+            "clip_pixel_std": cfg.MODEL.CLIP_PIXEL_STD,
+            "train_class_json": cfg.MODEL.SEM_SEG_HEAD.TRAIN_CLASS_JSON,
+            "test_class_json": cfg.MODEL.SEM_SEG_HEAD.TEST_CLASS_JSON,
+            "sliding_window": cfg.TEST.SLIDING_WINDOW,
+            "clip_finetune": cfg.MODEL.SEM_SEG_HEAD.CLIP_FINETUNE,
+            "backbone_multiplier": cfg.SOLVER.BACKBONE_MULTIPLIER,
+            "clip_pretrained": cfg.MODEL.SEM_SEG_HEAD.CLIP_PRETRAINED,
+            "arch": arch_from_cfg(cfg),
+            "dtype": hip.get("DTYPE", "bf16") if hip else "bf16",
+            "return_all_images": bool(hip.get("RETURN_ALL_IMAGES", True)) if hip else True,
+            "synthetic_seed": int(hip.get("SYNTHETIC_SEED", 0)) if hip else 0,
+        }
+
+    # ------------------------------------------------------------------ parameters
+    @property
+    def device(self):
+        return self.pixel_mean.device
+
+    def state_dict(self, *args, **kwargs):        # reference checkpoint keys
+        return dict(self._sd)
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        sd = state_dict.get("model", state_dict)
+        sd = {k: (v if torch.is_tensor(v) else torch.as_tensor(v)) for k, v in sd.items()}
+        if any(k.endswith("attn.in_proj_weight") for k in sd):
+            sd = convert_openai_clip_keys(sd)
+        missing = [k for k in self._sd if k not in sd]
+        unexpected = [k for k in sd if k not in self._sd]
+        if strict and (missing or unexpected):
+            raise KeyError(f"load_state_dict: missing {missing[:5]}... unexpected {unexpected[:5]}...")
+        for k in self._sd:
+            if k in sd:
+                if tuple(sd[k].shape) != tuple(self._sd[k].shape):
+                    raise ValueError(f"{k}: shape {tuple(sd[k].shape)} != {tuple(self._sd[k].shape)}")
+                self._sd[k] = sd[k].float().cpu()
+        self._engine = None
+        return missing, unexpected
+
+    @property
+    def engine(self) -> CatSegEngine:
+        if self._engine is None or self._engine.device != self.device:
+            dev = self.device if self.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+            self._engine = CatSegEngine(self.arch, self._sd, dtype=self.compute_dtype, device=dev)
+            self.sem_seg_head.predictor.attach_engine(self._engine)
+        return self._engine
+
+    # ------------------------------------------------------------------ forward
+    def _batch(self, images: List[torch.Tensor]):
+        """Stage the images into one zero-padded fp32 canvas on the device (ImageList.from_tensors
+        geometry: batch max, rounded up to size_divisibility)."""
+        d = max(self.size_divisibility, 1)
+        H = max(int(i.shape[-2]) for i in images)
+        W = max(int(i.shape[-1]) for i in images)
+        H, W = -(-H // d) * d, -(-W // d) * d
+        raw = torch.zeros(len(images), 3, H, W, dtype=torch.float32, pin_memory=True)
+        for k, im in enumerate(images):
+            raw[k, :, : im.shape[-2], : im.shape[-1]].copy_(im)
+        sizes = torch.tensor([[int(i.shape[-2]), int(i.shape[-1])] for i in images], dtype=torch.int32)
+        dev = self.engine.device
+        return raw.to(dev, non_blocking=True), sizes.to(dev), sizes.tolist()
+
+    def forward(self, batched_inputs: List[dict]):
+        if self.training:
+            raise NotImplementedError("CATSeg training is outside the MI355X inference path")
+        if self.sliding_window:
+            raise NotImplementedError("TEST.SLIDING_WINDOW: not implemented on the MI355X path yet")
+        with torch.no_grad():
+            eng = self.engine
+            self.sem_seg_head.predictor.get_text_embeds()
+            raw, sizes_dev, sizes = self._batch([x["image"] for x in batched_inputs])
+            logits = eng.head_logits(raw, sizes_dev)
+            n = len(batched_inputs) if self.return_all_images else 1
+            results = []
+            h_l, w_l = logits.shape[-2:]
+            for i in range(n):
+                ih, iw = sizes[i]
+                h = int(batched_inputs[i].get("height", ih))
+                w = int(batched_inputs[i].get("width", iw))
+                out = torch.empty(1, logits.shape[1], h, w, device=eng.device)
+                ops.postprocess(logits[i:i + 1], out, crop=(min(h_l, ih), min(w_l, iw)))
+                results.append({"sem_seg": out[0]})
+            return results
+
+
+def arch_from_cfg_defaults(clip_pretrained: str) -> CatSegArch:
+    from .arch import PRESETS
+    return PRESETS[clip_pretrained]

@@ -314,17 +314,19 @@ class CatSegEngine:
         Returns fp32 logits (B, T0, 4*grid, 4*grid)."""
         if self._text is None:
             raise RuntimeError("set_text() / encode_text() must run before the image forward")
-        a, dev, dt, w, tx = self.arch, self.device, self.dt, self.w, self._text
-        B = raw.shape[0]
+        feats, hooks = self.encode_image(raw, sizes)
+        res3, res4, res5 = self.guidance(feats, hooks)
+        return self.aggregate(feats, res3, res4, res5)
+
+    def guidance(self, feats, hooks):
+        """res3 / res4 / res5 guidance maps, NHWC in the engine dtype (cat_seg_model.py:178-186):
+        res3 = dense tokens w/o CLS, res4/res5 = ConvTranspose2d(k=s=2/4) of the hook tokens."""
+        a, dev, dt, w = self.arch, self.device, self.dt, self.w
         G = a.grid
         HW = G * G
-        Lt = HW + 1
-        D = a.hidden_dim
-        Co = a.embed_dim
-        feats, hooks = self.encode_image(raw, sizes)
-        drop_cls = rowmap(d1=HW, s1=Lt, d2=1, m2=HW, s2=1, off=1)
-        # ---- guidance sources (cat_seg_model.py:178-186) ----
-        res3 = torch.empty(B * HW, Co, device=dev, dtype=dt)
+        B = feats.shape[0] // (HW + 1)
+        drop_cls = rowmap(d1=HW, s1=HW + 1, d2=1, m2=HW, s2=1, off=1)
+        res3 = torch.empty(B * HW, a.embed_dim, device=dev, dtype=dt)
         ops.convert(feats, res3, inmap=drop_cls)
         res45 = []
         for i, (k, cout) in enumerate(((2, a.decoder_guidance_dims[0]), (4, a.decoder_guidance_dims[1]))):
@@ -333,6 +335,23 @@ class CatSegEngine:
             r = torch.empty(B * HW * k * k, cout, device=dev, dtype=dt)
             ops.gemm(hk, w[f"up{i + 1}_w"], r, bias=w[f"up{i + 1}_b"], store=(k, G, G, cout))
             res45.append(r)
+        return res3, res45[0], res45[1]
+
+    def aggregate(self, feats, res3, res4, res5) -> torch.Tensor:
+        """Aggregator.forward (model.py:683-725) on engine-layout inputs: feats fp32 (B*(1+HW), C_o)
+        dense CLIP tokens, res3 (B*HW, C_o), res4 (B*4HW, 256), res5 (B*16HW, 128) NHWC.
+        Returns fp32 logits (B, T0, 4G, 4G)."""
+        if self._text is None:
+            raise RuntimeError("set_text() / encode_text() must run before the aggregator")
+        a, dev, dt, w, tx = self.arch, self.device, self.dt, self.w, self._text
+        G = a.grid
+        HW = G * G
+        Lt = HW + 1
+        B = feats.shape[0] // Lt
+        D = a.hidden_dim
+        Co = a.embed_dim
+        res45 = [res4, res5]
+        drop_cls = rowmap(d1=HW, s1=Lt, d2=1, m2=HW, s2=1, off=1)
         # ---- cost volume (model.py:648-652) ----
         fn = torch.empty(B * HW, Co, device=dev, dtype=dt)
         ops.l2normalize(feats, fn, inmap=drop_cls)

@@ -1,0 +1,111 @@
+"""CPU tests of the host side: config surface, registry/build_model, the C-ABI library
+exports, loud failure without a GPU, the tokenizer and the weight synthesizer."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from cat_seg import CATSeg, add_cat_seg_config, build_model, get_cfg
+from cat_seg import _lib as L
+from cat_seg.arch import TINY, VIT_L14_336
+from cat_seg.weights import synthesize_state_dict
+
+from conftest import GOLDEN, ROOT
+
+REF_VOCAB = "/root/reference/cat_seg/third_party/bpe_simple_vocab_16e6.txt.gz"
+
+
+def tiny_cfg(**over):
+    cfg = get_cfg()
+    add_cat_seg_config(cfg)
+    cfg.merge_from_file(os.path.join(ROOT, "cat-seg_amd", "configs", "vitb_384.yaml"))
+    cfg.merge_from_list(["MODEL.SEM_SEG_HEAD.POOLING_SIZES", "[1,1]", "MODEL.SEM_SEG_HEAD.CLIP_PRETRAINED", "tiny",
+                         "MODEL.SEM_SEG_HEAD.TEXT_GUIDANCE_DIM", "96", "MODEL.SEM_SEG_HEAD.APPEARANCE_GUIDANCE_DIM",
+                         "96", "MODEL.CATSEG_HIP.DTYPE", "f32"])
+    for k, v in over.items():
+        cfg.merge_from_list([k, v])
+    return cfg
+
+
+def test_config_base_and_overrides():
+    cfg = tiny_cfg()
+    assert cfg.MODEL.META_ARCHITECTURE == "CATSeg"
+    assert list(cfg.MODEL.SEM_SEG_HEAD.POOLING_SIZES) == [1, 1]
+    assert cfg.MODEL.MASK_FORMER.SIZE_DIVISIBILITY == 32
+    assert cfg.MODEL.CLIP_PIXEL_MEAN[0] == pytest.approx(122.7709383)
+    assert cfg.TEST.SLIDING_WINDOW is False
+
+
+def test_build_model_registry_and_state_dict_keys():
+    m = build_model(tiny_cfg())
+    assert isinstance(m, CATSeg)
+    sd = m.state_dict()
+    assert "sem_seg_head.predictor.clip_model.visual.transformer.resblocks.0.attn.q_proj_weight" in sd
+    assert "sem_seg_head.predictor.transformer.layers.1.swin_block.block_2.attn.q.weight" in sd
+    assert "upsample1.weight" in sd
+    # round trip + OpenAI in_proj format accepted
+    m.load_state_dict({"model": sd})
+    with pytest.raises(KeyError):
+        m.load_state_dict({"bogus": torch.zeros(1)})
+
+
+def test_forward_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    m = build_model(tiny_cfg()).eval()
+    with pytest.raises(RuntimeError):
+        m([{"image": torch.zeros(3, 64, 64)}])
+
+
+def test_capi_library_exports_every_header_symbol():
+    hdr = open(os.path.join(ROOT, "include", "catseg_hip.h")).read()
+    declared = set(re.findall(r"\b(catseg_[a-z0-9_]+)\s*\(", hdr))
+    lib = L.load()
+    missing = [s for s in sorted(declared) if not hasattr(lib, s)]
+    assert not missing, missing
+    assert declared <= set(L.EXPORTED) | {"catseg_conv3x3_head_gn"}
+    assert lib.catseg_abi_version() == 1
+    assert lib.catseg_conv_tile_rows() == 128
+
+
+def test_capi_argument_validation_without_gpu():
+    """Host-side checks reject bad shapes before any launch (no GPU needed)."""
+    a = L.GemmArgs()
+    a.A, a.W, a.out = 16, 16, 16
+    a.M, a.N, a.K = 8, 6, 8          # N % 4 != 0
+    a.amap = L.IDENTITY
+    lib = L.load()
+    assert lib.catseg_gemm(a, None) == -1
+    assert b"multiple of 4" in lib.catseg_last_error()
+
+
+def test_weight_synthesizer_deterministic():
+    a = synthesize_state_dict(TINY, seed=0)
+    b = synthesize_state_dict(TINY, seed=0)
+    c = synthesize_state_dict(TINY, seed=1)
+    k = "sem_seg_head.predictor.transformer.conv1.weight"
+    assert torch.equal(a[k], b[k]) and not torch.equal(a[k], c[k])
+    # fingerprint pinned so the GPU box regenerates exactly the fixtures' weights
+    assert abs(float(a[k].double().sum()) - float(np.load(os.path.join(GOLDEN, "synth_fingerprint.npy")))) < 1e-9
+
+
+@pytest.mark.skipif(not os.path.exists(REF_VOCAB), reason="CLIP BPE vocabulary not present")
+def test_tokenizer_matches_reference_token_ids():
+    import json
+    from cat_seg.tokenizer import BPETokenizer, class_prompts
+    tok = BPETokenizer(REF_VOCAB)
+    g = np.load(os.path.join(GOLDEN, "class_tokens.npz"))
+    for ds in ("voc20", "ade150", "pc459", "ade847"):
+        names = json.load(open(f"/root/reference/datasets/{ds}.json"))
+        np.testing.assert_array_equal(tok.tokenize(class_prompts(names)), g[ds].astype(np.int64))
+
+
+def test_bundled_tokens_for_reference_lists():
+    from cat_seg.modeling.transformer.cat_seg_predictor import bundled_tokens
+    assert bundled_tokens(["not", "a", "reference", "list"]) is None
+    if os.path.exists("/root/reference/datasets/voc20.json"):
+        import json
+        names = json.load(open("/root/reference/datasets/voc20.json"))
+        np.testing.assert_array_equal(bundled_tokens(names), np.load(os.path.join(GOLDEN, "class_tokens.npz"))["voc20"])

@@ -1,0 +1,50 @@
+"""The drop-in boundary on the GPU: build_model(cfg) -> CATSeg.forward(list[dict]) vs the
+reference golden vectors (sem_seg of image 0) and vs the oracle for every image."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cat_seg import build_model
+from oracle import catseg_oracle as O
+
+from conftest import GOLDEN
+from test_boundary_cpu import tiny_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_catseg_forward_matches_golden(dtype):
+    g = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_pad.npz")))
+    cfg = tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": dtype})
+    model = build_model(cfg).cuda().eval()
+    model.sem_seg_head.predictor.set_class_tokens(g["tokens"])
+    model.arch = model.arch.replace(pad_len=int(g["pad_len"]))
+    model._engine = None
+    imgs = [torch.from_numpy(g[k]) for k in sorted(k for k in g if k.startswith("image"))]  # uint8 CPU
+    out = model([{"image": im} for im in imgs])
+    assert len(out) == len(imgs)
+    got0 = out[0]["sem_seg"]
+    assert got0.shape == (10, imgs[0].shape[1], imgs[0].shape[2]) and got0.device.type == "cuda"
+    err = (got0[:, ::8, ::8].cpu() - torch.from_numpy(g["sem_seg0_sub"])).abs()
+    tol = 1e-3 if dtype == "f32" else 2e-2
+    assert err.max().item() < tol, err.max().item()
+    # every image vs the oracle (the reference returns image 0 only; the batched boundary returns all)
+    sd = model.state_dict()
+    text = O.text_embeds(model.arch, sd, torch.from_numpy(g["tokens"]))
+    ref = O.catseg_forward(model.arch, sd, [{"image": im} for im in imgs], text, all_images=True)
+    for r, o in zip(ref, out):
+        e = (o["sem_seg"].cpu() - r["sem_seg"]).abs().max().item()
+        assert e < tol, e
+
+
+def test_catseg_height_width_and_reference_mode():
+    cfg = tiny_cfg(**{"MODEL.CATSEG_HIP.RETURN_ALL_IMAGES": "False"})
+    model = build_model(cfg).cuda().eval()
+    g = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_eval.npz")))
+    model.sem_seg_head.predictor.set_class_tokens(g["tokens"])
+    im = torch.from_numpy(g["image0"]).float().cuda()
+    out = model([{"image": im, "height": 200, "width": 300}, {"image": im}])
+    assert len(out) == 1 and out[0]["sem_seg"].shape == (20, 200, 300)
