@@ -67,6 +67,18 @@ class LinAttnArgs(C.Structure):
     ]
 
 
+class RowsEpi(C.Structure):
+    _fields_ = [
+        ("bias", vp),
+        ("add", vp), ("ld_add", i64), ("addmap", RowMap), ("add_ncols", i64),
+        ("act", i32),
+        ("res", vp), ("ld_res", i64),
+        ("res2", vp), ("ld_res2", i64),
+        ("out", vp), ("ldo", i64),
+        ("store_mode", i32), ("cvt_k", i32), ("cvt_hin", i32), ("cvt_win", i32), ("cvt_cout", i32),
+    ]
+
+
 class ConvArgs(C.Structure):
     _fields_ = [
         ("src1", vp), ("s1_slice_stride", i64), ("s1_offset", i64), ("c1", i32),
@@ -83,6 +95,8 @@ class ConvArgs(C.Structure):
 # name -> (argtypes); every entry returns int
 _SIGS = {
     "catseg_gemm": [C.POINTER(GemmArgs), vp],
+    "catseg_rows_gemm": [vp, i64, i64, vp, vp, f32, vp, i64, C.POINTER(RowsEpi), i32, vp],
+    "catseg_rows_mlp": [vp, i64, i64, vp, vp, f32, vp, vp, i64, i32, vp, C.POINTER(RowsEpi), i32, vp],
     "catseg_layernorm": [vp, i64, RowMap, i32, vp, i64, i32, vp, vp, i64, i64, f32, vp],
     "catseg_l2normalize": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, f32, vp],
     "catseg_attention": [C.POINTER(AttnArgs), vp],

@@ -391,10 +391,8 @@ class CatSegEngine:
             tgqk = tx.tgqk
             tmap = rowmap(d1=HW, m1=T)
         # ---- aggregation layers (model.py:717-718) ----
-        h = torch.empty(R, D, device=dev, dtype=dt)
         qkv = torch.empty(R, 3 * D, device=dev, dtype=dt)
         o = torch.empty(R, D, device=dev, dtype=dt)
-        hid = torch.empty(R, 4 * D, device=dev, dtype=dt)
         Y = torch.empty(R, D, device=dev, dtype=dt)
         gn = torch.empty(B * HW, D, device=dev, dtype=dt)
         gqk = torch.empty(B * HW, 2 * D, device=dev, dtype=dt)
@@ -411,25 +409,24 @@ class CatSegEngine:
             for name, shift in (("block_1", 0), ("block_2", shift2)):
                 blk = lay[name]
                 ops.gemm(gn, blk.wqk_g, gqk)                   # W_g . LN(g): per image
-                ops.layernorm(X, blk.n1w, blk.n1b, h)
-                ops.gemm(h, blk.wqkv, qkv, bias=blk.bqkv, add=gqk, addmap=gmap, add_ncols=2 * D)
+                # LN1 + [q|k|v] projection + guidance half, one pass over X
+                ops.rows_gemm(X, blk.wqkv, qkv, ln=(blk.n1w, blk.n1b), bias=blk.bqkv, add=gqk, addmap=gmap,
+                              add_ncols=2 * D)
                 ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, n_seq=S * nwin, seq_len=ws * ws,
                               n_heads=a.nheads, head_dim=D // a.nheads, scale=(D // a.nheads) ** -0.5, mode=1,
                               img_hw=(H_, W_), window=ws, shift=shift)
-                ops.gemm(o, blk.wproj, X, bias=blk.bproj, res=X)
-                ops.layernorm(X, blk.n2w, blk.n2b, h)
-                ops.gemm(h, blk.wfc1, hid, bias=blk.bfc1, act=L.ACT_GELU)
-                ops.gemm(hid, blk.wfc2, X, bias=blk.bfc2, res=X)
+                ops.rows_gemm(o, blk.wproj, X, bias=blk.bproj, res=X)          # x = shortcut + proj(attn)
+                ops.rows_mlp(X, blk.wfc1, blk.bfc1, blk.wfc2, X, ln=(blk.n2w, blk.n2b), b2=blk.bfc2,
+                             act=L.ACT_GELU, res=X)                              # x = x + Mlp(norm2(x))
             ca = lay.ca
-            ops.layernorm(X, ca.n1w, ca.n1b, h)
-            ops.gemm(h, ca.wqkv, qkv, bias=ca.bqkv, add=tgqk[l], addmap=tmap, add_ncols=2 * D)
+            ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
+                          add_ncols=2 * D)
             ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
                                  n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
                                  k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
-            ops.layernorm(Y, ca.n2w, ca.n2b, h)
-            ops.gemm(h, ca.w0, hid, bias=ca.b0, act=L.ACT_RELU)
-            ops.gemm(hid, ca.w2, X, bias=ca.b2, res=Y, res2=X)   # x + (x_pool + MLP) (model.py:413,423)
-        del h, qkv, o, hid, Y, gn, gqk
+            # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
+            ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y, res2=X)
+        del qkv, o, Y, gn, gqk
         # ---- guided upsampler (model.py:674-681, 540-555) ----
         src, Hc = X, G
         tile = ops.conv_tile_rows()
@@ -437,7 +434,10 @@ class CatSegEngine:
             cu = dec.up_c
             Ho = Hc * 2
             up = torch.empty(S * Ho * Ho, cu, device=dev, dtype=dt)
-            ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+            if src.shape[1] == 128 and dec.up_w.shape[0] % 128 == 0:
+                ops.rows_gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+            else:
+                ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
             cout = dec.c0.shape[0]
             groups = cout // 16
             tiles = Ho * Ho // tile

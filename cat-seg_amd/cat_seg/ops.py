@@ -11,7 +11,7 @@ from typing import Optional
 import torch
 
 from . import _lib as L
-from ._lib import call, rowmap, IDENTITY
+from ._lib import rowmap, IDENTITY
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -30,17 +30,31 @@ class _rec:
 
     def __enter__(self):
         if PROFILE is not None:
+            _ACTIVE[0] = True
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
             self.e0.record(torch.cuda.current_stream())
         return self
 
     def __exit__(self, *exc):
-        if PROFILE is not None and exc[0] is None:
-            self.e1.record(torch.cuda.current_stream())
-            PROFILE.append({"kernel": self.kernel, "flops": self.flops, "bytes": self.nbytes,
-                            "start": self.e0, "end": self.e1})
+        if PROFILE is not None:
+            _ACTIVE[0] = False
+            if exc[0] is None:
+                self.e1.record(torch.cuda.current_stream())
+                PROFILE.append({"kernel": self.kernel, "flops": self.flops, "bytes": self.nbytes,
+                                "start": self.e0, "end": self.e1})
         return False
+
+
+_ACTIVE = [False]
+
+
+def call(name, *args):
+    """Launch through the C ABI; under PROFILE, launches without their own record get one."""
+    if PROFILE is None or _ACTIVE[0]:
+        return L.call(name, *args)
+    with _rec(name[len("catseg_"):]):
+        return L.call(name, *args)
 
 
 def _dt(t: torch.Tensor) -> int:
@@ -260,4 +274,48 @@ def token_embed(tokens, tok_emb, pos, out):
 def eot_gather(x, tokens, out):
     n, ctx = tokens.shape
     call("catseg_eot_gather", x.data_ptr(), tokens.data_ptr(), n, ctx, out.shape[-1], out.data_ptr(), _stream())
+    return out
+
+
+def _rows_epi(out, bias, add, addmap, add_ncols, act, res, res2, store):
+    e = L.RowsEpi()
+    e.bias = _p(bias)
+    e.addmap = addmap or IDENTITY
+    if add is not None:
+        e.add, e.ld_add = add.data_ptr(), _ld(add)
+        e.add_ncols = add_ncols if add_ncols is not None else add.shape[-1]
+    e.act = act
+    if res is not None:
+        e.res, e.ld_res = res.data_ptr(), _ld(res)
+    if res2 is not None:
+        e.res2, e.ld_res2 = res2.data_ptr(), _ld(res2)
+    e.out = out.data_ptr()
+    if store is None:
+        e.ldo = _ld(out)
+    else:
+        e.store_mode = 1
+        e.cvt_k, e.cvt_hin, e.cvt_win, e.cvt_cout = store
+    return e
+
+
+def rows_gemm(x, w, out, *, ln=None, eps=1e-5, bias=None, add=None, addmap=None, add_ncols=None,
+              act=L.ACT_NONE, res=None, res2=None, store=None, M=None):
+    """out = epi(LN?(x) . w^T) over 128-wide rows (catseg_rows_gemm)."""
+    M = M if M is not None else x.shape[0]
+    N = w.shape[0]
+    e = _rows_epi(out, bias, add, addmap, add_ncols, act, res, res2, store)
+    g, b = (ln if ln is not None else (None, None))
+    with _rec("rows_gemm", 2 * M * N * w.shape[1], x.element_size() * M * (w.shape[1] + N)):
+        call("catseg_rows_gemm", x.data_ptr(), _ld(x), M, _p(g), _p(b), eps, w.data_ptr(), N, e, _dt(x), _stream())
+    return out
+
+
+def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=None, eps=1e-5, M=None):
+    """out = act(LN(y) . w1^T + b1) . w2^T + b2 + res + res2 (catseg_rows_mlp)."""
+    M = M if M is not None else y.shape[0]
+    hidden = w1.shape[0]
+    e = _rows_epi(out, b2, None, None, None, L.ACT_NONE, res, res2, None)
+    with _rec("rows_mlp", 4 * M * hidden * w1.shape[1], y.element_size() * M * 2 * w1.shape[1]):
+        call("catseg_rows_mlp", y.data_ptr(), _ld(y), M, ln[0].data_ptr(), ln[1].data_ptr(), eps, w1.data_ptr(),
+             b1.data_ptr(), hidden, act, w2.data_ptr(), e, _dt(y), _stream())
     return out

@@ -65,6 +65,40 @@ typedef struct {
 } CatsegGemmArgs;
 int catseg_gemm(const CatsegGemmArgs* args, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Row-block kernels over the 128-channel cost-embedding rows (K = 128).
+ * Epilogue (applied on full output rows, 16-byte vectors): v = acc + bias[n]
+ * (+ add[addmap(m), n < add_ncols]); v = act(v); v += res[m, n] + res2[m, n];
+ * stored row-major (ldo) or ConvTranspose-scattered (store_mode 1, as catseg_gemm).
+ * add/res/res2/out have the kernel dtype; bias is fp32.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const float* bias;
+  const void* add; int64_t ld_add; CatsegRowMap addmap; int64_t add_ncols;
+  int act;
+  const void* res; int64_t ld_res;
+  const void* res2; int64_t ld_res2;
+  void* out; int64_t ldo;
+  int store_mode; int cvt_k, cvt_hin, cvt_win, cvt_cout;
+} CatsegRowsEpi;
+
+/* catseg_rows_gemm — out = epi(LN?(X) . W^T), X: [M][128], W: [N][128].  LayerNorm
+ * (ln_gamma/ln_beta, eps; NULL = none) is applied to X on load.  Replaces LN + q/k/v of
+ * SwinTransformerBlock / AttentionLayer (model.py:191-196, 94-96, 344-346, 412), the
+ * Swin output proj + residual (:112, :222) and the decoder ConvTranspose2d (:546). */
+int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const float* ln_gamma,
+                     const float* ln_beta, float eps, const void* w, int64_t N,
+                     const CatsegRowsEpi* epi, int dtype, void* stream);
+
+/* catseg_rows_mlp — out = epi(act(LN(Y) . W1^T + b1) . W2^T): the whole token MLP with
+ * the hidden activations kept on chip.  Y: [M][128], W1: [hidden][128], b1 fp32,
+ * W2: [128][hidden], epi.bias = b2.  Replaces timm Mlp after norm2 (model.py:223, GELU)
+ * and the class-attention MLP (model.py:362-366,413, ReLU). */
+int catseg_rows_mlp(const void* y, int64_t ld_y, int64_t M, const float* ln_gamma,
+                    const float* ln_beta, float eps, const void* w1, const float* b1,
+                    int64_t hidden, int act, const void* w2, const CatsegRowsEpi* epi,
+                    int dtype, void* stream);
+
 /* catseg_layernorm — LayerNorm over the last dim (fp32 math).  Replaces
  * model_vpt.py:156-162 (ln_pre/ln_1/ln_2/ln_post/ln_final) and the nn.LayerNorm of
  * model.py:152,158,233,368-369.  in rows use `inmap`. */

@@ -292,6 +292,66 @@ def test_bicubic_postprocess():
     close(o, ref, atol=2e-6, what="postprocess")
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M", [300, 1000])
+def test_rows_gemm_ln_add_res_and_convt(dt, M):
+    D, N = 128, 384
+    x = rnd(M, D, seed=40) * 2 + 0.3
+    g, b = rnd(D, seed=41) + 1, rnd(D, seed=42)
+    w = rnd(N, D, seed=43) / math.sqrt(D)
+    bias = rnd(N, seed=44)
+    add = rnd(M // 10 + 1, 256, seed=45)
+    res = rnd(M, N, seed=46)
+    amap = rowmap(d1=10)                        # row m -> add row m // 10
+    out = torch.empty(M, N, device=dev, dtype=dt)
+    ops.rows_gemm(x.to(dev, dt), w.to(dev, dt), out, ln=(g.to(dev), b.to(dev)), bias=bias.to(dev),
+                  add=add.to(dev, dt), addmap=amap, add_ncols=256, act=L.ACT_GELU, res=res.to(dev, dt))
+    xn = F.layer_norm(x.to(dt).double(), (D,), g.double(), b.double(), 1e-5)
+    v = xn.to(dt).double() @ w.to(dt).double().T + bias.double()
+    v[:, :256] += add.to(dt).double()[torch.arange(M) // 10]
+    ref = F.gelu(v) + res.to(dt).double()
+    close(out, ref, atol=5e-5 if dt == torch.float32 else 4e-2, rtol=0 if dt == torch.float32 else 1e-2,
+          what="rows_gemm")
+    # ConvTranspose scatter store, no LN
+    S, H, W_, co = 3, 4, 5, 96
+    xs = rnd(S * H * W_, D, seed=47)
+    wt = rnd(D, co, 2, 2, seed=48) / 8
+    bt = rnd(co, seed=49)
+    Wg = wt.permute(2, 3, 1, 0).reshape(4 * co, D).contiguous()
+    o2 = torch.empty(S * 4 * H * W_, co, device=dev, dtype=dt)
+    ops.rows_gemm(xs.to(dev, dt), Wg.to(dev, dt), o2, bias=bt.repeat(4).to(dev), store=(2, H, W_, co))
+    ref2 = F.conv_transpose2d(xs.to(dt).double().reshape(S, H, W_, D).permute(0, 3, 1, 2), wt.to(dt).double(),
+                              bt.double(), stride=2)
+    close(o2.reshape(S, 2 * H, 2 * W_, co).permute(0, 3, 1, 2), ref2, atol=2e-5 if dt == torch.float32 else 2e-2,
+          what="rows convT")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
+def test_rows_mlp(dt, act):
+    M, D, Hd = 700, 128, 512
+    y = rnd(M, D, seed=50) * 2
+    g, b = rnd(D, seed=51) + 1, rnd(D, seed=52)
+    w1, b1 = rnd(Hd, D, seed=53) / math.sqrt(D), rnd(Hd, seed=54)
+    w2, b2 = rnd(D, Hd, seed=55) / math.sqrt(Hd), rnd(D, seed=56)
+    x = rnd(M, D, seed=57)
+    yd, xd = y.to(dev, dt), x.to(dev, dt)
+    out = torch.empty_like(xd)
+    ops.rows_mlp(yd, w1.to(dev, dt), b1.to(dev), w2.to(dev, dt), out, ln=(g.to(dev), b.to(dev)), b2=b2.to(dev),
+                 act=act, res=yd, res2=xd)
+    yn = F.layer_norm(y.to(dt).double(), (D,), g.double(), b.double(), 1e-5).to(dt).double()
+    fn = F.gelu if act == L.ACT_GELU else F.relu
+    h = fn(yn @ w1.to(dt).double().T + b1.double()).to(dt).double()
+    ref = h @ w2.to(dt).double().T + b2.double() + y.to(dt).double() + x.to(dt).double()
+    close(out, ref, atol=5e-5 if dt == torch.float32 else 4e-2, rtol=0 if dt == torch.float32 else 1e-2,
+          what="rows_mlp")
+    # in place (out aliases the residual), as the engine uses it
+    ops.rows_mlp(yd, w1.to(dev, dt), b1.to(dev), w2.to(dev, dt), yd, ln=(g.to(dev), b.to(dev)), b2=b2.to(dev),
+                 act=act, res=yd)
+    close(yd, ref - x.to(dt).double(), atol=5e-5 if dt == torch.float32 else 4e-2,
+          rtol=0 if dt == torch.float32 else 1e-2, what="rows_mlp in place")
+
+
 def test_text_helpers():
     n, ctx, Wd, vocab = 3, 16, 64, 50
     tok = torch.randint(0, vocab, (n, ctx), generator=torch.Generator().manual_seed(3)).int()
