@@ -118,6 +118,7 @@ _SIGS = {
     "catseg_postprocess": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
     "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
+    "catseg_set_persistent": [i32],
     "catseg_abi_version": [],
     "catseg_last_error": [],
 }
@@ -140,7 +141,8 @@ def load() -> C.CDLL:
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = C.c_char_p if name == "catseg_last_error" else C.c_int
+        fn.restype = (C.c_char_p if name == "catseg_last_error" else
+                      None if name == "catseg_set_persistent" else C.c_int)
     _lib = lib
     return lib
 

@@ -1,24 +1,25 @@
 // Flash-style softmax attention for gfx950 (MFMA, online softmax, LDS-staged K/V).
 //
-// One workgroup = NW waves = 16*NW queries of one (sequence, head).  Each wave owns
-// 16 queries and computes S^T = K . Q^T per 16-key tile, so the 16x16 C/D layout puts
-// ONE query per lane column (col = lane & 15) and 4 keys per register group
-// (row = 4*(lane>>4) + r): the per-query max / sum need only the two xor-16/32
-// shuffles, and the exponentiated tile is already the B operand of O^T = V^T . P^T
-// (k order permuted inside each 32-key step; V^T is read from LDS in the same
-// permuted order — cdna_hip_programming.md §3 "An accumulator tile as the next
-// MFMA's operand").  K tiles are stored [key][d], V tiles transposed [d][key].
+// One workgroup = NW waves; each wave owns QT query tiles of 16 queries of one
+// (sequence, head), so one staged K/V block serves 16*NW*QT queries.  Per 16-key tile
+// a wave computes S^T = K . Q^T: the 16x16 C/D layout then puts ONE query per lane
+// column (col = lane & 15) and 4 keys per register group (row = 4*(lane>>4) + r), so
+// the per-query max / sum need only the two xor-16/32 shuffles, and the exponentiated
+// tile is already the B operand of O^T = V^T . P^T (k order permuted inside each 32-key
+// step; V^T is read from LDS in the same permuted order — cdna_hip_programming.md §3
+// "An accumulator tile as the next MFMA's operand").  K tiles are stored [key][d],
+// V tiles transposed [d][key].
 //
 // mode 0: dense sequences (CLIP ViT MHA, model_vpt.py:202-206; causal text encoder,
-//         model_vpt.py:400-406).
+//         model_vpt.py:400-406).  KB = 64-key blocks, online softmax across blocks.
 // mode 1: Swin windows with cyclic shift + -100 region mask (model.py:86-114,
-//         161-216); the roll/partition/reverse are folded into the row index.
+//         161-216); the roll/partition/reverse are folded into the row index.  The
+//         whole 144-key window is one block (KB = 160), so one workgroup does all 144
+//         queries of a (window, head) from a single K/V staging.
 #include "common.h"
 #include "capi.h"
 
 namespace {
-
-constexpr int KB = 64;   // keys per LDS block
 
 struct AttnP {
   const void* q; const void* k; const void* v; int64_t ld;
@@ -37,59 +38,69 @@ DEV int64_t seq_row(const AttnP& p, int64_t s, int i) {
   return slice * (int64_t)p.img_h * p.img_w + (int64_t)y * p.img_w + x;
 }
 
-DEV int swin_region(const AttnP& p, int s_local_w, int i) {
+DEV int swin_region(const AttnP& p, int wloc, int i) {
   const int nwx = p.img_w / p.ws;
-  const int Y = (s_local_w / nwx) * p.ws + i / p.ws, X = (s_local_w % nwx) * p.ws + i % p.ws;
+  const int Y = (wloc / nwx) * p.ws + i / p.ws, X = (wloc % nwx) * p.ws + i % p.ws;
   const int hb = Y < p.img_h - p.ws ? 0 : (Y < p.img_h - p.shift ? 1 : 2);
   const int wb = X < p.img_w - p.ws ? 0 : (X < p.img_w - p.shift ? 1 : 2);
   return hb * 3 + wb;
 }
 
-template <typename T, int D, int NW>
+template <typename T, int D, int NW, int KB, int QT>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   constexpr int NT = NW * 64;
   constexpr int VN = Vec16<T>::N;
   constexpr int KP = D + (sizeof(T) == 2 ? 8 : 4);     // K row stride (elements)
   constexpr int VP = KB + 4;                            // V^T row stride
   constexpr int DT = D / 16;                            // d tiles of O^T
+  constexpr int KT = KB / 16;                           // key tiles per block
+  constexpr int QF = sizeof(T) == 2 ? D / 32 : D / 4;
+  using QFrag = typename std::conditional<sizeof(T) == 2, s16x8, float>::type;
   __shared__ __attribute__((aligned(16))) T Ks[KB * KP];
   __shared__ __attribute__((aligned(16))) T Vt[D * VP];
+  __shared__ signed char kreg_s[KB];                    // SW-MSA region id of each staged key
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t s = blockIdx.y / p.H;
   const int h = blockIdx.y % p.H;
-  const int q0 = blockIdx.x * 16 * NW + wave * 16;
-  const int qi = q0 + (lane & 15);            // this lane's query (column)
   const int g = lane >> 4;
-  const bool q_ok = qi < p.L;
-  const int64_t qrow = seq_row(p, s, q_ok ? qi : 0);
-  const T* Q = reinterpret_cast<const T*>(p.q) + qrow * p.ld + h * D;
   const T* Kg = reinterpret_cast<const T*>(p.k);
   const T* Vg = reinterpret_cast<const T*>(p.v);
   const int nwin = p.mode == 1 ? (p.img_h / p.ws) * (p.img_w / p.ws) : 1;
   const int wloc = p.mode == 1 ? (int)(s % nwin) : 0;
   const bool swmask = p.mode == 1 && p.shift > 0;
-  const int qreg = swmask ? swin_region(p, wloc, q_ok ? qi : 0) : 0;
-
-  // Q fragments (B operand of S^T = K Q^T)
-  constexpr int QF = sizeof(T) == 2 ? D / 32 : D / 4;
-  typename std::conditional<sizeof(T) == 2, s16x8, float>::type qf[QF];
-  if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int ks = 0; ks < QF; ++ks) {
-      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
-      qf[ks] = *reinterpret_cast<s16x8*>(&u);
-    }
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < QF; ++ks) qf[ks] = q_ok ? to_f<T>(Q[4 * ks + g]) : 0.f;
-  }
-
-  f32x4 o[DT];
-#pragma unroll
-  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f, l_run = 0.f;
   const float sl2 = p.scale * 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
+
+  int qi[QT], qreg[QT];
+  int64_t qrow[QT];
+  bool q_ok[QT], tile_live[QT];
+  QFrag qf[QT][QF];
+  f32x4 o[QT][DT];
+  float m_run[QT], l_run[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int q0 = (blockIdx.x * NW * QT + wave * QT + t) * 16;
+    tile_live[t] = q0 < p.L;
+    qi[t] = q0 + (lane & 15);
+    q_ok[t] = qi[t] < p.L;
+    qrow[t] = seq_row(p, s, q_ok[t] ? qi[t] : 0);
+    qreg[t] = swmask ? swin_region(p, wloc, q_ok[t] ? qi[t] : 0) : 0;
+    const T* Q = reinterpret_cast<const T*>(p.q) + qrow[t] * p.ld + h * D;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < QF; ++ks) {
+        uint4 u = q_ok[t] ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+        qf[t][ks] = *reinterpret_cast<s16x8*>(&u);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < QF; ++ks) qf[t][ks] = q_ok[t] ? to_f<T>(Q[4 * ks + g]) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run[t] = -1e30f;
+    l_run[t] = 0.f;
+  }
 
   const int nblk = (p.L + KB - 1) / KB;
   for (int blk = 0; blk < nblk; ++blk) {
@@ -109,120 +120,131 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
       const T* ve = reinterpret_cast<const T*>(&vu);
 #pragma unroll
       for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
+      if (swmask && d0 == 0) kreg_s[kk] = key < p.L ? (signed char)swin_region(p, wloc, key) : (signed char)-1;
     }
     __syncthreads();
 
-    // ---- S^T tiles ----
-    f32x4 st[KB / 16];
 #pragma unroll
-    for (int kt = 0; kt < KB / 16; ++kt) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      const int kr = kt * 16 + (lane & 15);
+    for (int t = 0; t < QT; ++t) {
+      if (!tile_live[t]) continue;
+      // ---- S^T tiles ----
+      f32x4 st[KT];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        const int kr = kt * 16 + (lane & 15);
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int ks = 0; ks < QF; ++ks) {
+            const s16x8 kf = *reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]);
+            a = mfma_bf16(kf, qf[t][ks], a);
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < QF; ++ks) a = mfma_f32(to_f<T>(Ks[kr * KP + 4 * ks + g]), qf[t][ks], a);
+        }
+        st[kt] = a;
+      }
+      // ---- mask + online softmax (per query column) ----
+      float bmax = -1e30f;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kt * 16 + 4 * g + r;
+          float x = st[kt][r] * sl2;
+          if (key >= p.L || (p.causal && key > qi[t])) x = -INFINITY;
+          else if (swmask && kreg_s[kt * 16 + 4 * g + r] != qreg[t]) x += -100.f * 1.4426950408889634f;
+          st[kt][r] = x;
+          bmax = fmaxf(bmax, x);
+        }
+      }
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      const float m_new = fmaxf(m_run[t], bmax);
+      const float alpha = exp2f(m_run[t] - m_new);
+      m_run[t] = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(st[kt][r] - m_new);
+          st[kt][r] = e;
+          psum += e;
+        }
+      l_run[t] = l_run[t] * alpha + psum;
+#pragma unroll
+      for (int i = 0; i < DT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[t][i][r] *= alpha;
+
+      // ---- O^T += V^T . P^T ----
       if constexpr (sizeof(T) == 2) {
 #pragma unroll
-        for (int ks = 0; ks < QF; ++ks) {
-          s16x8 kf = *reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]);
-          a = mfma_bf16(kf, qf[ks], a);
+        for (int u = 0; u < KB / 32; ++u) {
+          s16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pb[j] = (short)f2bf(st[2 * u][j]);
+            pb[4 + j] = (short)f2bf(st[2 * u + 1][j]);
+          }
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const T* vr = &Vt[(dt * 16 + (lane & 15)) * VP + 32 * u + 4 * g];
+            const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+            const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+            uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            o[t][dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[t][dt]);
+          }
         }
       } else {
 #pragma unroll
-        for (int ks = 0; ks < QF; ++ks) a = mfma_f32(to_f<T>(Ks[kr * KP + 4 * ks + g]), qf[ks], a);
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              const float va = to_f<T>(Vt[(dt * 16 + (lane & 15)) * VP + kt * 16 + 4 * g + r]);
+              o[t][dt] = mfma_f32(va, st[kt][r], o[t][dt]);
+            }
       }
-      st[kt] = a;
-    }
-    // ---- mask + online softmax (per query column) ----
-    float bmax = -1e30f;
-#pragma unroll
-    for (int kt = 0; kt < KB / 16; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + kt * 16 + 4 * g + r;
-        float x = st[kt][r] * sl2;
-        if (key >= p.L || (p.causal && key > qi)) x = -INFINITY;
-        else if (swmask && swin_region(p, wloc, key) != qreg) x += -100.f * 1.4426950408889634f;
-        st[kt][r] = x;
-        bmax = fmaxf(bmax, x);
-      }
-    }
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
-    const float m_new = fmaxf(m_run, bmax);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    float psum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < KB / 16; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(st[kt][r] - m_new);
-        st[kt][r] = e;
-        psum += e;
-      }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int i = 0; i < DT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[i][r] *= alpha;
-
-    // ---- O^T += V^T . P^T ----
-    if constexpr (sizeof(T) == 2) {
-#pragma unroll
-      for (int u = 0; u < KB / 32; ++u) {
-        s16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pb[j] = (short)f2bf(st[2 * u][j]);
-          pb[4 + j] = (short)f2bf(st[2 * u + 1][j]);
-        }
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const T* vr = &Vt[(dt * 16 + (lane & 15)) * VP + 32 * u + 4 * g];
-          uint2 lo = *reinterpret_cast<const uint2*>(vr);
-          uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-          uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < KB / 16; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const float va = to_f<T>(Vt[(dt * 16 + (lane & 15)) * VP + kt * 16 + 4 * g + r]);
-            o[dt] = mfma_f32(va, st[kt][r], o[dt]);
-          }
     }
     __syncthreads();
   }
 
   // ---- normalize + store: lane holds O^T[d = dt*16 + 4g + r][q] ----
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (!q_ok) return;
-  const float inv = 1.f / l_run;
-  T* O = reinterpret_cast<T*>(p.out) + qrow * p.ldo + h * D;
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
-    store4<T>(O + dt * 16 + 4 * g, v);
+  for (int t = 0; t < QT; ++t) {
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (!q_ok[t]) continue;
+    const float inv = 1.f / l;
+    T* O = reinterpret_cast<T*>(p.out) + qrow[t] * p.ldo + h * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      float v[4] = {o[t][dt][0] * inv, o[t][dt][1] * inv, o[t][dt][2] * inv, o[t][dt][3] * inv};
+      store4<T>(O + dt * 16 + 4 * g, v);
+    }
   }
 }
 
-template <typename T, int D, int NW>
+template <typename T, int D, int NW, int KB, int QT>
 void launch(const AttnP& p, hipStream_t st) {
-  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((attn_kernel<T, D, NW>), grid, dim3(NW * 64), 0, st, p);
+  constexpr int QW = 16 * NW * QT;
+  dim3 grid((unsigned)((p.L + QW - 1) / QW), (unsigned)(p.n_seq * p.H));
+  hipLaunchKernelGGL((attn_kernel<T, D, NW, KB, QT>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <typename T>
 int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
   if (p.mode == 1) {
-    if (head_dim == 32) { launch<T, 32, 3>(p, st); return 0; }
+    if (head_dim == 32 && p.L <= 160) { launch<T, 32, 3, 160, 3>(p, st); return 0; }
+    if (head_dim == 32) { launch<T, 32, 4, 64, 2>(p, st); return 0; }
   } else {
-    if (head_dim == 64) { launch<T, 64, 4>(p, st); return 0; }
-    if (head_dim == 32) { launch<T, 32, 4>(p, st); return 0; }
+    if (head_dim == 64) { launch<T, 64, 4, 64, 2>(p, st); return 0; }
+    if (head_dim == 32) { launch<T, 32, 4, 64, 2>(p, st); return 0; }
   }
   return -1;
 }

@@ -86,10 +86,33 @@ DEV float warp_max(float v) {
 // Activations (epilogues).  GELU is the exact erf form (nn.GELU default, timm Mlp);
 // QuickGELU is CLIP's x*sigmoid(1.702x) (model_vpt.py:165-167).
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_QUICKGELU = 3, ACT_SIGMOID = 4 };
+
+// erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7): one exp + one rcp + 5 FMAs,
+// branch-free (ocml erff is a multi-branch polynomial that dominated the Swin MLP).
+DEV float fast_erf(float x) {
+  const float a = fabsf(x);
+  const float t = __frcp_rn(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.f - p * t * __expf(-a * a);
+  return copysignf(y, x);
+}
+DEV float gelu_erf(float v) { return 0.5f * v * (1.f + fast_erf(v * 0.70710678118654752f)); }
+
+template <int ACT> DEV float act_t(float v) {
+  if constexpr (ACT == ACT_RELU) return fmaxf(v, 0.f);
+  else if constexpr (ACT == ACT_GELU) return gelu_erf(v);
+  else if constexpr (ACT == ACT_QUICKGELU) return v / (1.f + __expf(-1.702f * v));
+  else if constexpr (ACT == ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  else return v;
+}
+
 DEV float apply_act(float v, int act) {
   switch (act) {
     case ACT_RELU: return fmaxf(v, 0.f);
-    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case ACT_GELU: return gelu_erf(v);
     case ACT_QUICKGELU: return v / (1.f + __expf(-1.702f * v));
     case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
     default: return v;

@@ -28,18 +28,15 @@ struct ConvP {
   void* out; float* stats; int scpg;
 };
 
+// GroupNorm + ReLU on a loaded chunk with the block's per-channel scale/shift (LDS):
+// relu(x * rstd*gamma + (beta - mean*rstd*gamma)).  A conv tile never spans two slices
+// when GN is on (host-checked H*W % BM == 0), so one table per block suffices.
 template <typename T>
-DEV uint4 gn_chunk(uint4 u, const ConvP& p, int64_t s, int ci) {
+DEV uint4 gn_chunk(uint4 u, const float* gsc, const float* gsh, int ci) {
   constexpr int VN = Vec16<T>::N;
   T* e = reinterpret_cast<T*>(&u);
-  const int grp = ci / p.gcpg;
-  const int ngroups = p.c1 / p.gcpg;
-  const float mu = p.gmean[s * ngroups + grp], rs = p.grstd[s * ngroups + grp];
 #pragma unroll
-  for (int j = 0; j < VN; ++j) {
-    float v = (to_f<T>(e[j]) - mu) * rs * p.ggamma[ci + j] + p.gbeta[ci + j];
-    e[j] = from_f<T>(fmaxf(v, 0.f));
-  }
+  for (int j = 0; j < VN; ++j) e[j] = from_f<T>(fmaxf(fmaf(to_f<T>(e[j]), gsc[ci + j], gsh[ci + j]), 0.f));
   return u;
 }
 
@@ -54,6 +51,7 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
   __shared__ __attribute__((aligned(16))) T sA[2][BM * LDR];
   __shared__ __attribute__((aligned(16))) T sW[2][BN * LDR];
   __shared__ float red[4][8];
+  __shared__ float gsc[128], gsh[128];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t HW = (int64_t)p.H * p.W;
@@ -94,7 +92,7 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
           const int64_t pix = (int64_t)yy * p.W + xx;
           if (ci < p.c1) {
             u = ld16(S1 + a_s[i] * p.s1_ss + p.s1_off + pix * p.c1 + ci);
-            if (p.gmean) u = gn_chunk<T>(u, p, a_s[i], ci);
+            if (p.gmean) u = gn_chunk<T>(u, gsc, gsh, ci);
           } else {
             u = ld16(S2 + (a_s[i] / p.s2_div) * p.s2_ss + p.s2_off + pix * p.c2 + (ci - p.c1));
           }
@@ -131,6 +129,17 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int ktiles = (int)((K + BK - 1) / BK);
+  if (p.gmean) {
+    const int64_t s0 = (m0 < M ? m0 : 0) / HW;
+    const int ngroups = p.c1 / p.gcpg;
+    for (int c = tid; c < p.c1; c += NT) {
+      const float rs = p.grstd[s0 * ngroups + c / p.gcpg], mu = p.gmean[s0 * ngroups + c / p.gcpg];
+      const float sc = rs * p.ggamma[c];
+      gsc[c] = sc;
+      gsh[c] = p.gbeta[c] - mu * sc;
+    }
+    __syncthreads();
+  }
   gload(0);
   sstore(0);
   __syncthreads();
@@ -305,39 +314,52 @@ template <typename T>
 __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, const float* w, float bias,
                             const float* mean, const float* rstd, const float* gamma, const float* beta, int cpg,
                             const int32_t* classes, int Tout, float* out) {
-  extern __shared__ float sw[];   // [9][C] weights, then gamma, beta
-  for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) sw[i] = w[i];
-  __syncthreads();
-  const int64_t HW = (int64_t)H * W;
-  const int64_t total = B * Tn * HW;
+  // grid: (pixel blocks, slices).  Per block: weights [9][C] and the slice's GroupNorm
+  // scale/shift per channel in LDS; one output pixel per thread, 16-byte channel loads.
+  extern __shared__ float sw[];   // [9][C] weights | scale[C] | shift[C]
+  float* ssc = sw + 9 * C;
+  float* ssh = ssc + C;
+  const int64_t s = blockIdx.y;
   const int groups = C / cpg;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = i / HW;
-    const int pix = (int)(i % HW), y = pix / W, xx = pix % W;
-    float acc = bias;
-    for (int tap = 0; tap < 9; ++tap) {
-      const int yy = y + tap / 3 - 1, x2 = xx + tap % 3 - 1;
-      if (yy < 0 || yy >= H || x2 < 0 || x2 >= W) continue;
-      const T* src = x + (s * HW + (int64_t)yy * W + x2) * C;
-      for (int c = 0; c < C; c += 4) {
-        float v[4];
-        load4<T>(src + c, v);
+  for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) sw[i] = w[i];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    if (mean) {
+      const float sc = rstd[s * groups + c / cpg] * gamma[c];
+      ssc[c] = sc;
+      ssh[c] = beta[c] - mean[s * groups + c / cpg] * sc;
+    } else {
+      ssc[c] = 1.f;
+      ssh[c] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int HW = H * W;
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= HW) return;
+  const int y = pix / W, xx = pix % W;
+  const bool relu = mean != nullptr;
+  float acc = bias;
+  for (int tap = 0; tap < 9; ++tap) {
+    const int yy = y + tap / 3 - 1, x2 = xx + tap % 3 - 1;
+    if (yy < 0 || yy >= H || x2 < 0 || x2 >= W) continue;
+    const T* src = x + (s * HW + (int64_t)yy * W + x2) * C;
+    const float* wt = sw + tap * C;
+    for (int c = 0; c < C; c += 8) {
+      float v[8];
+      load4<T>(src + c, v);
+      load4<T>(src + c + 4, v + 4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float u = v[r];
-          if (mean) {
-            const int g = (c + r) / cpg;
-            u = fmaxf((u - mean[s * groups + g]) * rstd[s * groups + g] * gamma[c + r] + beta[c + r], 0.f);
-          }
-          acc += u * sw[tap * C + c + r];
-        }
+      for (int r = 0; r < 8; ++r) {
+        float u = fmaf(v[r], ssc[c + r], ssh[c + r]);
+        if (relu) u = fmaxf(u, 0.f);
+        acc = fmaf(u, wt[c + r], acc);
       }
     }
-    const int64_t b = s / Tn;
-    const int t = (int)(s % Tn);
-    const int cls = classes ? classes[b * Tn + t] : t;
-    out[(b * Tout + cls) * HW + pix] = acc;
   }
+  const int64_t b = s / Tn;
+  const int t = (int)(s % Tn);
+  const int cls = classes ? classes[b * Tn + t] : t;
+  out[(b * Tout + cls) * (int64_t)HW + pix] = acc;
 }
 
 }  // namespace
@@ -353,8 +375,8 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a->c_out % 4 == 0, "conv3x3: c_out must be a multiple of 4");
   CATSEG_CHECK(a->s1_slice_stride % vn == 0 && a->s1_offset % vn == 0, "conv3x3: src1 stride alignment");
   CATSEG_CHECK(!a->gn_mean || (a->gn_rstd && a->gn_gamma && a->gn_beta && a->gn_cpg > 0 && a->c1 % a->gn_cpg == 0 &&
-                               a->gn_cpg % vn == 0),
-               "conv3x3: bad GroupNorm prologue");
+                               a->gn_cpg % vn == 0 && a->c1 <= 128 && ((int64_t)a->H * a->W) % BM == 0),
+               "conv3x3: bad GroupNorm prologue (needs c1 <= 128, H*W % 128 == 0)");
   if (a->stats) {
     CATSEG_CHECK(((int64_t)a->H * a->W) % BM == 0, "conv3x3: GN stats need H*W % 128 == 0");
     CATSEG_CHECK(a->c_out <= 64 && a->stats_cpg == 16 && a->c_out % 16 == 0, "conv3x3: GN stats need cout<=64, 16/group");
@@ -400,16 +422,15 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                                       float bias, const float* mean, const float* rstd, const float* gamma,
                                       const float* beta, int cpg, const int32_t* classes, int T_out, float* out,
                                       int dtype, void* stream) {
-  CATSEG_CHECK(x && weight && out && C % 4 == 0 && B > 0 && T > 0, "conv3x3_head: bad args");
+  CATSEG_CHECK(x && weight && out && C % 8 == 0 && C <= 256 && B > 0 && T > 0, "conv3x3_head: bad args");
   CATSEG_CHECK(!mean || (rstd && gamma && beta && cpg > 0 && C % cpg == 0), "conv3x3_head: bad GN args");
-  const int64_t total = B * T * (int64_t)H * W;
-  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 16384);
-  const size_t sh = 9 * C * sizeof(float);
+  const dim3 grid((unsigned)(((int64_t)H * W + 255) / 256), (unsigned)(B * T));
+  const size_t sh = 11 * C * sizeof(float);
   if (dtype == CATSEG_BF16)
-    hipLaunchKernelGGL(head_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const bf16*)x, B, T, H, W,
+    hipLaunchKernelGGL(head_kernel<bf16>, grid, dim3(256), sh, (hipStream_t)stream, (const bf16*)x, B, T, H, W,
                        C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
   else
-    hipLaunchKernelGGL(head_kernel<float>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const float*)x, B, T, H,
+    hipLaunchKernelGGL(head_kernel<float>, grid, dim3(256), sh, (hipStream_t)stream, (const float*)x, B, T, H,
                        W, C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
   return catseg_launch_status("conv3x3_head");
 }

@@ -202,6 +202,124 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
   }
 }
 
+// ------------------------------------------------------------------------------------
+// bf16 main GEMM: BK = 64, 16-byte chunks XOR-swizzled in LDS (chunk' = chunk ^ (row & 7))
+// so the 16 rows a fragment read touches spread over the bank row; register-staged
+// double buffer (next tile's global loads issued before the MFMAs of this one);
+// 1-D grid remapped so consecutive tiles (same A row panel) land on one XCD's L2.
+// ------------------------------------------------------------------------------------
+constexpr int BK2 = 64;
+
+DEV int xcd_remap(int bid, int nwg) {
+  const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <typename TO, int BM, int BN>
+__global__ __launch_bounds__(NT) void gemm2_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
+                                                   const bf16* __restrict__ W, int64_t ldw, int64_t M, int64_t N,
+                                                   int64_t K, int tiles_n, EpiArgs e) {
+  constexpr int CPR = BK2 / 8;               // 8 chunks of 16 B per tile row
+  constexpr int A_CH = BM * CPR / NT, W_CH = BN * CPR / NT;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 sA[2][BM * BK2];
+  __shared__ __attribute__((aligned(16))) bf16 sW[2][BN * BK2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+  const int wm = (wave & 1) * WM, wn = (wave >> 1) * WN;
+
+  const bf16* a_ptr[A_CH]; int a_off[A_CH], a_col[A_CH]; bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int c = tid + i * NT, row = c / CPR, ch = c % CPR;
+    a_col[i] = ch * 8;
+    a_off[i] = (row * CPR + (ch ^ (row & 7))) * 8;
+    const int64_t m = m0 + row;
+    a_ok[i] = m < M;
+    a_ptr[i] = A + (a_ok[i] ? rowmap(amap, m) : 0) * lda;
+  }
+  const bf16* w_ptr[W_CH]; int w_off[W_CH], w_col[W_CH]; bool w_ok[W_CH];
+#pragma unroll
+  for (int i = 0; i < W_CH; ++i) {
+    const int c = tid + i * NT, row = c / CPR, ch = c % CPR;
+    w_col[i] = ch * 8;
+    w_off[i] = (row * CPR + (ch ^ (row & 7))) * 8;
+    const int64_t n = n0 + row;
+    w_ok[i] = n < N;
+    w_ptr[i] = W + (w_ok[i] ? n : 0) * ldw;
+  }
+  uint4 ra[A_CH], rw[W_CH];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int64_t k = k0 + a_col[i];
+      ra[i] = (a_ok[i] && k < K) ? ld16(a_ptr[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int64_t k = k0 + w_col[i];
+      rw[i] = (w_ok[i] && k < K) ? ld16(w_ptr[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_off[i]], ra[i]);
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) st16(&sW[buf][w_off[i]], rw[i]);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r = lane & 15, q = lane >> 4;
+  const int ktiles = (int)((K + BK2 - 1) / BK2);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BK2);
+    const bf16* As = sA[buf];
+    const bf16* Ws = sW[buf];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + q;
+      s16x8 bfrag[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int row = wm + 16 * j + r;
+        bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(row * CPR + (ch ^ (row & 7))) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn + 16 * i + r;
+        const s16x8 afrag = *reinterpret_cast<const s16x8*>(&Ws[(row * CPR + (ch ^ (row & 7))) * 8]);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag, bfrag[j], acc[i][j]);
+      }
+    }
+    if (kt + 1 < ktiles) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int64_t n = n0 + wn + 16 * i + rq;
+    if (n >= N) continue;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int64_t m = m0 + wm + 16 * j + col;
+      if (m < M) epilogue4<TO>(e, m, n, acc[i][j]);
+    }
+  }
+}
+
 template <typename TA, typename TO, int BM, int BN>
 void launch(const CatsegGemmArgs* g, hipStream_t st) {
   EpiArgs e;
@@ -219,10 +337,34 @@ void launch(const CatsegGemmArgs* g, hipStream_t st) {
                      (const TA*)g->A, g->lda, am, (const TA*)g->W, g->ldw, g->M, g->N, g->K, e);
 }
 
+template <typename TO, int BM, int BN>
+void launch2(const CatsegGemmArgs* g, hipStream_t st) {
+  EpiArgs e;
+  e.bias = g->bias;
+  e.add = g->add; e.ld_add = g->ld_add; e.add_ncols = g->add_ncols;
+  e.addmap = RowMap{g->addmap.d1, g->addmap.m1, g->addmap.s1, g->addmap.d2, g->addmap.m2, g->addmap.s2, g->addmap.off};
+  e.act = g->act; e.alpha = g->alpha;
+  e.res = g->res; e.ld_res = g->ld_res; e.res2 = g->res2; e.ld_res2 = g->ld_res2;
+  e.out = g->out; e.ldo = g->ldo;
+  e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
+  e.cvt_cout = g->cvt_cout;
+  RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
+  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)((g->N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm2_kernel<TO, BM, BN>), dim3((unsigned)(tm * tn)), dim3(NT), 0, st, (const bf16*)g->A,
+                     g->lda, am, (const bf16*)g->W, g->ldw, g->M, g->N, g->K, tn, e);
+}
+
 template <typename TA, typename TO>
 void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
-  if (g->N <= 64) launch<TA, TO, 128, 64>(g, st);
-  else launch<TA, TO, 128, 128>(g, st);
+  if constexpr (sizeof(TA) == 2) {
+    const int64_t t128 = ((g->M + 127) / 128) * ((g->N + 127) / 128);
+    if (g->N <= 64) launch2<TO, 128, 64>(g, st);
+    else if (t128 < 512) launch2<TO, 64, 128>(g, st);     // fill 256 CUs x 2 slots
+    else launch2<TO, 128, 128>(g, st);
+  } else {
+    if (g->N <= 64) launch<TA, TO, 128, 64>(g, st);
+    else launch<TA, TO, 128, 128>(g, st);
+  }
 }
 
 }  // namespace

@@ -346,6 +346,16 @@ int check_epi(const CatsegRowsEpi* p, int n_total) {
 
 }  // namespace
 
+// persistent register-weight variants (rowpersist.hip); 0 = launched, 1 = not applicable
+int catseg_rows_gemm_persistent(const void* x, int64_t ld_x, int64_t M, const float* g, const float* b, float eps,
+                                const void* w, int64_t N, const CatsegRowsEpi* epi, hipStream_t st);
+int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
+                               const void* w1, const float* b1, int64_t hidden, int act, const void* w2,
+                               const CatsegRowsEpi* epi, hipStream_t st);
+
+static bool g_persistent = true;
+extern "C" void catseg_set_persistent(int enable) { g_persistent = enable != 0; }
+
 extern "C" int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const float* ln_gamma, const float* ln_beta,
                                 float eps, const void* w, int64_t N, const CatsegRowsEpi* epi, int dtype,
                                 void* stream) {
@@ -357,6 +367,9 @@ extern "C" int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const fl
   if (int rc = check_epi(epi, (int)N)) return rc;
   Epi e = make_epi(epi);
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CATSEG_BF16 && g_persistent &&
+      catseg_rows_gemm_persistent(x, ld_x, M, ln_gamma, ln_beta, eps, w, N, epi, st) == 0)
+    return catseg_launch_status("rows_gemm");
   if (dtype == CATSEG_BF16) {
     dim3 grid((unsigned)((M + RB<bf16>::BM - 1) / RB<bf16>::BM), (unsigned)(N / 128));
     hipLaunchKernelGGL(rows_gemm_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld_x, M, ln_gamma, ln_beta, eps,
@@ -378,6 +391,9 @@ extern "C" int catseg_rows_mlp(const void* y, int64_t ld_y, int64_t M, const flo
   if (int rc = check_epi(epi, KD)) return rc;
   Epi e = make_epi(epi);
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CATSEG_BF16 && g_persistent &&
+      catseg_rows_mlp_persistent(y, ld_y, M, ln_gamma, ln_beta, eps, w1, b1, hidden, act, w2, epi, st) == 0)
+    return catseg_launch_status("rows_mlp");
   if (dtype == CATSEG_BF16) {
     hipLaunchKernelGGL(rows_mlp_kernel<bf16>, dim3((unsigned)((M + RB<bf16>::BM - 1) / RB<bf16>::BM)), dim3(NT), 0, st,
                        (const bf16*)y, ld_y, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (int)hidden, act,

@@ -1,0 +1,367 @@
+// Persistent bf16 row-block kernels for the 128-channel aggregation stream
+// (reference model.py:117-225 Swin blocks, :357-424 class layers, :546 ConvTranspose).
+//
+// The whole weight matrix lives in REGISTERS as MFMA A-operand fragments for the life
+// of the workgroup (one 8-wave workgroup per CU walks 32-row tiles), so the only
+// HBM traffic is the compulsory row read and write.  Per tile:
+//   rows (prefetched one tile ahead, with any residual rows) -> LayerNorm in registers
+//   -> LDS -> MFMA against the register weights -> fp32 stage in LDS -> epilogue on
+//   full rows with 16-byte stores.
+// The MLP variant keeps the 512-wide hidden tile in LDS (H never touches HBM) and reads
+// its residual (= its own input rows) from an LDS copy.  Epilogue options are template
+// parameters so each variant compiles to one straight-line loop.
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int KD = 128;          // row width
+constexpr int NW = 8, NT = NW * 64;
+constexpr int BM = 32;           // rows per tile
+constexpr int LDX = KD + 8;      // LDS row stride of sX (272 B: conflict-free ds_read_b128)
+constexpr int CPT = BM * 16 / NT; // 16-byte chunks of a tile per thread (= 1)
+static_assert(CPT == 1, "one chunk per thread");
+
+struct PEpi {
+  const float* bias;
+  const bf16* add; int64_t ld_add; RowMap addmap; int add_ncols;
+  const bf16* res; int64_t ld_res;
+  const bf16* res2; int64_t ld_res2;
+  bf16* out; int64_t ldo;
+  int cvt_k, cvt_hin, cvt_win, cvt_cout;
+};
+
+// thread t holds chunk t of the tile: row t/16, columns (t%16)*8 .. +8
+DEV uint4 fetch_chunk(const bf16* X, int64_t ldx, int64_t m0, int64_t M) {
+  const int r = threadIdx.x >> 4, ch = threadIdx.x & 15;
+  const int64_t m = m0 + r;
+  return m < M ? ld16(X + m * ldx + ch * 8) : make_uint4(0, 0, 0, 0);
+}
+
+// LayerNorm one chunk (16 lanes per row) and store it to LDS
+DEV void put_chunk(uint4 u, const float* g, const float* b, float eps, bf16* sX) {
+  const int r = threadIdx.x >> 4, ch = threadIdx.x & 15;
+  if (g) {
+    bf16* e = reinterpret_cast<bf16*>(&u);
+    float v[8], s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { v[j] = bf2f(e[j]); s += v[j]; }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.f / KD);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { v[j] -= mean; q += v[j] * v[j]; }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q * (1.f / KD) + eps);
+    const float4 g0 = *reinterpret_cast<const float4*>(g + ch * 8), g1 = *reinterpret_cast<const float4*>(g + ch * 8 + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(b + ch * 8), b1 = *reinterpret_cast<const float4*>(b + ch * 8 + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = f2bf(v[j] * rstd * gg[j] + bb[j]);
+  }
+  st16(&sX[r * LDX + ch * 8], u);
+}
+
+DEV void add8(float* v, uint4 u) {
+  const bf16* e = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] += bf2f(e[j]);
+}
+
+DEV uint4 pack8(const float* v) {
+  uint4 o;
+  o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+  o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+  o.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+  o.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+  return o;
+}
+
+// ============================ persistent GEMM: out = epi(LN?(X) . W^T) =================
+// wave w owns output columns [w*NOUT/8, (w+1)*NOUT/8).  Epilogue: + bias (+ add on the
+// first add_ncols columns) (+ residual rows, prefetched with the input rows), row-major
+// or ConvTranspose-scattered store.
+template <int NOUT, bool ADD, bool RES, bool SCATTER>
+__global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X, int64_t ldx, int64_t M,
+                                                      const float* ln_g, const float* ln_b, float eps,
+                                                      const bf16* __restrict__ W, PEpi e) {
+  constexpr int WN = NOUT / NW, FN = WN / 16, FM = BM / 16;
+  constexpr int SLD = NOUT + 4;
+  constexpr int CH = NOUT / 8;                    // 8-column items per row
+  constexpr int ITEMS = BM * CH, PER = ITEMS / NT;
+  static_assert(ITEMS % NT == 0, "");
+  __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
+  __shared__ __attribute__((aligned(16))) float st[BM * SLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wn = wave * WN;
+  s16x8 wf[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 u = ld16(W + (int64_t)(wn + 16 * i + r16) * KD + ks * 32 + 8 * q);
+      wf[i][ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  const int64_t ntiles = (M + BM - 1) / BM;
+  int64_t tile = blockIdx.x;
+  uint4 rx = make_uint4(0, 0, 0, 0);
+  uint4 rres[PER];
+  auto fetch = [&](int64_t t) {
+    rx = fetch_chunk(X, ldx, t * BM, M);
+    if constexpr (RES) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * NT, r = i / CH, c = (i % CH) * 8;
+        const int64_t m = t * BM + r;
+        rres[k] = m < M ? ld16(e.res + m * e.ld_res + c) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t m0 = tile * BM;
+    put_chunk(rx, ln_g, ln_b, eps, sX);
+    uint4 res_cur[PER];
+    if constexpr (RES) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) res_cur[k] = rres[k];
+    }
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);     // prefetch the next tile
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s16x8 xf[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[(16 * j + r16) * LDX + ks * 32 + 8 * q]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wf[i][ks], xf[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        *reinterpret_cast<f32x4*>(&st[(16 * j + r16) * SLD + wn + 16 * i + 4 * q]) = acc[i][j];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * NT, r = i / CH, c = (i % CH) * 8;
+      const int64_t m = m0 + r;
+      uint4 ad = make_uint4(0, 0, 0, 0);
+      const bool do_add = ADD && c < e.add_ncols && m < M;
+      if (do_add) ad = ld16(e.add + rowmap(e.addmap, m) * e.ld_add + c);
+      float v[8];
+      *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c]);
+      *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c + 4]);
+      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + c), b1 = *reinterpret_cast<const float4*>(e.bias + c + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      if (do_add) add8(v, ad);
+      if constexpr (RES) add8(v, res_cur[k]);
+      if (m < M) {
+        int64_t off;
+        if constexpr (SCATTER) {
+          const int64_t kk = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
+          const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
+          const int64_t ky = c / (kk * cout), kx = (c / cout) % kk, co = c % cout;
+          off = ((s * hin * kk + y * kk + ky) * (win * kk) + x * kk + kx) * cout + co;
+        } else {
+          off = m * e.ldo + c;
+        }
+        st16(e.out + off, pack8(v));
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================ persistent MLP ===========================================
+// out = Y + act(LN(Y) . W1^T + b1) . W2^T + b2 (+ R2), hidden = 512.
+// wave w: GEMM1 hidden rows [64w, 64w+64) (W1 fragments in registers),
+//         GEMM2 output rows [16w, 16w+16) over all 512 hidden (W2 fragments in registers).
+constexpr int HID = 512, LDH = HID + 8;
+
+template <int ACT, bool RES2>
+__global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
+                                                     const float* ln_g, const float* ln_b, float eps,
+                                                     const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                     const bf16* __restrict__ W2, PEpi e) {
+  constexpr int FM = BM / 16, SLD = KD + 4;
+  __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
+  __shared__ __attribute__((aligned(16))) bf16 sH[BM * LDH];
+  __shared__ __attribute__((aligned(16))) float st[BM * SLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  s16x8 w1f[4][4], w2f[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 u = ld16(W1 + (int64_t)(64 * wave + 16 * i + r16) * KD + ks * 32 + 8 * q);
+      w1f[i][ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    uint4 u = ld16(W2 + (int64_t)(16 * wave + r16) * HID + ks * 32 + 8 * q);
+    w2f[ks] = *reinterpret_cast<s16x8*>(&u);
+  }
+  const int64_t ntiles = (M + BM - 1) / BM;
+  int64_t tile = blockIdx.x;
+  const int er = threadIdx.x >> 4, ec = (threadIdx.x & 15) * 8;   // epilogue item = the thread's input chunk
+  uint4 ry = make_uint4(0, 0, 0, 0), rr2 = make_uint4(0, 0, 0, 0);
+  auto fetch = [&](int64_t t) {
+    ry = fetch_chunk(Y, ldy, t * BM, M);
+    if constexpr (RES2) rr2 = fetch_chunk(e.res2, e.ld_res2, t * BM, M);
+  };
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t m0 = tile * BM;
+    const uint4 y_raw = ry, r2_cur = rr2;     // residuals of this tile stay in registers
+    put_chunk(ry, ln_g, ln_b, eps, sX);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x4 acc1[2][FM];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s16x8 xf[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[(16 * j + r16) * LDX + ks * 32 + 8 * q]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc1[i][j] = mfma_bf16(w1f[2 * hf + i][ks], xf[j], acc1[i][j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int hh = 64 * wave + 16 * (2 * hf + i) + 4 * q;
+        const float4 bv = *reinterpret_cast<const float4*>(b1 + hh);
+        const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r] + bb[r]);
+          store4<bf16>(&sH[(16 * j + r16) * LDH + hh], v);
+        }
+      }
+    }
+    __syncthreads();
+    f32x4 acc2[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + 8 * q]);
+        acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+      *reinterpret_cast<f32x4*>(&st[(16 * j + r16) * SLD + 16 * wave + 4 * q]) = acc2[j];
+    __syncthreads();
+    {
+      const int64_t m = m0 + er;
+      float v[8];
+      *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec]);
+      *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec + 4]);
+      const float4 c0 = *reinterpret_cast<const float4*>(e.bias + ec), c1 = *reinterpret_cast<const float4*>(e.bias + ec + 4);
+      v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+      v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+      add8(v, y_raw);
+      if constexpr (RES2) add8(v, r2_cur);
+      if (m < M) st16(e.out + m * e.ldo + ec, pack8(v));
+    }
+    __syncthreads();
+  }
+}
+
+PEpi make_pepi(const CatsegRowsEpi* p) {
+  PEpi e;
+  e.bias = p->bias;
+  e.add = (const bf16*)p->add; e.ld_add = p->ld_add; e.add_ncols = (int)p->add_ncols;
+  e.addmap = RowMap{p->addmap.d1, p->addmap.m1, p->addmap.s1, p->addmap.d2, p->addmap.m2, p->addmap.s2, p->addmap.off};
+  e.res = (const bf16*)p->res; e.ld_res = p->ld_res; e.res2 = (const bf16*)p->res2; e.ld_res2 = p->ld_res2;
+  e.out = (bf16*)p->out; e.ldo = p->ldo;
+  e.cvt_k = p->cvt_k; e.cvt_hin = p->cvt_hin; e.cvt_win = p->cvt_win; e.cvt_cout = p->cvt_cout;
+  return e;
+}
+
+unsigned persist_grid(int64_t M, int per_cu = 1) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int64_t tiles = (M + BM - 1) / BM;
+  return (unsigned)std::min<int64_t>(tiles, (int64_t)cus * per_cu);
+}
+
+template <int NOUT, bool ADD, bool RES, bool SCATTER>
+void launch_pgemm(const void* x, int64_t ld_x, int64_t M, const float* g, const float* b, float eps, const void* w,
+                  const PEpi& e, hipStream_t st) {
+  // NOUT=128 variants fit 3 workgroups per CU (<= 96 VGPRs, 25 KB LDS): more rows in flight
+  hipLaunchKernelGGL((pgemm_kernel<NOUT, ADD, RES, SCATTER>), dim3(persist_grid(M, NOUT == 128 ? 3 : 1)), dim3(NT), 0, st,
+                     (const bf16*)x, ld_x, M, g, b, eps, (const bf16*)w, e);
+}
+
+}  // namespace
+
+// bf16 fast paths used by catseg_rows_gemm / catseg_rows_mlp (rowblock.hip) when the
+// shapes and epilogue fit; return 1 if not applicable (the caller then uses the tiled kernels).
+int catseg_rows_gemm_persistent(const void* x, int64_t ld_x, int64_t M, const float* g, const float* b, float eps,
+                                const void* w, int64_t N, const CatsegRowsEpi* epi, hipStream_t st) {
+  if (!epi->bias || epi->act != 0 || epi->res2) return 1;
+  const bool add = epi->add != nullptr, res = epi->res != nullptr, sc = epi->store_mode == 1;
+  const PEpi e = make_pepi(epi);
+  if (N == 384 && add && !res && !sc) launch_pgemm<384, true, false, false>(x, ld_x, M, g, b, eps, w, e, st);
+  else if (N == 384 && !add && !res && sc) launch_pgemm<384, false, false, true>(x, ld_x, M, g, b, eps, w, e, st);
+  else if (N == 384 && !add && !res && !sc) launch_pgemm<384, false, false, false>(x, ld_x, M, g, b, eps, w, e, st);
+  else if (N == 128 && !add && res && !sc) launch_pgemm<128, false, true, false>(x, ld_x, M, g, b, eps, w, e, st);
+  else if (N == 128 && !add && !res && !sc) launch_pgemm<128, false, false, false>(x, ld_x, M, g, b, eps, w, e, st);
+  else return 1;
+  return 0;
+}
+
+int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
+                               const void* w1, const float* b1, int64_t hidden, int act, const void* w2,
+                               const CatsegRowsEpi* epi, hipStream_t st) {
+  // residual must be the input rows themselves (both reference MLPs: model.py:223, :413)
+  if (hidden != HID || !epi->bias || epi->res != y || epi->ld_res != ld_y || epi->add || epi->store_mode) return 1;
+  const PEpi e = make_pepi(epi);
+  const dim3 grid(persist_grid(M)), blk(NT);
+  const bf16* Yb = (const bf16*)y;
+  if (act == ACT_GELU && !epi->res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
+                       (const bf16*)w2, e);
+  else if (act == ACT_RELU && epi->res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
+                       (const bf16*)w2, e);
+  else if (act == ACT_RELU && !epi->res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
+                       (const bf16*)w2, e);
+  else if (act == ACT_GELU && epi->res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
+                       (const bf16*)w2, e);
+  else return 1;
+  return 0;
+}

@@ -99,6 +99,10 @@ int catseg_rows_mlp(const void* y, int64_t ld_y, int64_t M, const float* ln_gamm
                     int64_t hidden, int act, const void* w2, const CatsegRowsEpi* epi,
                     int dtype, void* stream);
 
+/* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
+ * 0 = the tiled variants, for A/B tests).  Process-wide. */
+void catseg_set_persistent(int enable);
+
 /* catseg_layernorm — LayerNorm over the last dim (fp32 math).  Replaces
  * model_vpt.py:156-162 (ln_pre/ln_1/ln_2/ln_post/ln_final) and the nn.LayerNorm of
  * model.py:152,158,233,368-369.  in rows use `inmap`. */

@@ -292,9 +292,16 @@ def test_bicubic_postprocess():
     close(o, ref, atol=2e-6, what="postprocess")
 
 
+@pytest.fixture(params=["persistent", "tiled"])
+def rows_variant(request):
+    L.load().catseg_set_persistent(1 if request.param == "persistent" else 0)
+    yield request.param
+    L.load().catseg_set_persistent(1)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M", [300, 1000])
-def test_rows_gemm_ln_add_res_and_convt(dt, M):
+def test_rows_gemm_ln_add_res_and_convt(dt, M, rows_variant):
     D, N = 128, 384
     x = rnd(M, D, seed=40) * 2 + 0.3
     g, b = rnd(D, seed=41) + 1, rnd(D, seed=42)
@@ -328,7 +335,7 @@ def test_rows_gemm_ln_add_res_and_convt(dt, M):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
-def test_rows_mlp(dt, act):
+def test_rows_mlp(dt, act, rows_variant):
     M, D, Hd = 700, 128, 512
     y = rnd(M, D, seed=50) * 2
     g, b = rnd(D, seed=51) + 1, rnd(D, seed=52)
