@@ -428,16 +428,26 @@ class CatSegEngine:
             ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y, res2=X)
         del qkv, o, Y, gn, gqk
         # ---- guided upsampler (model.py:674-681, 540-555) ----
-        src, Hc = X, G
+        src, Hc, src_gn = X, G, None
         tile = ops.conv_tile_rows()
         for i, dec in enumerate(w.dec):
             cu = dec.up_c
             Ho = Hc * 2
             up = torch.empty(S * Ho * Ho, cu, device=dev, dtype=dt)
-            if src.shape[1] == 128 and dec.up_w.shape[0] % 128 == 0:
-                ops.rows_gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+            if src_gn is not None and dt == torch.bfloat16 and tuple(dec.up_w.shape) == (192, 64):
+                # GroupNorm+ReLU of the previous DoubleConv fused into this ConvTranspose
+                ops.convt64_gn(src, dec.up_w, up, HW=Hc * Hc, gn=src_gn, bias=dec.up_b, store=(2, Hc, Hc, cu))
             else:
-                ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+                if src_gn is not None:
+                    z = torch.empty_like(src)
+                    m_, r_, g_, b_, cpg_ = src_gn
+                    ops.groupnorm_relu(src, z, S=S, HW=Hc * Hc, C=src.shape[1], cpg=cpg_, mean=m_, rstd=r_,
+                                       gamma=g_, beta=b_)
+                    src = z
+                if src.shape[1] == 128 and dec.up_w.shape[0] % 128 == 0:
+                    ops.rows_gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+                else:
+                    ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
             cout = dec.c0.shape[0]
             groups = cout // 16
             tiles = Ho * Ho // tile
@@ -454,10 +464,7 @@ class CatSegEngine:
             r2 = torch.empty_like(m1)
             ops.groupnorm_stats(st, S, tiles, groups, tile * 16, m2, r2)
             if i == 0:
-                z = torch.empty_like(c2)
-                ops.groupnorm_relu(c2, z, S=S, HW=Ho * Ho, C=cout, cpg=16, mean=m2, rstd=r2,
-                                   gamma=dec.g3[0], beta=dec.g3[1])
-                src, Hc = z, Ho
+                src, Hc, src_gn = c2, Ho, (m2, r2, dec.g3[0], dec.g3[1], 16)
             else:
                 logits = torch.empty(B, T0, Ho, Ho, device=dev, dtype=_f32)
                 if classes is not None:

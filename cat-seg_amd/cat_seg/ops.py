@@ -310,6 +310,17 @@ def rows_gemm(x, w, out, *, ln=None, eps=1e-5, bias=None, add=None, addmap=None,
     return out
 
 
+def convt64_gn(x, w, out, *, HW, gn, bias, store):
+    """out = ConvT_k2(relu(GN(x))) over 64-channel rows (catseg_convt64_gn, bf16)."""
+    mean, rstd, gamma, beta, cpg = gn
+    e = _rows_epi(out, bias, None, None, None, L.ACT_NONE, None, None, store)
+    M = x.shape[0]
+    with _rec("convt64_gn", 2 * M * w.shape[0] * w.shape[1], x.element_size() * M * (w.shape[1] + w.shape[0])):
+        call("catseg_convt64_gn", x.data_ptr(), M, HW, mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+             beta.data_ptr(), cpg, w.data_ptr(), w.shape[0], e, _stream())
+    return out
+
+
 def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=None, eps=1e-5, M=None):
     """out = act(LN(y) . w1^T + b1) . w2^T + b2 + res + res2 (catseg_rows_mlp)."""
     M = M if M is not None else y.shape[0]

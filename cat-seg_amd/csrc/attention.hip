@@ -28,25 +28,30 @@ struct AttnP {
   int mode; int img_h, img_w, ws, shift;
 };
 
-DEV int64_t seq_row(const AttnP& p, int64_t s, int i) {
-  if (p.mode == 0) return s * p.L + i;
-  const int nwx = p.img_w / p.ws, nwin = (p.img_h / p.ws) * nwx;
-  const int64_t slice = s / nwin;
-  const int w = (int)(s % nwin);
-  const int Y = (w / nwx) * p.ws + i / p.ws, X = (w % nwx) * p.ws + i % p.ws;
-  const int y = (Y + p.shift) % p.img_h, x = (X + p.shift) % p.img_w;
-  return slice * (int64_t)p.img_h * p.img_w + (int64_t)y * p.img_w + x;
+// GEO != 0: the window geometry is compile-time (GEO x GEO image, GEO/2 windows — CAT-Seg's
+// 24x24 feature map with 12x12 windows), so every index division is by a constant.
+template <int GEO>
+DEV int64_t seq_row(const AttnP& p, int s, int i) {
+  if (p.mode == 0) return (int64_t)s * p.L + i;
+  const int IH = GEO ? GEO : p.img_h, IW = GEO ? GEO : p.img_w, WS = GEO ? GEO / 2 : p.ws;
+  const int nwx = IW / WS, nwin = (IH / WS) * nwx;
+  const int slice = s / nwin, w = s % nwin;
+  const int Y = (w / nwx) * WS + i / WS, X = (w % nwx) * WS + i % WS;
+  const int y = (Y + p.shift) % IH, x = (X + p.shift) % IW;
+  return (int64_t)slice * IH * IW + y * IW + x;
 }
 
+template <int GEO>
 DEV int swin_region(const AttnP& p, int wloc, int i) {
-  const int nwx = p.img_w / p.ws;
-  const int Y = (wloc / nwx) * p.ws + i / p.ws, X = (wloc % nwx) * p.ws + i % p.ws;
-  const int hb = Y < p.img_h - p.ws ? 0 : (Y < p.img_h - p.shift ? 1 : 2);
-  const int wb = X < p.img_w - p.ws ? 0 : (X < p.img_w - p.shift ? 1 : 2);
+  const int IH = GEO ? GEO : p.img_h, IW = GEO ? GEO : p.img_w, WS = GEO ? GEO / 2 : p.ws;
+  const int nwx = IW / WS;
+  const int Y = (wloc / nwx) * WS + i / WS, X = (wloc % nwx) * WS + i % WS;
+  const int hb = Y < IH - WS ? 0 : (Y < IH - p.shift ? 1 : 2);
+  const int wb = X < IW - WS ? 0 : (X < IW - p.shift ? 1 : 2);
   return hb * 3 + wb;
 }
 
-template <typename T, int D, int NW, int KB, int QT>
+template <typename T, int D, int NW, int KB, int QT, int GEO>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   constexpr int NT = NW * 64;
   constexpr int VN = Vec16<T>::N;
@@ -61,13 +66,13 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   __shared__ signed char kreg_s[KB];                    // SW-MSA region id of each staged key
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t s = blockIdx.y / p.H;
+  const int s = blockIdx.y / p.H;
   const int h = blockIdx.y % p.H;
   const int g = lane >> 4;
   const T* Kg = reinterpret_cast<const T*>(p.k);
   const T* Vg = reinterpret_cast<const T*>(p.v);
-  const int nwin = p.mode == 1 ? (p.img_h / p.ws) * (p.img_w / p.ws) : 1;
-  const int wloc = p.mode == 1 ? (int)(s % nwin) : 0;
+  const int nwin = p.mode == 1 ? (GEO ? 4 : (p.img_h / p.ws) * (p.img_w / p.ws)) : 1;
+  const int wloc = p.mode == 1 ? s % nwin : 0;
   const bool swmask = p.mode == 1 && p.shift > 0;
   const float sl2 = p.scale * 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
@@ -83,8 +88,8 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
     tile_live[t] = q0 < p.L;
     qi[t] = q0 + (lane & 15);
     q_ok[t] = qi[t] < p.L;
-    qrow[t] = seq_row(p, s, q_ok[t] ? qi[t] : 0);
-    qreg[t] = swmask ? swin_region(p, wloc, q_ok[t] ? qi[t] : 0) : 0;
+    qrow[t] = seq_row<GEO>(p, s, q_ok[t] ? qi[t] : 0);
+    qreg[t] = swmask ? swin_region<GEO>(p, wloc, q_ok[t] ? qi[t] : 0) : 0;
     const T* Q = reinterpret_cast<const T*>(p.q) + qrow[t] * p.ld + h * D;
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
       const int key = k0 + kk;
       uint4 ku = make_uint4(0, 0, 0, 0), vu = make_uint4(0, 0, 0, 0);
       if (key < p.L) {
-        const int64_t r = seq_row(p, s, key);
+        const int64_t r = seq_row<GEO>(p, s, key);
         ku = ld16(Kg + r * p.ld + h * D + d0);
         vu = ld16(Vg + r * p.ld + h * D + d0);
       }
@@ -120,7 +125,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
       const T* ve = reinterpret_cast<const T*>(&vu);
 #pragma unroll
       for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
-      if (swmask && d0 == 0) kreg_s[kk] = key < p.L ? (signed char)swin_region(p, wloc, key) : (signed char)-1;
+      if (swmask && d0 == 0) kreg_s[kk] = key < p.L ? (signed char)swin_region<GEO>(p, wloc, key) : (signed char)-1;
     }
     __syncthreads();
 
@@ -230,17 +235,18 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D, int NW, int KB, int QT>
+template <typename T, int D, int NW, int KB, int QT, int GEO = 0>
 void launch(const AttnP& p, hipStream_t st) {
   constexpr int QW = 16 * NW * QT;
   dim3 grid((unsigned)((p.L + QW - 1) / QW), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((attn_kernel<T, D, NW, KB, QT>), grid, dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((attn_kernel<T, D, NW, KB, QT, GEO>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <typename T>
 int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
   if (p.mode == 1) {
-    if (head_dim == 32 && p.L <= 160) { launch<T, 32, 3, 160, 3>(p, st); return 0; }
+    if (head_dim == 32 && p.img_h == 24 && p.img_w == 24 && p.ws == 12) { launch<T, 32, 9, 160, 1, 24>(p, st); return 0; }
+    if (head_dim == 32 && p.L <= 160) { launch<T, 32, 9, 160, 1>(p, st); return 0; }
     if (head_dim == 32) { launch<T, 32, 4, 64, 2>(p, st); return 0; }
   } else {
     if (head_dim == 64) { launch<T, 64, 4, 64, 2>(p, st); return 0; }

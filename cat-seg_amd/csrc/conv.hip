@@ -366,6 +366,10 @@ __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, 
 
 extern "C" int catseg_conv_tile_rows(void) { return BM; }
 
+int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st);   // conv_lds.hip
+static bool g_conv_lds = true;
+extern "C" void catseg_set_conv_lds(int enable) { g_conv_lds = enable != 0; }
+
 extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a && a->src1 && a->weight && a->out, "conv3x3: null pointer");
   CATSEG_CHECK(a->S > 0 && a->H > 0 && a->W > 0 && a->c1 > 0 && a->c_out > 0, "conv3x3: empty shape");
@@ -388,6 +392,7 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.out = a->out; p.stats = a->stats; p.scpg = a->stats_cpg;
   hipStream_t st = (hipStream_t)stream;
+  if (g_conv_lds && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
   if (a->dtype == CATSEG_BF16) launch_conv<bf16>(p, st);
   else launch_conv<float>(p, st);
   return catseg_launch_status("conv3x3");

@@ -72,12 +72,7 @@ DEV void add8(float* v, uint4 u) {
 }
 
 DEV uint4 pack8(const float* v) {
-  uint4 o;
-  o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-  o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-  o.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-  o.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
-  return o;
+  return make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7]));
 }
 
 // ============================ persistent GEMM: out = epi(LN?(X) . W^T) =================
@@ -293,6 +288,101 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   }
 }
 
+// ============================ decoder ConvTranspose over 64-channel rows ================
+// out = scatter_k2(relu(GN(X)) . W^T + bias): the second Up block's ConvTranspose2d
+// (model.py:546) fused with the preceding GroupNorm+ReLU of DoubleConv (model.py:532-533).
+// X: [M][64] NHWC rows, slice = row / HW (HW % 64 == 0), W: [NOUT][64] in registers.
+constexpr int K64 = 64, NW4 = 4, NT4 = NW4 * 64, BM64 = 64, LDX64 = K64 + 8;
+
+template <int NOUT>
+__global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict__ X, int64_t M, int64_t HW,
+                                                          const float* mean, const float* rstd, const float* gamma,
+                                                          const float* beta, int cpg, const bf16* __restrict__ W,
+                                                          PEpi e) {
+  constexpr int WN = NOUT / NW4, FN = WN / 16, FM = BM64 / 16;
+  constexpr int SLD = NOUT + 4, CH = NOUT / 8, ITEMS = BM64 * CH, PER = ITEMS / NT4;
+  static_assert(WN % 16 == 0 && ITEMS % NT4 == 0, "");
+  __shared__ __attribute__((aligned(16))) bf16 sX[BM64 * LDX64];
+  __shared__ __attribute__((aligned(16))) float st[BM64 * SLD];
+  __shared__ float ssc[K64], ssh[K64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wn = wave * WN;
+  s16x8 wf[FN][2];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 u = ld16(W + (int64_t)(wn + 16 * i + r16) * K64 + ks * 32 + 8 * q);
+      wf[i][ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  const int groups = K64 / cpg;
+  const int64_t ntiles = (M + BM64 - 1) / BM64;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t m0 = tile * BM64;
+    const int64_t s = m0 / HW;
+    uint4 u[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = threadIdx.x + k * NT4, r = c >> 3, ch = c & 7;
+      u[k] = m0 + r < M ? ld16(X + (m0 + r) * K64 + ch * 8) : make_uint4(0, 0, 0, 0);
+    }
+    if (threadIdx.x < K64) {
+      const int c = threadIdx.x;
+      const float sc = rstd[s * groups + c / cpg] * gamma[c];
+      ssc[c] = sc;
+      ssh[c] = beta[c] - mean[s * groups + c / cpg] * sc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = threadIdx.x + k * NT4, r = c >> 3, ch = c & 7;
+      bf16* ev = reinterpret_cast<bf16*>(&u[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ev[j] = f2bf(fmaxf(fmaf(bf2f(ev[j]), ssc[ch * 8 + j], ssh[ch * 8 + j]), 0.f));
+      st16(&sX[r * LDX64 + ch * 8], u[k]);
+    }
+    __syncthreads();
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s16x8 xf[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[(16 * j + r16) * LDX64 + ks * 32 + 8 * q]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wf[i][ks], xf[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        *reinterpret_cast<f32x4*>(&st[(16 * j + r16) * SLD + wn + 16 * i + 4 * q]) = acc[i][j];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * NT4, r = i / CH, c = (i % CH) * 8;
+      const int64_t m = m0 + r;
+      if (m >= M) continue;
+      float v[8];
+      *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c]);
+      *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c + 4]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += e.bias[c + j];
+      const int64_t kk = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
+      const int64_t sl = m / (hin * win), y = (m / win) % hin, x = m % win;
+      const int64_t ky = c / (kk * cout), kx = (c / cout) % kk, co = c % cout;
+      st16(e.out + ((sl * hin * kk + y * kk + ky) * (win * kk) + x * kk + kx) * cout + co, pack8(v));
+    }
+    __syncthreads();
+  }
+}
+
 PEpi make_pepi(const CatsegRowsEpi* p) {
   PEpi e;
   e.bias = p->bias;
@@ -340,6 +430,21 @@ int catseg_rows_gemm_persistent(const void* x, int64_t ld_x, int64_t M, const fl
   else if (N == 128 && !add && !res && !sc) launch_pgemm<128, false, false, false>(x, ld_x, M, g, b, eps, w, e, st);
   else return 1;
   return 0;
+}
+
+extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const float* mean, const float* rstd,
+                                 const float* gamma, const float* beta, int cpg, const void* w, int64_t N,
+                                 const CatsegRowsEpi* epi, void* stream) {
+  CATSEG_CHECK(x && w && epi && epi->out && epi->bias && mean && rstd && gamma && beta, "convt64_gn: null pointer");
+  CATSEG_CHECK(M > 0 && HW > 0 && HW % BM64 == 0 && M % HW == 0, "convt64_gn: rows must tile slices of HW % 64 == 0");
+  CATSEG_CHECK(cpg > 0 && K64 % cpg == 0, "convt64_gn: bad GroupNorm grouping");
+  CATSEG_CHECK(epi->store_mode == 1 && epi->cvt_cout % 8 == 0 && N == (int64_t)epi->cvt_k * epi->cvt_k * epi->cvt_cout,
+               "convt64_gn: needs the ConvTranspose scatter store");
+  CATSEG_CHECK(N == 192, "convt64_gn: N = 192 (k=2, 48 channels) only");
+  const PEpi e = make_pepi(epi);
+  hipLaunchKernelGGL((pconvt64_kernel<192>), dim3(persist_grid((M + 1) / 2, 2)), dim3(NT4), 0, (hipStream_t)stream,
+                     (const bf16*)x, M, HW, mean, rstd, gamma, beta, cpg, (const bf16*)w, e);
+  return catseg_launch_status("convt64_gn");
 }
 
 int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,

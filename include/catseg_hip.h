@@ -99,6 +99,17 @@ int catseg_rows_mlp(const void* y, int64_t ld_y, int64_t M, const float* ln_gamm
                     int64_t hidden, int act, const void* w2, const CatsegRowsEpi* epi,
                     int dtype, void* stream);
 
+/* catseg_convt64_gn — bf16: out = ConvTranspose2d(k=2, s=2)(relu(GroupNorm(X))) for 64-channel
+ * NHWC rows X [M][64] (slice = row / HW, HW % 64 == 0): the second guided-upsampler stage
+ * (model.py:546) fused with DoubleConv's last GroupNorm+ReLU (:532-533).  W: [N=4*cout][64],
+ * epi: bias + store_mode 1 scatter (cvt_k = 2). */
+int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const float* mean, const float* rstd,
+                      const float* gamma, const float* beta, int cpg, const void* w, int64_t N,
+                      const CatsegRowsEpi* epi, void* stream);
+
+/* Select the LDS-resident-input bf16 conv3x3 (default 1) or the im2col one (0), for A/B tests. */
+void catseg_set_conv_lds(int enable);
+
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */
 void catseg_set_persistent(int enable);

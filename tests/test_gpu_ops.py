@@ -359,6 +359,68 @@ def test_rows_mlp(dt, act, rows_variant):
           rtol=0 if dt == torch.float32 else 1e-2, what="rows_mlp in place")
 
 
+@pytest.mark.parametrize("W_,c1,c2,co,gn", [(48, 96, 32, 64, False), (48, 64, 0, 64, True), (96, 48, 16, 32, False),
+                                            (96, 32, 0, 32, True)])
+@pytest.mark.parametrize("lds", [1, 0])
+def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
+    """The decoder conv shapes (bf16), LDS-resident-input kernel and im2col kernel."""
+    B, T = 2, 3
+    S, H = B * T, W_
+    x1 = rnd(S, H, W_, c1, seed=70) * 2
+    x2 = rnd(B, H, W_, max(c2, 8), seed=71)[..., :c2]
+    w = rnd(co, c1 + c2, 3, 3, seed=72) / 12
+    dt = torch.bfloat16
+    mean = rnd(S * (c1 // 16), seed=73) * 0.2
+    rstd = rnd(S * (c1 // 16), seed=74) * 0.2 + 1
+    gam, bet = rnd(c1, seed=75) + 1, rnd(c1, seed=76)
+    xin = x1.to(dt).double()
+    if gn:
+        g = torch.arange(c1) // 16
+        sc = rstd.reshape(S, -1)[:, g].double() * gam.double()
+        sh = bet.double() - mean.reshape(S, -1)[:, g].double() * sc
+        xin = torch.relu(xin * sc[:, None, None, :] + sh[:, None, None, :]).to(dt).double()
+    if c2:
+        xin = torch.cat([xin, x2.to(dt).double().repeat_interleave(T, 0)], -1)
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), w.to(dt).double(), padding=1)
+    L.load().catseg_set_conv_lds(lds)
+    try:
+        out = torch.empty(S * H * W_, co, device=dev, dtype=dt)
+        tiles = H * W_ // ops.conv_tile_rows()
+        st = torch.empty(S * tiles * (co // 16) * 2, device=dev)
+        ops.conv3x3(x1.reshape(-1, c1).contiguous().to(dev, dt), w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt),
+                    out, S=S, H=H, W=W_, c1=c1, src2=x2.reshape(-1, c2).contiguous().to(dev, dt) if c2 else None, c2=c2,
+                    src2_div=T, stats=st, gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16) if gn else None)
+        close(out.reshape(S, H, W_, co).permute(0, 3, 1, 2), ref, atol=3e-2, rtol=1e-2, what="conv decoder")
+        m_ = torch.empty(S * (co // 16), device=dev)
+        r_ = torch.empty_like(m_)
+        ops.groupnorm_stats(st, S, tiles, co // 16, ops.conv_tile_rows() * 16, m_, r_)
+        gref = ref.reshape(S, co // 16, 16, H * W_)
+        close(m_, gref.mean((-1, -2)).reshape(-1), atol=2e-3, what="gn mean")
+    finally:
+        L.load().catseg_set_conv_lds(1)
+
+
+def test_convt64_gn():
+    S, H, W_, C, co = 3, 8, 16, 64, 48
+    x = rnd(S, H, W_, C, seed=60) * 2
+    mean, rstd = rnd(S * 4, seed=61) * 0.3, rnd(S * 4, seed=62) * 0.2 + 1
+    gam, bet = rnd(C, seed=63) + 1, rnd(C, seed=64)
+    wt, bt = rnd(C, co, 2, 2, seed=65) / 8, rnd(co, seed=66)
+    xd = x.reshape(-1, C).to(dev, torch.bfloat16)
+    out = torch.empty(S * 4 * H * W_, co, device=dev, dtype=torch.bfloat16)
+    Wg = wt.permute(2, 3, 1, 0).reshape(4 * co, C).contiguous()
+    ops.convt64_gn(xd, Wg.to(dev, torch.bfloat16), out, HW=H * W_,
+                   gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16), bias=bt.repeat(4).to(dev),
+                   store=(2, H, W_, co))
+    xb = x.to(torch.bfloat16).double()
+    g = torch.arange(C) // 16
+    sc = rstd.reshape(S, 4)[:, g].double() * gam.double()
+    sh = bet.double() - mean.reshape(S, 4)[:, g].double() * sc
+    z = torch.relu(xb * sc[:, None, None, :] + sh[:, None, None, :]).to(torch.bfloat16).double()
+    ref = F.conv_transpose2d(z.permute(0, 3, 1, 2), wt.to(torch.bfloat16).double(), bt.double(), stride=2)
+    close(out.reshape(S, 2 * H, 2 * W_, co).permute(0, 3, 1, 2), ref, atol=3e-2, rtol=1e-2, what="convt64_gn")
+
+
 def test_text_helpers():
     n, ctx, Wd, vocab = 3, 16, 64, 50
     tok = torch.randint(0, vocab, (n, ctx), generator=torch.Generator().manual_seed(3)).int()
