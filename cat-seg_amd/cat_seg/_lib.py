@@ -120,6 +120,7 @@ _SIGS = {
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
     "catseg_set_persistent": [i32],
     "catseg_set_conv_lds": [i32],
+    "catseg_set_gemm_variant": [i32],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
     "catseg_abi_version": [],
     "catseg_last_error": [],
@@ -144,7 +145,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = (C.c_char_p if name == "catseg_last_error" else
-                      None if name in ("catseg_set_persistent", "catseg_set_conv_lds") else C.c_int)
+                      None if name.startswith("catseg_set_") else C.c_int)
     _lib = lib
     return lib
 

@@ -320,6 +320,204 @@ __global__ __launch_bounds__(NT) void gemm2_kernel(const bf16* __restrict__ A, i
   }
 }
 
+// ------------------------------------------------------------------------------------
+// bf16 large GEMM (ViT QKV / out-proj / MLP): LDS-DMA staging (global_load_lds 16 B,
+// no VGPR round trip) into an S-stage ring of BK-deep K-tiles, with a counted `vmcnt` so
+// S-2 tiles stay in flight across the single raw barrier of each K-step.  The LDS image
+// of a tile is lane-linear per wave-instruction (64 x 16 B); the XOR swizzle
+// slot = chunk ^ ((row / RPB) % BKC) (RPB = rows per 256-byte bank row) is applied on the
+// per-lane GLOBAL source address and again on the fragment reads (the same involution
+// on both sides), which makes the 16 rows of a ds_read_b128 fragment read hit 16
+// distinct 16-byte bank slots.  WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN)
+// sub-tile of D = W . A^T (4 consecutive output columns per lane).  Needs K % BK == 0 and
+// N % BN == 0 (host-checked); rows >= M read row M-1 and are masked in the epilogue.
+// ------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N>
+DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // gfx9 s_waitcnt encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int BK>
+struct Swz {
+  static constexpr int BKC = BK / 8;            // 16-byte chunks per tile row
+  static constexpr int RPB = 256 / (BK * 2);    // tile rows per 256-byte bank row
+  static DEV int slot(int row, int ch) { return ch ^ ((row / RPB) % BKC); }
+};
+
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
+                                                            const bf16* __restrict__ W, int64_t ldw, int64_t M,
+                                                            int64_t K, int tiles_n, EpiArgs e) {
+  constexpr int NT3 = 64 * WGM * WGN;
+  using SW = Swz<BK>;
+  constexpr int BKC = SW::BKC;
+  constexpr int AG = BM * BKC / NT3, WG = BN * BKC / NT3, G = AG + WG;
+  static_assert(AG * NT3 == BM * BKC && WG * NT3 == BN * BKC, "tile / thread mismatch");
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  constexpr int STAGE = (BM + BN) * BK;           // elements per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+  const int wm = (wave % WGM) * WM, wn = (wave / WGM) * WN;
+  const bool ident = amap.d1 == 1 && amap.m1 >= M && amap.s1 == 1 && amap.m2 == 1 && amap.off == 0;
+
+  // per-instruction source pointers: chunk c = g*NT3 + tid -> LDS row c/BKC, slot c%BKC,
+  // which holds the global chunk slot(row, c%BKC)
+  const bf16* asrc[AG];
+#pragma unroll
+  for (int g = 0; g < AG; ++g) {
+    const int c = g * NT3 + tid, row = c / BKC, ch = SW::slot(row, c % BKC);
+    int64_t m = m0 + row;
+    if (m >= M) m = M - 1;
+    asrc[g] = A + (ident ? m : rowmap(amap, m)) * lda + ch * 8;
+  }
+  const bf16* wsrc[WG];
+#pragma unroll
+  for (int g = 0; g < WG; ++g) {
+    const int c = g * NT3 + tid, row = c / BKC, ch = SW::slot(row, c % BKC);
+    wsrc[g] = W + (n0 + row) * ldw + ch * 8;
+  }
+  auto issue = [&](int kt) {
+    bf16* sa = smem + (kt % S) * STAGE;
+    bf16* sw = sa + BM * BK;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int g = 0; g < AG; ++g)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[g] + k0), (lds_void_t*)(sa + (g * NT3 + wave * 64) * 8), 16, 0, 0);
+#pragma unroll
+    for (int g = 0; g < WG; ++g)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(wsrc[g] + k0), (lds_void_t*)(sw + (g * NT3 + wave * 64) * 8), 16, 0, 0);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r = lane & 15, q = lane >> 4;
+  const int ktiles = (int)(K / BK);
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < ktiles) issue(t);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    // tiles kt .. min(kt+S-2, ktiles-1) are in flight; retire tile kt
+    if (kt + S - 2 < ktiles) wait_vmcnt<(S - 2) * G>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();                 // tile kt visible; stage (kt-1)%S free
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + S - 1 < ktiles) issue(kt + S - 1);
+    const bf16* As = smem + (kt % S) * STAGE;
+    const bf16* Ws = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = ks * 4 + q;
+      s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int row = wm + 16 * j + r;
+        bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(row * BKC + SW::slot(row, ch)) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn + 16 * i + r;
+        afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(row * BKC + SW::slot(row, ch)) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
+    }
+  }
+  // ---- epilogue through LDS: rounds of 64 tile rows (JR m-fragments per wave row) are
+  // staged as fp32, then every thread walks whole output rows (coalesced stores); the
+  // accumulator indices stay compile-time constants (no scratch) ----
+  constexpr int JR = 4 / WGM, ROWS = 64, SLD = BN + 4;
+  static_assert(JR >= 1 && FM % JR == 0, "epilogue rounds");
+  static_assert(ROWS * SLD * 4 <= S * STAGE * 2, "epilogue stage exceeds LDS");
+  float* stg = reinterpret_cast<float*>(smem);
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  const int wmi = wave % WGM;
+#pragma unroll
+  for (int h = 0; h < FM / JR; ++h) {
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int jj = 0; jj < JR; ++jj)
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        *reinterpret_cast<f32x4*>(&stg[((wmi * JR + jj) * 16 + col) * SLD + wn + 16 * i + rq]) = acc[i][h * JR + jj];
+    __syncthreads();
+    for (int idx = tid; idx < ROWS * (BN / 4); idx += NT3) {
+      const int lrow = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+      const int wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
+      const int64_t m = m0 + wi * WM + (h * JR + jj) * 16 + rr;
+      if (m < M) epilogue4<TO>(e, m, n0 + c4, *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c4]));
+    }
+  }
+}
+
+EpiArgs make_epi(const CatsegGemmArgs* g) {
+  EpiArgs e;
+  e.bias = g->bias;
+  e.add = g->add; e.ld_add = g->ld_add; e.add_ncols = g->add_ncols;
+  e.addmap = RowMap{g->addmap.d1, g->addmap.m1, g->addmap.s1, g->addmap.d2, g->addmap.m2, g->addmap.s2, g->addmap.off};
+  e.act = g->act; e.alpha = g->alpha;
+  e.res = g->res; e.ld_res = g->ld_res; e.res2 = g->res2; e.ld_res2 = g->ld_res2;
+  e.out = g->out; e.ldo = g->ldo;
+  e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
+  e.cvt_cout = g->cvt_cout;
+  return e;
+}
+
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+bool launch3(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->N % BN != 0 || g->K % BK != 0) return false;
+  const EpiArgs e = make_epi(g);
+  RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
+  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
+  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
+                     st, (const bf16*)g->A, g->lda, am, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e);
+  return true;
+}
+
+int g_gemm_variant = 0;   // 0 = automatic; >0 forces a gemm3 tile (tests / tuning)
+
+// returns true when a gemm3 variant was launched
+template <typename TO>
+bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->K % 32 != 0 || g->lda % 8 != 0 || g->ldw % 8 != 0) return false;
+  int v = g_gemm_variant;
+  if (v < 0) return false;
+  if (v == 0) {
+    if (g->M < 1024 || g->K < 256) return false;
+    // Measured on ViT-L/14 shapes (M = 4616, tools/micro_gemm.py): the 256x256 tile wins
+    // when its tiles fit one round on the 256 CUs (QKV: 40 us vs 45), otherwise the
+    // 128x128 BK=64 tile at two blocks per CU (fc1 78 us vs 94, fc2 69 vs 115).
+    const int64_t t256 = ((g->M + 255) / 256) * (g->N / 256);
+    if (g->N % 256 == 0 && t256 >= 160 && t256 <= 256) v = 1;
+    else if (g->N % 128 == 0) v = 5;
+    else return false;
+  }
+  switch (v) {
+    case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
+    case 2: return launch3<TO, 256, 256, 2, 4, 4, 32>(g, st);
+    case 3: return launch3<TO, 256, 256, 2, 4, 3, 32>(g, st);
+    case 4: return launch3<TO, 128, 128, 2, 2, 4, 32>(g, st);
+    case 5: return launch3<TO, 128, 128, 2, 2, 2, 64>(g, st);
+    case 6: return launch3<TO, 256, 128, 4, 2, 3, 64>(g, st);
+    case 7: return launch3<TO, 128, 256, 2, 4, 4, 32>(g, st);
+    case 8: return launch3<TO, 256, 128, 4, 2, 4, 32>(g, st);
+    default: return false;
+  }
+}
+
 template <typename TA, typename TO, int BM, int BN>
 void launch(const CatsegGemmArgs* g, hipStream_t st) {
   EpiArgs e;
@@ -357,6 +555,7 @@ void launch2(const CatsegGemmArgs* g, hipStream_t st) {
 template <typename TA, typename TO>
 void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
   if constexpr (sizeof(TA) == 2) {
+    if (g->store_mode == 0 && try_gemm3<TO>(g, st)) return;
     const int64_t t128 = ((g->M + 127) / 128) * ((g->N + 127) / 128);
     if (g->N <= 64) launch2<TO, 128, 64>(g, st);
     else if (t128 < 512) launch2<TO, 64, 128>(g, st);     // fill 256 CUs x 2 slots
@@ -368,6 +567,8 @@ void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
 }
 
 }  // namespace
+
+extern "C" void catseg_set_gemm_variant(int v) { g_gemm_variant = v; }
 
 extern "C" int catseg_gemm(const CatsegGemmArgs* g, void* stream) {
   CATSEG_CHECK(g && g->A && g->W && g->out, "gemm: null pointer");

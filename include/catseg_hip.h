@@ -65,6 +65,11 @@ typedef struct {
 } CatsegGemmArgs;
 int catseg_gemm(const CatsegGemmArgs* args, void* stream);
 
+/* Tile selection of the bf16 GEMM: 0 = automatic (default), -1 = never the LDS-DMA
+ * pipelined kernel, 1..8 = force one of its tile / stage / K-depth configurations
+ * (gemm.hip try_gemm3) where the shape allows.  For A/B tests and tuning; process-wide. */
+void catseg_set_gemm_variant(int variant);
+
 /* ---------------------------------------------------------------------------
  * Row-block kernels over the 128-channel cost-embedding rows (K = 128).
  * Epilogue (applied on full output rows, 16-byte vectors): v = acc + bias[n]

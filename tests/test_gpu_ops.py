@@ -90,6 +90,36 @@ def test_gemm_convtranspose_store(dt):
     close(got, ref, atol=1e-5 if dt == torch.float32 else 2e-2, what="convT")
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_gemm_pipelined_variants(variant):
+    """Every LDS-DMA pipelined bf16 tile (gemm.hip gemm3_kernel) against fp64: ragged M
+    (sliver tile), a CLS-dropping row map, bias + QuickGELU + fp32 residual epilogue."""
+    B, L_, K, N = 3, 401, 512, 512
+    M = B * (L_ - 1)                                      # 1200 rows: 4 full 256-tiles + a sliver
+    A = rnd(B * L_, K, seed=40)
+    W = rnd(N, K, seed=41) / math.sqrt(K)
+    b = rnd(N, seed=42)
+    res = rnd(M, N, seed=43)
+    amap = rowmap(d1=L_ - 1, s1=L_, d2=1, m2=L_ - 1, s2=1, off=1)
+    arow = A.reshape(B, L_, K)[:, 1:].reshape(-1, K)
+    lib = L.load()
+    try:
+        lib.catseg_set_gemm_variant(variant)
+        for act, odt in ((L.ACT_QUICKGELU, torch.bfloat16), (L.ACT_NONE, torch.float32)):
+            out = torch.full((M, N), float("nan"), device=dev, dtype=odt)
+            r = res.to(dev, odt)
+            ops.gemm(A.to(dev, torch.bfloat16), W.to(dev, torch.bfloat16), out, M=M, bias=b.to(dev), act=act,
+                     res=r, amap=amap)
+            v = arow.to(torch.bfloat16).double() @ W.to(torch.bfloat16).double().T + b.double()
+            if act == L.ACT_QUICKGELU:
+                v = v * torch.sigmoid(1.702 * v)
+            ref = v + r.double().cpu()
+            close(out, ref, atol=1e-4 if odt == torch.float32 else 2e-2, rtol=0 if odt == torch.float32 else 1e-2,
+                  what=f"gemm3 variant {variant} act {act}")
+    finally:
+        lib.catseg_set_gemm_variant(0)
+
+
 def test_gemm_amap_cls_drop():
     B, L_, C = 2, 5, 16
     A = rnd(B * L_, C, seed=13)

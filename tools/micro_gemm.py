@@ -1,0 +1,57 @@
+"""Time the bf16 GEMM tile variants on the ViT-L/14@336 (B=8) shapes and check them.
+
+usage: python tools/micro_gemm.py [variants, default "-1,0,1,2,3,4,5,6,7,8"]
+Each variant is checked against torch (fp32 accumulate of the same bf16 operands) and
+timed over interleaved rounds in one process (median of per-round means).
+"""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
+import torch
+from cat_seg import ops
+from cat_seg import _lib as L
+
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "-1,0,1,2,3,4,5,6,7,8").split(",")]
+M = 8 * 577
+shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
+          "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True)}
+dev = "cuda"
+torch.manual_seed(0)
+lib = L.load()
+res = {}
+for name, (N, K, act, has_res) in shapes.items():
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    W = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.rand(N, device=dev) - 0.5
+    # the residual-stream GEMMs (out-proj, fc2) write the fp32 stream, as in the engine
+    R = (torch.rand(M, N, device=dev) - 0.5) if has_res else None
+    out = torch.empty(M, N, device=dev, dtype=torch.float32 if has_res else torch.bfloat16)
+    ref = A.float() @ W.float().t() + bias
+    if act == L.ACT_QUICKGELU:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    if R is not None:
+        ref = ref + R.float()
+    def run():
+        ops.gemm(A, W, out, bias=bias, act=act, res=R)
+    for v in variants:
+        lib.catseg_set_gemm_variant(v)
+        out.zero_()
+        run(); torch.cuda.synchronize()
+        err = (out.float() - ref).abs().max().item()
+        res[(name, v)] = {"err": err, "t": []}
+    flops = 2 * M * N * K
+    for rnd in range(7):
+        for v in variants:
+            lib.catseg_set_gemm_variant(v)
+            run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                run()
+            e1.record(); torch.cuda.synchronize()
+            res[(name, v)]["t"].append(e0.elapsed_time(e1) / 20)
+    for v in variants:
+        t = sorted(res[(name, v)]["t"])[3]
+        print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  "
+              f"max_err {res[(name, v)]['err']:.3e}", flush=True)
+lib.catseg_set_gemm_variant(0)
