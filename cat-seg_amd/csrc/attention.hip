@@ -51,47 +51,59 @@ DEV int swin_region(const AttnP& p, int wloc, int i) {
   return hb * 3 + wb;
 }
 
-template <typename T, int D, int NW, int KB, int QT, int GEO>
+// SWM: the shifted-window -100 region mask (model.py:161-183) is applied by the MFMA
+// itself: each staged key row gets XD extra dims holding the one-hot of its region
+// (3 x 3 regions) and each query fragment the matching dims -100/scale for every other
+// region, so S = q.k + mask comes out of the same instruction chain and the softmax
+// loop carries no per-score mask work (this kernel is VALU-bound: head_dim 32 gives one
+// 16x16x32 MFMA per 256 scores).  The softmax row sums come from the MFMA too: a
+// constant all-ones A fragment times P^T adds one MFMA per 32 keys instead of one VALU
+// add per score.
+template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   constexpr int NT = NW * 64;
+  constexpr bool BF = sizeof(T) == 2;
   constexpr int VN = Vec16<T>::N;
-  constexpr int KP = D + (sizeof(T) == 2 ? 8 : 4);     // K row stride (elements)
+  constexpr int XD = SWM ? (BF ? 32 : 12) : 0;          // region dims appended to K / Q
+  constexpr int KP = D + XD + (BF ? 8 : 4);             // K row stride (elements)
   constexpr int VP = KB + 4;                            // V^T row stride
   constexpr int DT = D / 16;                            // d tiles of O^T
   constexpr int KT = KB / 16;                           // key tiles per block
-  constexpr int QF = sizeof(T) == 2 ? D / 32 : D / 4;
-  using QFrag = typename std::conditional<sizeof(T) == 2, s16x8, float>::type;
+  constexpr int KS = BF ? 32 : 4;                       // K depth of one MFMA
+  constexpr int QF = D / KS, QX = XD / KS;
+  constexpr int LC = GEO ? (GEO / 2) * (GEO / 2) : 0;   // compile-time sequence length
+  constexpr int KTV = LC ? (LC + 15) / 16 : KT;         // key tiles that can hold a key
+  static_assert(!LC || (LC <= KB && LC % 16 == 0), "fixed window must fill whole key tiles");
+  using QFrag = typename std::conditional<BF, s16x8, float>::type;
   __shared__ __attribute__((aligned(16))) T Ks[KB * KP];
   __shared__ __attribute__((aligned(16))) T Vt[D * VP];
-  __shared__ signed char kreg_s[KB];                    // SW-MSA region id of each staged key
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int s = blockIdx.y / p.H;
   const int h = blockIdx.y % p.H;
   const int g = lane >> 4;
+  const int L = LC ? LC : p.L;
   const T* Kg = reinterpret_cast<const T*>(p.k);
   const T* Vg = reinterpret_cast<const T*>(p.v);
   const int nwin = p.mode == 1 ? (GEO ? 4 : (p.img_h / p.ws) * (p.img_w / p.ws)) : 1;
   const int wloc = p.mode == 1 ? s % nwin : 0;
-  const bool swmask = p.mode == 1 && p.shift > 0;
   const float sl2 = p.scale * 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
-  int qi[QT], qreg[QT];
+  int qi[QT];
   int64_t qrow[QT];
   bool q_ok[QT], tile_live[QT];
-  QFrag qf[QT][QF];
-  f32x4 o[QT][DT];
-  float m_run[QT], l_run[QT];
+  QFrag qf[QT][QF + QX];
+  f32x4 o[QT][DT], osum[QT];
+  float m_run[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     const int q0 = (blockIdx.x * NW * QT + wave * QT + t) * 16;
-    tile_live[t] = q0 < p.L;
+    tile_live[t] = q0 < L;
     qi[t] = q0 + (lane & 15);
-    q_ok[t] = qi[t] < p.L;
+    q_ok[t] = qi[t] < L;
     qrow[t] = seq_row<GEO>(p, s, q_ok[t] ? qi[t] : 0);
-    qreg[t] = swmask ? swin_region<GEO>(p, wloc, q_ok[t] ? qi[t] : 0) : 0;
     const T* Q = reinterpret_cast<const T*>(p.q) + qrow[t] * p.ld + h * D;
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (BF) {
 #pragma unroll
       for (int ks = 0; ks < QF; ++ks) {
         uint4 u = q_ok[t] ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
@@ -101,22 +113,48 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
 #pragma unroll
       for (int ks = 0; ks < QF; ++ks) qf[t][ks] = q_ok[t] ? to_f<T>(Q[4 * ks + g]) : 0.f;
     }
+    if constexpr (SWM) {
+      const int qreg = swin_region<GEO>(p, wloc, q_ok[t] ? qi[t] : 0);
+      const float neg = -100.f / p.scale;                // raw-score units (scores are scaled later)
+      if constexpr (BF) {
+        s16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int dim = 8 * g + j;
+          f[j] = (short)f2bf(dim < 9 && dim != qreg ? neg : 0.f);
+        }
+        qf[t][QF] = f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < QX; ++e) {
+          const int dim = 4 * e + g;
+          qf[t][QF + e] = dim < 9 && dim != qreg ? neg : 0.f;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < DT; ++i) o[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    osum[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     m_run[t] = -1e30f;
-    l_run[t] = 0.f;
+  }
+  QFrag ones;
+  if constexpr (BF) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
+  } else {
+    ones = 1.f;
   }
 
-  const int nblk = (p.L + KB - 1) / KB;
+  const int nblk = (L + KB - 1) / KB;
   for (int blk = 0; blk < nblk; ++blk) {
     const int k0 = blk * KB;
-    // ---- stage K [key][d] and V^T [d][key] ----
+    // ---- stage K [key][d (+ region one-hot)] and V^T [d][key] ----
     constexpr int CPK = D / VN;
     for (int c = tid; c < KB * CPK; c += NT) {
       const int kk = c / CPK, d0 = (c % CPK) * VN;
       const int key = k0 + kk;
       uint4 ku = make_uint4(0, 0, 0, 0), vu = make_uint4(0, 0, 0, 0);
-      if (key < p.L) {
+      if (key < L) {
         const int64_t r = seq_row<GEO>(p, s, key);
         ku = ld16(Kg + r * p.ld + h * D + d0);
         vu = ld16(Vg + r * p.ld + h * D + d0);
@@ -125,75 +163,79 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
       const T* ve = reinterpret_cast<const T*>(&vu);
 #pragma unroll
       for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
-      if (swmask && d0 == 0) kreg_s[kk] = key < p.L ? (signed char)swin_region<GEO>(p, wloc, key) : (signed char)-1;
+      if constexpr (SWM) {
+        if (d0 == 0) {
+          const int kreg = key < L ? swin_region<GEO>(p, wloc, key) : -1;
+#pragma unroll
+          for (int e = 0; e < XD; ++e) Ks[kk * KP + D + e] = from_f<T>(e == kreg ? 1.f : 0.f);
+        }
+      }
     }
     __syncthreads();
+    const bool tail = !LC && k0 + KB > L;                 // block-uniform: keys past L exist
 
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       if (!tile_live[t]) continue;
-      // ---- S^T tiles ----
+      // ---- S^T tiles (raw q.k, + region mask dims) ----
       f32x4 st[KT];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
-        const int kr = kt * 16 + (lane & 15);
-        if constexpr (sizeof(T) == 2) {
+        if (kt < KTV) {
+          const int kr = kt * 16 + (lane & 15);
 #pragma unroll
-          for (int ks = 0; ks < QF; ++ks) {
-            const s16x8 kf = *reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]);
-            a = mfma_bf16(kf, qf[t][ks], a);
+          for (int ks = 0; ks < QF + QX; ++ks) {
+            if constexpr (BF) {
+              const s16x8 kf = *reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]);
+              a = mfma_bf16(kf, qf[t][ks], a);
+            } else {
+              a = mfma_f32(Ks[kr * KP + 4 * ks + g], qf[t][ks], a);
+            }
           }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < QF; ++ks) a = mfma_f32(to_f<T>(Ks[kr * KP + 4 * ks + g]), qf[t][ks], a);
         }
         st[kt] = a;
       }
-      // ---- mask + online softmax (per query column) ----
+      if (tail || CAUSAL) {
+#pragma unroll
+        for (int kt = 0; kt < KTV; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + kt * 16 + 4 * g + r;
+            if (key >= L || (CAUSAL && key > qi[t])) st[kt][r] = -INFINITY;
+          }
+      }
+      // ---- online softmax (per query column): max, then exp2(s * sl2 - m * sl2) ----
       float bmax = -1e30f;
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
+      for (int kt = 0; kt < KTV; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + kt * 16 + 4 * g + r;
-          float x = st[kt][r] * sl2;
-          if (key >= p.L || (p.causal && key > qi[t])) x = -INFINITY;
-          else if (swmask && kreg_s[kt * 16 + 4 * g + r] != qreg[t]) x += -100.f * 1.4426950408889634f;
-          st[kt][r] = x;
-          bmax = fmaxf(bmax, x);
-        }
-      }
+        for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, st[kt][r]);
       bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
       bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
       const float m_new = fmaxf(m_run[t], bmax);
-      const float alpha = exp2f(m_run[t] - m_new);
+      const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * sl2);
       m_run[t] = m_new;
-      float psum = 0.f;
+      const float nb = -m_new * sl2;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(st[kt][r] - m_new);
-          st[kt][r] = e;
-          psum += e;
-        }
-      l_run[t] = l_run[t] * alpha + psum;
+        for (int r = 0; r < 4; ++r)
+          st[kt][r] = kt < KTV ? __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb)) : 0.f;
+      if (blk > 0) {
 #pragma unroll
-      for (int i = 0; i < DT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[t][i][r] *= alpha;
+        for (int i = 0; i < DT; ++i) o[t][i] *= alpha;
+        osum[t] *= alpha;
+      }
 
-      // ---- O^T += V^T . P^T ----
-      if constexpr (sizeof(T) == 2) {
+      // ---- O^T += V^T . P^T ; row sums += 1 . P^T ----
+      if constexpr (BF) {
 #pragma unroll
         for (int u = 0; u < KB / 32; ++u) {
-          s16x8 pb;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            pb[j] = (short)f2bf(st[2 * u][j]);
-            pb[4 + j] = (short)f2bf(st[2 * u + 1][j]);
-          }
+          if (2 * u >= KTV) continue;
+          uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                                f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+          const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
             const T* vr = &Vt[(dt * 16 + (lane & 15)) * VP + 32 * u + 4 * g];
@@ -202,30 +244,30 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
             uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
             o[t][dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[t][dt]);
           }
+          osum[t] = mfma_bf16(ones, pb, osum[t]);
         }
       } else {
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt)
+        for (int kt = 0; kt < KTV; ++kt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+          for (int r = 0; r < 4; ++r) {
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
               const float va = to_f<T>(Vt[(dt * 16 + (lane & 15)) * VP + kt * 16 + 4 * g + r]);
               o[t][dt] = mfma_f32(va, st[kt][r], o[t][dt]);
             }
+            osum[t] = mfma_f32(ones, st[kt][r], osum[t]);
+          }
       }
     }
     __syncthreads();
   }
 
-  // ---- normalize + store: lane holds O^T[d = dt*16 + 4g + r][q] ----
+  // ---- normalize + store: lane holds O^T[d = dt*16 + 4g + r][q]; osum rows all = l[q] ----
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    float l = l_run[t];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
     if (!q_ok[t]) continue;
-    const float inv = 1.f / l;
+    const float inv = 1.f / osum[t][0];
     T* O = reinterpret_cast<T*>(p.out) + qrow[t] * p.ldo + h * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
@@ -235,22 +277,34 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   }
 }
 
-template <typename T, int D, int NW, int KB, int QT, int GEO = 0>
+template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
 void launch(const AttnP& p, hipStream_t st) {
   constexpr int QW = 16 * NW * QT;
   dim3 grid((unsigned)((p.L + QW - 1) / QW), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((attn_kernel<T, D, NW, KB, QT, GEO>), grid, dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((attn_kernel<T, D, NW, KB, QT, GEO, SWM, CAUSAL>), grid, dim3(NW * 64), 0, st, p);
+}
+
+template <typename T, int D, int NW, int KB, int QT, int GEO>
+void launch_win(const AttnP& p, hipStream_t st) {
+  if (p.shift > 0) launch<T, D, NW, KB, QT, GEO, true, false>(p, st);
+  else launch<T, D, NW, KB, QT, GEO, false, false>(p, st);
+}
+
+template <typename T, int D>
+void launch_dense(const AttnP& p, hipStream_t st) {
+  if (p.causal) launch<T, D, 4, 64, 2, 0, false, true>(p, st);
+  else launch<T, D, 4, 64, 2, 0, false, false>(p, st);
 }
 
 template <typename T>
 int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
   if (p.mode == 1) {
-    if (head_dim == 32 && p.img_h == 24 && p.img_w == 24 && p.ws == 12) { launch<T, 32, 9, 160, 1, 24>(p, st); return 0; }
-    if (head_dim == 32 && p.L <= 160) { launch<T, 32, 9, 160, 1>(p, st); return 0; }
-    if (head_dim == 32) { launch<T, 32, 4, 64, 2>(p, st); return 0; }
+    if (head_dim == 32 && p.img_h == 24 && p.img_w == 24 && p.ws == 12) { launch_win<T, 32, 9, 160, 1, 24>(p, st); return 0; }
+    if (head_dim == 32 && p.L <= 160) { launch_win<T, 32, 9, 160, 1, 0>(p, st); return 0; }
+    if (head_dim == 32) { launch_win<T, 32, 4, 64, 2, 0>(p, st); return 0; }
   } else {
-    if (head_dim == 64) { launch<T, 64, 4, 64, 2>(p, st); return 0; }
-    if (head_dim == 32) { launch<T, 32, 4, 64, 2>(p, st); return 0; }
+    if (head_dim == 64) { launch_dense<T, 64>(p, st); return 0; }
+    if (head_dim == 32) { launch_dense<T, 32>(p, st); return 0; }
   }
   return -1;
 }

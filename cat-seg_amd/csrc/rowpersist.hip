@@ -20,6 +20,8 @@ constexpr int NW = 8, NT = NW * 64;
 constexpr int BM = 32;           // rows per tile
 constexpr int LDX = KD + 8;      // LDS row stride of sX (272 B: conflict-free ds_read_b128)
 constexpr int CPT = BM * 16 / NT; // 16-byte chunks of a tile per thread (= 1)
+constexpr int DEPTH = 3;          // tiles of input rows in flight per workgroup
+constexpr int DEPTH_MLP = 1;      // (the MLP holds both weight matrices in registers: no room)
 static_assert(CPT == 1, "one chunk per thread");
 
 struct PEpi {
@@ -102,31 +104,39 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
       wf[i][ks] = *reinterpret_cast<s16x8*>(&u);
     }
   const int64_t ntiles = (M + BM - 1) / BM;
-  int64_t tile = blockIdx.x;
-  uint4 rx = make_uint4(0, 0, 0, 0);
-  uint4 rres[PER];
-  auto fetch = [&](int64_t t) {
-    rx = fetch_chunk(X, ldx, t * BM, M);
+  const int64_t G = gridDim.x;
+  // register ring: the rows (and residual rows) of the next DEPTH tiles are in flight
+  // while this one computes (one tile per CU in flight left the loop latency-bound)
+  uint4 rx[DEPTH];
+  uint4 rres[DEPTH][PER];
+  auto fetch = [&](uint4& x, uint4* rr, int64_t t) {
+    x = fetch_chunk(X, ldx, t * BM, M);
     if constexpr (RES) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const int i = threadIdx.x + k * NT, r = i / CH, c = (i % CH) * 8;
         const int64_t m = t * BM + r;
-        rres[k] = m < M ? ld16(e.res + m * e.ld_res + c) : make_uint4(0, 0, 0, 0);
+        rr[k] = m < M ? ld16(e.res + m * e.ld_res + c) : make_uint4(0, 0, 0, 0);
       }
     }
   };
-  if (tile < ntiles) fetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (blockIdx.x + d * G < ntiles) fetch(rx[d], rres[d], blockIdx.x + d * G);
+  for (int64_t base = blockIdx.x; base < ntiles; base += DEPTH * G)
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) {
+    const int64_t tile = base + d * G;
+    if (tile >= ntiles) break;
     const int64_t m0 = tile * BM;
-    put_chunk(rx, ln_g, ln_b, eps, sX);
+    put_chunk(rx[d], ln_g, ln_b, eps, sX);
     uint4 res_cur[PER];
     if constexpr (RES) {
 #pragma unroll
-      for (int k = 0; k < PER; ++k) res_cur[k] = rres[k];
+      for (int k = 0; k < PER; ++k) res_cur[k] = rres[d][k];
     }
     __syncthreads();
-    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);     // prefetch the next tile
+    if (tile + DEPTH * G < ntiles) fetch(rx[d], rres[d], tile + DEPTH * G);   // refill this ring slot
     f32x4 acc[FN][FM];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -211,20 +221,26 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     w2f[ks] = *reinterpret_cast<s16x8*>(&u);
   }
   const int64_t ntiles = (M + BM - 1) / BM;
-  int64_t tile = blockIdx.x;
+  const int64_t G = gridDim.x;
   const int er = threadIdx.x >> 4, ec = (threadIdx.x & 15) * 8;   // epilogue item = the thread's input chunk
-  uint4 ry = make_uint4(0, 0, 0, 0), rr2 = make_uint4(0, 0, 0, 0);
-  auto fetch = [&](int64_t t) {
-    ry = fetch_chunk(Y, ldy, t * BM, M);
-    if constexpr (RES2) rr2 = fetch_chunk(e.res2, e.ld_res2, t * BM, M);
+  uint4 ry[DEPTH_MLP] = {}, rr2[DEPTH_MLP] = {};
+  auto fetch = [&](uint4& y, uint4& r2, int64_t t) {
+    y = fetch_chunk(Y, ldy, t * BM, M);
+    if constexpr (RES2) r2 = fetch_chunk(e.res2, e.ld_res2, t * BM, M);
   };
-  if (tile < ntiles) fetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+  for (int d = 0; d < DEPTH_MLP; ++d)
+    if (blockIdx.x + d * G < ntiles) fetch(ry[d], rr2[d], blockIdx.x + d * G);
+  for (int64_t base = blockIdx.x; base < ntiles; base += DEPTH_MLP * G)
+#pragma unroll
+  for (int d = 0; d < DEPTH_MLP; ++d) {
+    const int64_t tile = base + d * G;
+    if (tile >= ntiles) break;
     const int64_t m0 = tile * BM;
-    const uint4 y_raw = ry, r2_cur = rr2;     // residuals of this tile stay in registers
-    put_chunk(ry, ln_g, ln_b, eps, sX);
+    const uint4 y_raw = ry[d], r2_cur = rr2[d];     // residuals of this tile stay in registers
+    put_chunk(ry[d], ln_g, ln_b, eps, sX);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+    if (tile + DEPTH_MLP * G < ntiles) fetch(ry[d], rr2[d], tile + DEPTH_MLP * G);
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       f32x4 acc1[2][FM];
@@ -250,8 +266,14 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
           float v[4];
+          if constexpr (ACT == ACT_GELU) {
+            const f32x2 g0 = gelu2(f32x2{acc1[i][j][0] + bb[0], acc1[i][j][1] + bb[1]});
+            const f32x2 g1 = gelu2(f32x2{acc1[i][j][2] + bb[2], acc1[i][j][3] + bb[3]});
+            v[0] = g0.x; v[1] = g0.y; v[2] = g1.x; v[3] = g1.y;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r] + bb[r]);
+            for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r] + bb[r]);
+          }
           store4<bf16>(&sH[(16 * j + r16) * LDH + hh], v);
         }
       }
