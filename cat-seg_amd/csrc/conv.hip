@@ -362,13 +362,112 @@ __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, 
   out[(b * Tout + cls) * (int64_t)HW + pix] = acc;
 }
 
+// ---------------- head conv, banded (bf16 input) ---------------------------------------
+// One workgroup = BR output rows of one slice.  The BR + 2 input rows (+ zero halo) are
+// staged ONCE into LDS with GroupNorm+ReLU applied in fp32 and stored as fp16 (10-bit
+// mantissa: the head's 288-term dot product then carries ~4x less input rounding than a
+// bf16 stage would), pixel stride C + 8 halves (conflict-free 16-byte reads across
+// consecutive pixels); the weights sit in LDS as fp16 pairs (broadcast reads).  Each
+// output is 9 x C/2 v_dot2c_f32_f16 (fp32 accumulate).  Replaces the per-tap global
+// gathers of head_kernel (every input element was re-read and re-normalised 9 times).
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+constexpr int HBR = 8;            // output rows per workgroup
+
+template <int C>
+__global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__ x, int Tn, int H, int W,
+                                                        const float* __restrict__ w, float bias, const float* mean,
+                                                        const float* rstd, const float* gamma, const float* beta,
+                                                        int cpg, const int32_t* classes, int Tout, float* out) {
+  constexpr int CPX = C / 8, CP = C + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  _Float16* wl = reinterpret_cast<_Float16*>(smem);                    // [9][C]
+  float* ssc = reinterpret_cast<float*>(smem + 9 * C * 2);              // [C]
+  float* ssh = ssc + C;                                                 // [C]
+  _Float16* tile = reinterpret_cast<_Float16*>(smem + 9 * C * 2 + 2 * C * 4);   // [HBR+2][W+2][CP]
+  const int64_t s = blockIdx.y;
+  const int y0 = blockIdx.x * HBR;
+  const int rows = min(HBR, H - y0);
+  const int WP = W + 2;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 9 * C; i += 256) wl[i] = (_Float16)w[i];
+  const int groups = C / cpg;
+  for (int c = tid; c < C; c += 256) {
+    if (mean) {
+      const float sc = rstd[s * groups + c / cpg] * gamma[c];
+      ssc[c] = sc;
+      ssh[c] = beta[c] - mean[s * groups + c / cpg] * sc;
+    } else {
+      ssc[c] = 1.f;
+      ssh[c] = 0.f;
+    }
+  }
+  __syncthreads();
+  const bool relu = mean != nullptr;
+  const int64_t HW = (int64_t)H * W;
+  const bf16* xs = x + s * HW * C;
+  const int total = (rows + 2) * WP * CPX;
+  for (int i0 = 0; i0 < total; i0 += 256 * 4) {
+    uint4 u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * 256 + tid;
+      const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
+      const int yy = y0 - 1 + r, xx = xc - 1;
+      u[j] = (i < total && yy >= 0 && yy < H && xx >= 0 && xx < W) ? ld16(xs + ((int64_t)yy * W + xx) * C + ch * 8)
+                                                                   : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * 256 + tid;
+      if (i >= total) continue;
+      const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
+      const int yy = y0 - 1 + r, xx = xc - 1;
+      const bool inside = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const bf16* e = reinterpret_cast<const bf16*>(&u[j]);
+      _Float16 hv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = fmaf(bf2f(e[k]), ssc[ch * 8 + k], ssh[ch * 8 + k]);
+        if (relu) v = fmaxf(v, 0.f);
+        hv[k] = (_Float16)(inside ? v : 0.f);
+      }
+      st16(&tile[pos * CP + ch * 8], *reinterpret_cast<uint4*>(hv));
+    }
+  }
+  __syncthreads();
+  const int b = (int)(s / Tn), t = (int)(s % Tn);
+  const int cls = classes ? classes[(int64_t)b * Tn + t] : t;
+  float* o = out + ((int64_t)b * Tout + cls) * HW + (int64_t)y0 * W;
+  for (int idx = tid; idx < rows * W; idx += 256) {
+    const int yy = idx / W, xx = idx - yy * W;
+    float acc = bias;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const _Float16* px = &tile[((yy + dy) * WP + xx + dx) * CP];
+        const _Float16* wt = &wl[(dy * 3 + dx) * C];
+#pragma unroll
+        for (int k = 0; k < CPX; ++k) {
+          const uint4 a = ld16(px + k * 8), bw = ld16(wt + k * 8);
+          const h2* ah = reinterpret_cast<const h2*>(&a);
+          const h2* bh = reinterpret_cast<const h2*>(&bw);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_fdot2(ah[m], bh[m], acc, false);
+        }
+      }
+    o[idx] = acc;
+  }
+}
+
 }  // namespace
 
 extern "C" int catseg_conv_tile_rows(void) { return BM; }
 
-int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st);   // conv_lds.hip
-static bool g_conv_lds = true;
-extern "C" void catseg_set_conv_lds(int enable) { g_conv_lds = enable != 0; }
+int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st);    // conv_lds.hip
+int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st);   // conv_ring.hip
+static int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = im2col only
+extern "C" void catseg_set_conv_lds(int mode) { g_conv_mode = mode; }
 
 extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a && a->src1 && a->weight && a->out, "conv3x3: null pointer");
@@ -392,7 +491,8 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.out = a->out; p.stats = a->stats; p.scpg = a->stats_cpg;
   hipStream_t st = (hipStream_t)stream;
-  if (g_conv_lds && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
+  if (g_conv_mode >= 2 && catseg_conv3x3_ring(a, st) == 0) return catseg_launch_status("conv3x3_ring");
+  if (g_conv_mode >= 1 && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
   if (a->dtype == CATSEG_BF16) launch_conv<bf16>(p, st);
   else launch_conv<float>(p, st);
   return catseg_launch_status("conv3x3");
@@ -429,6 +529,19 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                                       int dtype, void* stream) {
   CATSEG_CHECK(x && weight && out && C % 8 == 0 && C <= 256 && B > 0 && T > 0, "conv3x3_head: bad args");
   CATSEG_CHECK(!mean || (rstd && gamma && beta && cpg > 0 && C % cpg == 0), "conv3x3_head: bad GN args");
+  if (dtype == CATSEG_BF16 && C == 32 && W <= 128) {
+    const size_t shb = 9 * C * 2 + 2 * C * 4 + (size_t)(HBR + 2) * (W + 2) * (C + 8) * 2;
+    static bool configured = false;
+    if (!configured) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_band_kernel<32>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      configured = true;
+    }
+    hipLaunchKernelGGL(head_band_kernel<32>, dim3((unsigned)((H + HBR - 1) / HBR), (unsigned)(B * T)), dim3(256), shb,
+                       (hipStream_t)stream, (const bf16*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg,
+                       classes, T_out, out);
+    return catseg_launch_status("conv3x3_head");
+  }
   const dim3 grid((unsigned)(((int64_t)H * W + 255) / 256), (unsigned)(B * T));
   const size_t sh = 11 * C * sizeof(float);
   if (dtype == CATSEG_BF16)

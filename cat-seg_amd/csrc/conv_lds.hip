@@ -252,7 +252,7 @@ int launch(const LdsConvP& p, hipStream_t st) {
   const unsigned grid = (unsigned)(p.S * p.H * p.W / TP);
   static size_t configured = 0;
   if (sh > configured) {   // > 64 KiB dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_lds_kernel<C, COUT>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_lds_kernel<C, COUT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }

@@ -335,6 +335,51 @@ __global__ void post_kernel(const float* lg, int64_t planes, int h, int w, int c
   }
 }
 
+// One workgroup per (plane, band of output rows): the crop region's sigmoids are computed
+// ONCE into LDS (each source logit feeds ~(H/ch)^2 outputs), then every thread writes 4
+// consecutive outputs of a row (16-byte stores) from 4 LDS taps each.
+constexpr int POST_ROWS = 48;    // output rows per workgroup
+__global__ __launch_bounds__(256) void post_band_kernel(const float* lg, int h, int w, int ch, int cw, float* out,
+                                                        int H, int W) {
+  extern __shared__ float sgm[];           // sigmoid of the source rows this band reads [rows][cw]
+  const int64_t pl = blockIdx.y;
+  const int oy0 = blockIdx.x * POST_ROWS, oy1 = min(H, oy0 + POST_ROWS);
+  const float sy = (float)ch / (float)H, sx = (float)cw / (float)W;
+  int ya, yb, yt;
+  float lt;
+  lin_idx(oy0, ch, sy, ya, yt, lt);
+  lin_idx(oy1 - 1, ch, sy, yt, yb, lt);
+  const int nrows = yb - ya + 1;
+  const float* src = lg + pl * (int64_t)h * w;
+  for (int i = threadIdx.x; i < nrows * cw; i += 256) {
+    const int r = i / cw, c = i - r * cw;
+    sgm[i] = 1.f / (1.f + __expf(-src[(int64_t)(ya + r) * w + c]));
+  }
+  __syncthreads();
+  const int W4 = W / 4;
+  float* o = out + pl * (int64_t)H * W;
+  for (int idx = threadIdx.x; idx < (oy1 - oy0) * W4; idx += 256) {
+    const int ry = idx / W4, x4 = (idx - ry * W4) * 4;
+    const int y = oy0 + ry;
+    int y0, y1;
+    float ly;
+    lin_idx(y, ch, sy, y0, y1, ly);
+    const float* r0 = sgm + (y0 - ya) * cw;
+    const float* r1 = sgm + (y1 - ya) * cw;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int x0, x1;
+      float lx;
+      lin_idx(x4 + k, cw, sx, x0, x1, lx);
+      const float top = fmaf(lx, r0[x1] - r0[x0], r0[x0]);
+      const float bot = fmaf(lx, r1[x1] - r1[x0], r1[x0]);
+      v[k] = fmaf(ly, bot - top, top);
+    }
+    *reinterpret_cast<float4*>(o + (int64_t)y * W + x4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // ---------------- text: token embedding + EOT gather ------------------------------
 __global__ void token_embed_kernel(const int32_t* tok, int64_t n, int ctx, const float* emb, const float* pos, int width,
                                    float* x) {
@@ -462,6 +507,14 @@ extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, 
   CATSEG_CHECK(logits && out && B > 0 && T > 0 && H > 0 && W > 0, "postprocess: bad args");
   CATSEG_CHECK(crop_h > 0 && crop_h <= h && crop_w > 0 && crop_w <= w, "postprocess: bad crop");
   const int64_t total = B * T * (int64_t)H * W;
+  // banded kernel: source rows of one band (<= POST_ROWS * ch / H + 2) fit LDS
+  const int64_t band_src_rows = (int64_t)POST_ROWS * crop_h / H + 3;
+  if (W % 4 == 0 && band_src_rows * crop_w * 4 <= 64 * 1024) {
+    hipLaunchKernelGGL(post_band_kernel, dim3((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T)),
+                       dim3(256), (size_t)(band_src_rows * crop_w * 4), (hipStream_t)stream, logits, h, w, crop_h,
+                       crop_w, out, H, W);
+    return catseg_launch_status("postprocess");
+  }
   hipLaunchKernelGGL(post_kernel, dim3(grid_for(total, 65536)), dim3(256), 0, (hipStream_t)stream, logits, B * T, h, w,
                      crop_h, crop_w, out, H, W);
   return catseg_launch_status("postprocess");

@@ -396,10 +396,14 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c + 4]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += e.bias[c + j];
-      const int64_t kk = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
-      const int64_t sl = m / (hin * win), y = (m / win) % hin, x = m % win;
-      const int64_t ky = c / (kk * cout), kx = (c / cout) % kk, co = c % cout;
-      st16(e.out + ((sl * hin * kk + y * kk + ky) * (win * kk) + x * kk + kx) * cout + co, pack8(v));
+      // ConvTranspose scatter, 32-bit index math (m < 2^31, host-checked): kk = 2
+      const uint32_t hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
+      const uint32_t mu = (uint32_t)m, mw = mu / win, x = mu - mw * win;
+      const uint32_t sl = mw / hin, y = mw - sl * hin;
+      const uint32_t ky = (uint32_t)c / (2 * cout), rem = (uint32_t)c - ky * 2 * cout;
+      const uint32_t kx = rem / cout, co = rem - kx * cout;
+      const int64_t orow = ((int64_t)(sl * hin + y) * 2 + ky) * (2 * win) + x * 2 + kx;
+      st16(e.out + orow * cout + co, pack8(v));
     }
     __syncthreads();
   }
@@ -420,8 +424,8 @@ unsigned persist_grid(int64_t M, int per_cu = 1) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
   const int64_t tiles = (M + BM - 1) / BM;
@@ -462,7 +466,8 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
   CATSEG_CHECK(cpg > 0 && K64 % cpg == 0, "convt64_gn: bad GroupNorm grouping");
   CATSEG_CHECK(epi->store_mode == 1 && epi->cvt_cout % 8 == 0 && N == (int64_t)epi->cvt_k * epi->cvt_k * epi->cvt_cout,
                "convt64_gn: needs the ConvTranspose scatter store");
-  CATSEG_CHECK(N == 192, "convt64_gn: N = 192 (k=2, 48 channels) only");
+  CATSEG_CHECK(N == 192 && epi->cvt_k == 2, "convt64_gn: N = 192 (k=2, 48 channels) only");
+  CATSEG_CHECK(M < (1LL << 31), "convt64_gn: row count must fit 31 bits");
   const PEpi e = make_pepi(epi);
   hipLaunchKernelGGL((pconvt64_kernel<192>), dim3(persist_grid((M + 1) / 2, 2)), dim3(NT4), 0, (hipStream_t)stream,
                      (const bf16*)x, M, HW, mean, rstd, gamma, beta, cpg, (const bf16*)w, e);

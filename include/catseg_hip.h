@@ -112,8 +112,10 @@ int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const float* mean, c
                       const float* gamma, const float* beta, int cpg, const void* w, int64_t N,
                       const CatsegRowsEpi* epi, void* stream);
 
-/* Select the LDS-resident-input bf16 conv3x3 (default 1) or the im2col one (0), for A/B tests. */
-void catseg_set_conv_lds(int enable);
+/* Select the bf16 conv3x3 kernel family, for A/B tests (process-wide): 2 = row-ring kernel
+ * with register-resident weights (default), 1 = LDS-tile kernel, 0 = im2col only.  Shapes a
+ * family does not cover fall through to the next one down. */
+void catseg_set_conv_lds(int mode);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */

@@ -391,9 +391,9 @@ def test_rows_mlp(dt, act, rows_variant):
 
 @pytest.mark.parametrize("W_,c1,c2,co,gn", [(48, 96, 32, 64, False), (48, 64, 0, 64, True), (96, 48, 16, 32, False),
                                             (96, 32, 0, 32, True)])
-@pytest.mark.parametrize("lds", [1, 0])
+@pytest.mark.parametrize("lds", [2, 1, 0])
 def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
-    """The decoder conv shapes (bf16), LDS-resident-input kernel and im2col kernel."""
+    """The decoder conv shapes (bf16): row-ring kernel (2), LDS-tile kernel (1), im2col (0)."""
     B, T = 2, 3
     S, H = B * T, W_
     x1 = rnd(S, H, W_, c1, seed=70) * 2
@@ -427,7 +427,7 @@ def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
         gref = ref.reshape(S, co // 16, 16, H * W_)
         close(m_, gref.mean((-1, -2)).reshape(-1), atol=2e-3, what="gn mean")
     finally:
-        L.load().catseg_set_conv_lds(1)
+        L.load().catseg_set_conv_lds(2)
 
 
 def test_convt64_gn():
