@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--classes", type=int, default=150)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
-    ap.add_argument("--cpu-images", type=int, default=2, help="oracle sample size for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-images", type=int, default=4, help="oracle sample size for cpu_baseline (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
     return ap.parse_args()
 
@@ -174,6 +174,20 @@ def main():
         dist.destroy_process_group()
 
 
+def pmc_traffic(family):
+    """HBM bytes per launch of `family` from the newest committed PMC summary
+    (profiles/<round>/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per the gfx950 note)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    if not files:
+        return None, None
+    fam = json.load(open(files[-1]))["families"].get(family)
+    if fam is None:
+        return None, None
+    return fam["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def roofline_pass(step, stream, dtype):
     """One eager pass with HIP events around every wrapped launch (on the launch stream)."""
     ops.PROFILE = []
@@ -192,18 +206,20 @@ def roofline_pass(step, stream, dtype):
     top = max(agg, key=lambda k: agg[k]["ms"])
     a = agg[top]
     avg_s = a["ms"] / a["launches"] / 1e3
+    traffic, tsrc = pmc_traffic(top)
     if a["flops"] > 0:
         achieved = a["flops"] / a["launches"] / avg_s / 1e12
         peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
         roof = {"bound": "mfma", "kernel": top, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2),
-                "flops_per_launch": a["flops"] // a["launches"]}
+                "flops_per_launch": a["flops"] // a["launches"],
+                "algorithmic_bytes_per_launch": a["bytes"] // a["launches"], "traffic_source": tsrc}
     else:
         achieved = a["bytes"] / a["launches"] / avg_s / 1e9
         roof = {"bound": "hbm", "kernel": top, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2)}
+                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2), "traffic_source": tsrc}
     kern = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                 "tflops": round(v["flops"] / (v["ms"] / 1e3) / 1e12, 2) if v["flops"] else None}
             for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])}

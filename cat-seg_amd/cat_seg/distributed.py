@@ -1,0 +1,84 @@
+"""Batch-sharded inference across the GPUs of one node.
+
+Images are independent, so the only exchange is one all-gather of the per-image
+logits.  This restates, for the MI355X path, what the reference gets from detectron2's
+eval loop: `InferenceSampler` hands every rank a contiguous slice of the dataset
+(detectron2 `data/samplers/distributed_sampler.py`, used via `build_detection_test_loader`
+in `train_net.py:124-149`), each rank runs `model(inputs)` on its slice, and results are
+combined with `comm.all_gather` (`plain_train_net.py:136-146`, over gloo there).
+
+Here the gather moves the pre-upsample logits (B, T, 96, 96) fp32 — 5.5 MB per image at
+T=150 — with one `all_gather_into_tensor` on the process group's backend: RCCL over
+xGMI on the GPU box (backend "nccl" is RCCL on ROCm), gloo in the CPU tests.  The
+gathered tensor is a pure copy of every rank's logits (bit-identical to running the
+same shard alone).  Ragged shards (global batch not divisible by the world size) are
+padded to the largest shard for the collective and trimmed afterwards.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_sizes(n: int, world: int) -> List[int]:
+    """InferenceSampler's split: the first n % world ranks take one extra item."""
+    base, left = divmod(n, world)
+    return [base + int(r < left) for r in range(world)]
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """[begin, end) of rank's contiguous slice of n items."""
+    sizes = shard_sizes(n, world)
+    begin = sum(sizes[:rank])
+    return begin, begin + sizes[rank]
+
+
+def _world(group) -> Tuple[int, int]:
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def gather_logits(local: torch.Tensor, n_total: int, group=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """All-gather per-rank logits (b_r, ...) into (n_total, ...) on every rank, rank order.
+
+    One collective of max(b_r) rows per rank; `out` may be preallocated (hipGraph-friendly
+    callers reuse it).  With world size 1 this is the identity."""
+    rank, world = _world(group)
+    if world == 1:
+        return local
+    sizes = shard_sizes(n_total, world)
+    if local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank}: local batch {local.shape[0]} != shard size {sizes[rank]}")
+    bmax = max(sizes)
+    rest = tuple(local.shape[1:])
+    if local.shape[0] != bmax:      # ragged: pad this rank's block to the common size
+        padded = local.new_zeros((bmax,) + rest)
+        padded[:local.shape[0]] = local
+        local = padded
+    buf = local.new_empty((world * bmax,) + rest)
+    dist.all_gather_into_tensor(buf, local.contiguous(), group=group)
+    if all(s == bmax for s in sizes):
+        if out is None:
+            return buf
+        out.copy_(buf)
+        return out
+    if out is None:
+        out = local.new_empty((n_total,) + rest)
+    o = 0
+    for r, s in enumerate(sizes):
+        out[o:o + s] = buf[r * bmax:r * bmax + s]
+        o += s
+    return out
+
+
+def run_sharded(forward: Callable[[Sequence], torch.Tensor], items: Sequence, group=None) -> torch.Tensor:
+    """Run `forward` on this rank's slice of `items` and all-gather the results.
+
+    `forward(slice) -> Tensor (len(slice), ...)`; every rank returns the full (len(items), ...)."""
+    rank, world = _world(group)
+    b, e = shard_range(len(items), rank, world)
+    local = forward(items[b:e])
+    return gather_logits(local, len(items), group=group)
