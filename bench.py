@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "cat-seg_amd"))
 sys.path.insert(0, ROOT)
 
 from cat_seg import ops  # noqa: E402
+from cat_seg.distributed import gather_logits  # noqa: E402
 from cat_seg.arch import VIT_L14_336  # noqa: E402
 from cat_seg.engine import CatSegEngine  # noqa: E402
 from cat_seg.weights import synthesize_state_dict  # noqa: E402
@@ -116,7 +117,7 @@ def main():
                     lg = step()
             if world > 1:
                 with torch.cuda.stream(stream):
-                    dist.all_gather_into_tensor(gathered, lg.contiguous())
+                    gather_logits(lg, world * B, out=gathered)     # RCCL all-gather over xGMI
             return lg
 
         for _ in range(args.warmup):

@@ -58,13 +58,11 @@ def gather_logits(local: torch.Tensor, n_total: int, group=None, out: Optional[t
         padded = local.new_zeros((bmax,) + rest)
         padded[:local.shape[0]] = local
         local = padded
-    buf = local.new_empty((world * bmax,) + rest)
+    even = all(s == bmax for s in sizes)
+    buf = out if (even and out is not None) else local.new_empty((world * bmax,) + rest)
     dist.all_gather_into_tensor(buf, local.contiguous(), group=group)
-    if all(s == bmax for s in sizes):
-        if out is None:
-            return buf
-        out.copy_(buf)
-        return out
+    if even:
+        return buf
     if out is None:
         out = local.new_empty((n_total,) + rest)
     o = 0

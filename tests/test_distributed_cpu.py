@@ -1,0 +1,96 @@
+"""Batch-sharded inference over world_size 2 with the gloo backend on CPU.
+
+Each rank computes the logits of its InferenceSampler slice (the oracle stands in for the
+per-rank forward: these tests check the shard/gather host logic, not the kernels) and
+`cat_seg.distributed` all-gathers them; the result must be a bit-exact copy of the
+per-shard logits, in rank order, on every rank — even and ragged global batches.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cat_seg import distributed as D
+
+
+def test_shard_sizes_match_inference_sampler():
+    # detectron2 InferenceSampler._get_local_indices: first n % world ranks get one more
+    assert D.shard_sizes(10, 4) == [3, 3, 2, 2]
+    assert D.shard_sizes(8, 8) == [1] * 8
+    assert D.shard_sizes(3, 4) == [1, 1, 1, 0]
+    ranges = [D.shard_range(11, r, 3) for r in range(3)]
+    assert ranges == [(0, 4), (4, 8), (8, 11)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tiny_setup():
+    from cat_seg.arch import TINY
+    from cat_seg.weights import synthesize_state_dict
+    arch = TINY
+    sd = synthesize_state_dict(arch, seed=0)
+    gen = torch.Generator().manual_seed(5)
+    text = torch.nn.functional.normalize(torch.randn(6, arch.embed_dim, generator=gen), dim=-1).unsqueeze(1)
+    imgs = [torch.rand(3, 384, 384, generator=gen) * 255 for _ in range(3)]
+    return arch, sd, text, imgs
+
+
+def _oracle_forward(arch, sd, text):
+    from oracle import catseg_oracle as O
+
+    def fwd(items):
+        if len(items) == 0:
+            return torch.empty(0, text.shape[0], 4 * arch.grid, 4 * arch.grid)
+        clip, _ = O.preprocess(arch, list(items))
+        return O.head_logits(arch, sd, clip, text)
+    return fwd
+
+
+def _worker(rank, world, port, n_items, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        arch, sd, text, imgs = _tiny_setup()
+        with torch.no_grad():
+            full = D.run_sharded(_oracle_forward(arch, sd, text), imgs[:n_items])
+        torch.save(full, os.path.join(out_dir, f"rank{rank}.pt"))
+        # a preallocated output (the hipGraph-friendly form) gives the same bytes
+        b, e = D.shard_range(n_items, rank, world)
+        local = full[b:e].clone()
+        out = torch.empty_like(full)
+        D.gather_logits(local, n_items, out=out)
+        assert torch.equal(out, full)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_items", [2, 3])     # even and ragged global batch
+def test_gloo_world2_gather_is_exact_copy(n_items):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), n_items, d), nprocs=world, join=True)
+        got = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    arch, sd, text, imgs = _tiny_setup()
+    fwd = _oracle_forward(arch, sd, text)
+    torch.set_num_threads(2)
+    with torch.no_grad():
+        want = torch.cat([fwd(imgs[slice(*D.shard_range(n_items, r, world))]) for r in range(world)])
+    assert want.shape[0] == n_items
+    for g in got:
+        assert torch.equal(g, want)
+
+
+def test_world1_is_identity():
+    x = torch.randn(3, 4)
+    assert D.gather_logits(x, 3) is x
