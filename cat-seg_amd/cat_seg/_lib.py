@@ -116,6 +116,11 @@ _SIGS = {
     "catseg_vit_embed": [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp],
     "catseg_bicubic_resize": [vp, i32, i32, vp, i32, vp],
     "catseg_postprocess": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
+    "catseg_resize_bilinear": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
+    "catseg_avgpool_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
+    "catseg_upsample_add_rows": [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp],
+    "catseg_sliding_crops": [vp, vp, i64, i32, i32, i32, i32, i32, vp, vp],
+    "catseg_sliding_merge": [vp, i64, i32, i32, i32, i32, i32, i32, vp, vp],
     "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
     "catseg_set_persistent": [i32],

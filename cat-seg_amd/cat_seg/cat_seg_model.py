@@ -152,7 +152,7 @@ class CATSeg(nn.Module):
         if self.training:
             raise NotImplementedError("CATSeg training is outside the MI355X inference path")
         if self.sliding_window:
-            raise NotImplementedError("TEST.SLIDING_WINDOW: not implemented on the MI355X path yet")
+            return self._forward_sliding(batched_inputs)
         with torch.no_grad():
             eng = self.engine
             self.sem_seg_head.predictor.get_text_embeds()
@@ -169,6 +169,20 @@ class CATSeg(nn.Module):
                 ops.postprocess(logits[i:i + 1], out, crop=(min(h_l, ih), min(w_l, iw)))
                 results.append({"sem_seg": out[0]})
             return results
+
+
+    def _forward_sliding(self, batched_inputs: List[dict]):
+        """TEST.SLIDING_WINDOW eval (cat_seg_model.py:156-176,204-218): every image (or image 0 in
+        the reference mode) through 4 Unfold tiles + 1 global crop; height/width default to 640."""
+        with torch.no_grad():
+            eng = self.engine
+            self.sem_seg_head.predictor.get_text_embeds()
+            n = len(batched_inputs) if self.return_all_images else 1
+            inputs = batched_inputs[:n]
+            raw, sizes_dev, _ = self._batch([x["image"] for x in inputs])
+            res = eng.SLIDE_OUT
+            out_hw = [(int(x.get("height", res)), int(x.get("width", res))) for x in inputs]
+            return [{"sem_seg": o} for o in eng.forward_sliding(raw, sizes_dev, out_hw)]
 
 
 def arch_from_cfg_defaults(clip_pretrained: str) -> CatSegArch:

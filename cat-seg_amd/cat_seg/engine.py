@@ -52,8 +52,6 @@ class CatSegEngine:
     def __init__(self, arch: CatSegArch, state_dict: Dict[str, torch.Tensor], dtype=torch.bfloat16,
                  device="cuda"):
         L.require_gpu()
-        if tuple(arch.pooling_size) != (1, 1):
-            raise NotImplementedError("HIP path: class-attention pooling != (1, 1) is not implemented yet")
         if arch.hidden_dim != 128 or arch.nheads != 4:
             raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
         self.arch = arch
@@ -378,6 +376,11 @@ class CatSegEngine:
             g = torch.empty(B * HW * k * k, a.decoder_guidance_proj_dims[i], device=dev, dtype=dt)
             ops.conv3x3(src, w.dgp[i][0], g, S=B, H=G * k, W=G * k, c1=cin, bias=w.dgp[i][1], act=L.ACT_RELU)
             GD.append(g)
+        # ---- class-attention pooling geometry (ClassTransformerLayer.pool, model.py:358,374-385) ----
+        H_, W_ = a.feature_resolution
+        ph, pw = a.pooling_size
+        pooled = (ph, pw) != (1, 1)
+        HWc = (H_ // ph) * (W_ // pw)          # pixels per class-attention slice
         # ---- text guidance terms per class (gathered per image after top-k) ----
         if classes is not None:
             tgqk = []
@@ -386,18 +389,21 @@ class CatSegEngine:
                 o = torch.empty(S, 2 * D, device=dev, dtype=dt)
                 ops.gather_rows(t, idx, o)
                 tgqk.append(o)
-            tmap = rowmap(d1=HW)
+            tmap = rowmap(d1=HWc)
         else:
             tgqk = tx.tgqk
-            tmap = rowmap(d1=HW, m1=T)
+            tmap = rowmap(d1=HWc, m1=T)
         # ---- aggregation layers (model.py:717-718) ----
         qkv = torch.empty(R, 3 * D, device=dev, dtype=dt)
         o = torch.empty(R, D, device=dev, dtype=dt)
         Y = torch.empty(R, D, device=dev, dtype=dt)
         gn = torch.empty(B * HW, D, device=dev, dtype=dt)
         gqk = torch.empty(B * HW, 2 * D, device=dev, dtype=dt)
+        if pooled:
+            Rp = S * HWc
+            Xp = torch.empty(Rp, D, device=dev, dtype=dt)
+            Yp = torch.empty(Rp, D, device=dev, dtype=dt)
         ws = a.window_size
-        H_, W_ = a.feature_resolution
         shift2 = ws // 2
         if min(H_, W_) <= ws:   # model.py:146-149
             ws, shift2 = min(H_, W_), 0
@@ -419,13 +425,26 @@ class CatSegEngine:
                 ops.rows_mlp(X, blk.wfc1, blk.bfc1, blk.wfc2, X, ln=(blk.n2w, blk.n2b), b2=blk.bfc2,
                              act=L.ACT_GELU, res=X)                              # x = x + Mlp(norm2(x))
             ca = lay.ca
-            ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
-                          add_ncols=2 * D)
-            ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
-                                 n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
-                                 k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
-            # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
-            ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y, res2=X)
+            if not pooled:
+                ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
+                              add_ncols=2 * D)
+                ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
+                                     n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                                     k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
+                ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y,
+                             res2=X)
+            else:
+                # x_pool = AvgPool(x); x_pool += attn; x_pool += MLP; x += interp_ac(x_pool) (model.py:387-423)
+                ops.avgpool_rows(X, Xp, S=S, H=H_, W=W_, C=D, pool=(ph, pw))
+                qkvp = qkv[:Rp]
+                ops.rows_gemm(Xp, ca.wqkv, qkvp, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
+                              add_ncols=2 * D)
+                ops.linear_attention(qkvp[:, :D], qkvp[:, D:2 * D], qkvp[:, 2 * D:], Xp, Yp, B=B, T=T, HW=HWc,
+                                     n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                                     k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                ops.rows_mlp(Yp, ca.w0, ca.b0, ca.w2, Yp, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Yp)
+                ops.upsample_add_rows(Yp, X, S=S, Hp=H_ // ph, Wp=W_ // pw, C=D, H=H_, W=W_)
         del qkv, o, Y, gn, gqk
         # ---- guided upsampler (model.py:674-681, 540-555) ----
         src, Hc, src_gn = X, G, None
@@ -483,3 +502,35 @@ class CatSegEngine:
         ih, iw = [int(v) for v in sizes[0].tolist()] if sizes.is_cpu else (h, w)
         ops.postprocess(logits, out, crop=(min(h, ih), min(w, iw)))
         return out
+
+    # ------------------------------------------------------------------ sliding-window eval
+    SLIDE_KERNEL, SLIDE_OVERLAP, SLIDE_OUT = 384, 0.333, 640      # cat_seg_model.py:158-160
+
+    def sliding_logits(self, raw: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+        """TEST.SLIDING_WINDOW branch up to the merged probabilities (cat_seg_model.py:156-176,204-213),
+        for every image of the batch: 640² resize, Unfold(384, stride 256) tiles + the 384² global
+        crop through the head, then sigmoid / Fold / average.  raw (N,3,Hc,Wc) fp32 0-255 canvas,
+        sizes (N,2) int32 valid (h, w).  Returns fp32 probabilities (N, T0, 640, 640)."""
+        k, res = self.SLIDE_KERNEL, self.SLIDE_OUT
+        stride = int(k * (1 - self.SLIDE_OVERLAP))
+        nb = (res - k) // stride + 1
+        N = raw.shape[0]
+        crops = torch.empty(N * (nb * nb + 1), 3, k, k, device=self.device, dtype=_f32)
+        ops.sliding_crops(raw, sizes, crops, out_res=res, kernel=k, stride=stride)
+        csz = torch.full((crops.shape[0], 2), k, dtype=torch.int32, device=self.device)
+        logits = self.head_logits(crops, csz)                      # (N*(nb²+1), T0, 96, 96)
+        merged = torch.empty(N, logits.shape[1], res, res, device=self.device, dtype=_f32)
+        ops.sliding_merge(logits, merged, kernel=k, stride=stride, out_res=res)
+        return merged
+
+    def forward_sliding(self, raw: torch.Tensor, sizes: torch.Tensor, out_hw) -> List[torch.Tensor]:
+        """Sliding-window probabilities resized to out_hw[n] = (height, width) per image
+        (sem_seg_postprocess of the 640² merge, cat_seg_model.py:215-217)."""
+        merged = self.sliding_logits(raw, sizes)
+        res = self.SLIDE_OUT
+        outs = []
+        for n, (H, W) in enumerate(out_hw):
+            o = torch.empty(1, merged.shape[1], H, W, device=self.device, dtype=_f32)
+            ops.resize_bilinear(merged[n:n + 1], o, crop=(res, res))
+            outs.append(o[0])
+        return outs

@@ -264,6 +264,51 @@ def postprocess(logits, out, *, crop=None):
     return out
 
 
+def resize_bilinear(x, out, *, crop=None):
+    """Bilinear (align_corners=False) of fp32 planes [B][T][h][w] cropped to `crop` -> out [B][T][H][W]."""
+    B, T, h, w = x.shape
+    H, W = out.shape[-2:]
+    ch, cw = crop if crop is not None else (h, w)
+    with _rec("resize_bilinear", 0, 4 * (B * T * (ch * cw + H * W))):
+        call("catseg_resize_bilinear", x.data_ptr(), B, T, h, w, ch, cw, out.data_ptr(), H, W, _stream())
+    return out
+
+
+def avgpool_rows(x, out, *, S, H, W, C, pool):
+    """nn.AvgPool2d(pool) over [S][H][W][C] rows -> out [S][H/ph][W/pw][C] (catseg_avgpool_rows)."""
+    ph, pw = pool
+    with _rec("avgpool_rows", 0, x.element_size() * S * C * (H * W + (H // ph) * (W // pw))):
+        call("catseg_avgpool_rows", x.data_ptr(), S, H, W, C, ph, pw, out.data_ptr(), _dt(x), _stream())
+    return out
+
+
+def upsample_add_rows(xp, x, *, S, Hp, Wp, C, H, W):
+    """x += bilinear_align_corners(xp -> H x W) on [S][.][.][C] rows (catseg_upsample_add_rows)."""
+    assert xp.dtype == x.dtype
+    with _rec("upsample_add_rows", 0, x.element_size() * S * C * (Hp * Wp + 2 * H * W)):
+        call("catseg_upsample_add_rows", xp.data_ptr(), S, Hp, Wp, C, x.data_ptr(), H, W, _dt(x), _stream())
+    return x
+
+
+def sliding_crops(raw, sizes, out, *, out_res, kernel, stride):
+    """Unfold crops + global crop of each image, fp32 0-255 (catseg_sliding_crops)."""
+    N, _, Hc, Wc = raw.shape
+    with _rec("sliding_crops", 0, 4 * out.numel()):
+        call("catseg_sliding_crops", raw.data_ptr(), sizes.data_ptr(), N, Hc, Wc, out_res, kernel, stride,
+             out.data_ptr(), _stream())
+    return out
+
+
+def sliding_merge(logits, out, *, kernel, stride, out_res):
+    """(Fold(sigmoid(interp tiles))/count + interp(global)) / 2 (catseg_sliding_merge)."""
+    N, T = out.shape[:2]
+    h, w = logits.shape[-2:]
+    with _rec("sliding_merge", 0, 4 * (logits.numel() + out.numel())):
+        call("catseg_sliding_merge", logits.data_ptr(), N, T, h, w, kernel, stride, out_res, out.data_ptr(),
+             _stream())
+    return out
+
+
 def token_embed(tokens, tok_emb, pos, out):
     n, ctx = tokens.shape
     call("catseg_token_embed", tokens.data_ptr(), n, ctx, tok_emb.data_ptr(), pos.data_ptr(), tok_emb.shape[1],

@@ -318,6 +318,7 @@ __global__ void bicubic_kernel(const float* in, int Si, int D, float* out, int S
 }
 
 // ---------------- postprocess: sigmoid + bilinear resize -----------------------------
+template <bool SIG>
 __global__ void post_kernel(const float* lg, int64_t planes, int h, int w, int ch, int cw, float* out, int H, int W) {
   const int64_t total = planes * (int64_t)H * W;
   const float sy = (float)ch / (float)H, sx = (float)cw / (float)W;
@@ -330,7 +331,10 @@ __global__ void post_kernel(const float* lg, int64_t planes, int h, int w, int c
     lin_idx(y, ch, sy, y0, y1, ly);
     lin_idx(x, cw, sx, x0, x1, lx);
     const float* src = lg + pl * (int64_t)h * w;
-    auto sg = [&](int yy, int xx) -> float { return 1.f / (1.f + expf(-src[yy * w + xx])); };
+    auto sg = [&](int yy, int xx) -> float {
+      const float v = src[yy * w + xx];
+      return SIG ? 1.f / (1.f + expf(-v)) : v;
+    };
     out[i] = (1.f - ly) * ((1.f - lx) * sg(y0, x0) + lx * sg(y0, x1)) + ly * ((1.f - lx) * sg(y1, x0) + lx * sg(y1, x1));
   }
 }
@@ -339,6 +343,7 @@ __global__ void post_kernel(const float* lg, int64_t planes, int h, int w, int c
 // ONCE into LDS (each source logit feeds ~(H/ch)^2 outputs), then every thread writes 4
 // consecutive outputs of a row (16-byte stores) from 4 LDS taps each.
 constexpr int POST_ROWS = 48;    // output rows per workgroup
+template <bool SIG>
 __global__ __launch_bounds__(256) void post_band_kernel(const float* lg, int h, int w, int ch, int cw, float* out,
                                                         int H, int W) {
   extern __shared__ float sgm[];           // sigmoid of the source rows this band reads [rows][cw]
@@ -353,7 +358,8 @@ __global__ __launch_bounds__(256) void post_band_kernel(const float* lg, int h, 
   const float* src = lg + pl * (int64_t)h * w;
   for (int i = threadIdx.x; i < nrows * cw; i += 256) {
     const int r = i / cw, c = i - r * cw;
-    sgm[i] = 1.f / (1.f + __expf(-src[(int64_t)(ya + r) * w + c]));
+    const float v = src[(int64_t)(ya + r) * w + c];
+    sgm[i] = SIG ? 1.f / (1.f + __expf(-v)) : v;
   }
   __syncthreads();
   const int W4 = W / 4;
@@ -502,22 +508,35 @@ extern "C" int catseg_bicubic_resize(const float* in, int S_in, int D, float* ou
   return catseg_launch_status("bicubic");
 }
 
-extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
-                                  float* out, int H, int W, void* stream) {
-  CATSEG_CHECK(logits && out && B > 0 && T > 0 && H > 0 && W > 0, "postprocess: bad args");
-  CATSEG_CHECK(crop_h > 0 && crop_h <= h && crop_w > 0 && crop_w <= w, "postprocess: bad crop");
+namespace {
+template <bool SIG>
+int launch_post(const char* what, const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                float* out, int H, int W, void* stream) {
+  CATSEG_CHECK(logits && out && B > 0 && T > 0 && H > 0 && W > 0, "postprocess/resize: bad args");
+  CATSEG_CHECK(crop_h > 0 && crop_h <= h && crop_w > 0 && crop_w <= w, "postprocess/resize: bad crop");
   const int64_t total = B * T * (int64_t)H * W;
   // banded kernel: source rows of one band (<= POST_ROWS * ch / H + 2) fit LDS
   const int64_t band_src_rows = (int64_t)POST_ROWS * crop_h / H + 3;
   if (W % 4 == 0 && band_src_rows * crop_w * 4 <= 64 * 1024) {
-    hipLaunchKernelGGL(post_band_kernel, dim3((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T)),
+    hipLaunchKernelGGL(post_band_kernel<SIG>, dim3((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T)),
                        dim3(256), (size_t)(band_src_rows * crop_w * 4), (hipStream_t)stream, logits, h, w, crop_h,
                        crop_w, out, H, W);
-    return catseg_launch_status("postprocess");
+    return catseg_launch_status(what);
   }
-  hipLaunchKernelGGL(post_kernel, dim3(grid_for(total, 65536)), dim3(256), 0, (hipStream_t)stream, logits, B * T, h, w,
-                     crop_h, crop_w, out, H, W);
-  return catseg_launch_status("postprocess");
+  hipLaunchKernelGGL(post_kernel<SIG>, dim3(grid_for(total, 65536)), dim3(256), 0, (hipStream_t)stream, logits,
+                     B * T, h, w, crop_h, crop_w, out, H, W);
+  return catseg_launch_status(what);
+}
+}  // namespace
+
+extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                                  float* out, int H, int W, void* stream) {
+  return launch_post<true>("postprocess", logits, B, T, h, w, crop_h, crop_w, out, H, W, stream);
+}
+
+extern "C" int catseg_resize_bilinear(const float* in, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                                      float* out, int H, int W, void* stream) {
+  return launch_post<false>("resize_bilinear", in, B, T, h, w, crop_h, crop_w, out, H, W, stream);
 }
 
 extern "C" int catseg_token_embed(const int32_t* tokens, int64_t n, int ctx, const float* tok_emb, const float* pos,

@@ -1,0 +1,224 @@
+// Resampling kernels around the aggregation and the sliding-window branch (HBM-bound,
+// 16-byte channel vectors, no reductions beyond a pooling window):
+//   catseg_avgpool_rows       ClassTransformerLayer.pool_features   (model.py:374-385)
+//   catseg_upsample_add_rows  x + interpolate(x_pool, align_corners=True) (model.py:415-423)
+//   catseg_sliding_crops      640² resize + Unfold(384, 256) + global 384² (cat_seg_model.py:158-168)
+//   catseg_sliding_merge      interp 384 + sigmoid + Fold/count + global avg (cat_seg_model.py:204-213)
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+inline unsigned grid_of(int64_t n, int64_t cap = 65536) {
+  int64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+
+// PyTorch bilinear source index, align_corners=False (area_pixel_compute_source_index)
+DEV void lin_src(int dst, int in_size, float scale, int& i0, int& i1, float& l1) {
+  float src = fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in_size - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+// align_corners=True: src = scale * dst, scale = (in - 1) / (out - 1)
+DEV void lin_src_ac(int dst, int in_size, float scale, int& i0, int& i1, float& l1) {
+  const float src = scale * (float)dst;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in_size - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+// PyTorch's blend order: h0l * (w0l * v00 + w1l * v01) + h1l * (w0l * v10 + w1l * v11)
+DEV float blend(float v00, float v01, float v10, float v11, float ly, float lx) {
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
+// ---------------- class-attention pooling (rows layout [S][H][W][C]) -----------------
+template <typename T>
+__global__ void avgpool_rows_kernel(const T* __restrict__ in, int64_t S, int H, int W, int C, int ph, int pw,
+                                    T* __restrict__ out) {
+  const int Hp = H / ph, Wp = W / pw, C4 = C / 4;
+  const int64_t total = S * Hp * Wp * C4;
+  const float inv = 1.f / (float)(ph * pw);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const int64_t p = i / C4;
+    const int x = (int)(p % Wp), y = (int)((p / Wp) % Hp);
+    const int64_t s = p / ((int64_t)Wp * Hp);
+    const T* src = in + ((s * H + (int64_t)y * ph) * W + (int64_t)x * pw) * C + c;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int dy = 0; dy < ph; ++dy)
+      for (int dx = 0; dx < pw; ++dx) {
+        float v[4];
+        load4<T>(src + ((int64_t)dy * W + dx) * C, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += v[r];
+      }
+    // avg_pool2d divides the window sum by the window size (no padding, count_include_pad moot)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = acc[r] * inv;
+    store4<T>(out + p * C + c, acc);
+  }
+}
+
+template <typename T>
+__global__ void upsample_add_rows_kernel(const T* __restrict__ xp, int64_t S, int Hp, int Wp, int C, T* __restrict__ x,
+                                         int H, int W) {
+  const int C4 = C / 4;
+  const int64_t total = S * H * W * C4;
+  const float sy = H > 1 ? (float)(Hp - 1) / (float)(H - 1) : 0.f;
+  const float sx = W > 1 ? (float)(Wp - 1) / (float)(W - 1) : 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const int64_t p = i / C4;
+    const int xx = (int)(p % W), yy = (int)((p / W) % H);
+    const int64_t s = p / ((int64_t)W * H);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    lin_src_ac(yy, Hp, sy, y0, y1, ly);
+    lin_src_ac(xx, Wp, sx, x0, x1, lx);
+    const T* base = xp + s * Hp * Wp * (int64_t)C + c;
+    float a[4], b[4], d[4], e[4], o[4];
+    load4<T>(base + ((int64_t)y0 * Wp + x0) * C, a);
+    load4<T>(base + ((int64_t)y0 * Wp + x1) * C, b);
+    load4<T>(base + ((int64_t)y1 * Wp + x0) * C, d);
+    load4<T>(base + ((int64_t)y1 * Wp + x1) * C, e);
+    T* dst = x + p * C + c;
+    load4<T>(dst, o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] += blend(a[r], b[r], d[r], e[r], ly, lx);
+    store4<T>(dst, o);
+  }
+}
+
+// ---------------- sliding window ---------------------------------------------------------
+// crops[n*(nb*nb+1) + l][c][y][x], k x k, unnormalised 0-255: l < nb*nb is the Unfold block
+// (bi, bj) = (l / nb, l % nb) of the out_res x out_res bilinear resize; the last is the
+// k x k bilinear resize of the whole image (the "global" crop).
+__global__ void sliding_crops_kernel(const float* __restrict__ raw, const int32_t* __restrict__ sizes, int64_t N,
+                                     int Hc, int Wc, int out_res, int k, int stride, int nb, float* __restrict__ crops) {
+  const int L = nb * nb + 1;
+  const int64_t total = N * L * 3 * (int64_t)k * k;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % k), y = (int)((i / k) % k);
+    const int c = (int)((i / ((int64_t)k * k)) % 3);
+    const int64_t nl = i / (3 * (int64_t)k * k);
+    const int l = (int)(nl % L);
+    const int64_t n = nl / L;
+    const int h = sizes[2 * n], w = sizes[2 * n + 1];
+    int Y = y, X = x, R = k;
+    if (l < L - 1) {
+      Y = y + stride * (l / nb);
+      X = x + stride * (l % nb);
+      R = out_res;
+    }
+    int y0, y1, x0, x1;
+    float ly, lx;
+    lin_src(Y, h, (float)h / (float)R, y0, y1, ly);
+    lin_src(X, w, (float)w / (float)R, x0, x1, lx);
+    const float* src = raw + (n * 3 + c) * (int64_t)Hc * Wc;
+    crops[i] = blend(src[(int64_t)y0 * Wc + x0], src[(int64_t)y0 * Wc + x1], src[(int64_t)y1 * Wc + x0],
+                     src[(int64_t)y1 * Wc + x1], ly, lx);
+  }
+}
+
+DEV float sigm(float v) { return 1.f / (1.f + expf(-v)); }
+
+// sigmoid(bilinear(plane h x w -> k x k))(y, x)
+DEV float up_sig(const float* __restrict__ pl, int h, int w, int k, int y, int x) {
+  int y0, y1, x0, x1;
+  float ly, lx;
+  lin_src(y, h, (float)h / (float)k, y0, y1, ly);
+  lin_src(x, w, (float)w / (float)k, x0, x1, lx);
+  return sigm(blend(pl[y0 * w + x0], pl[y0 * w + x1], pl[y1 * w + x0], pl[y1 * w + x1], ly, lx));
+}
+
+// out[n][t][Y][X] (out_res²) = (Fold(tiles)/count + bilinear(global -> out_res)) / 2
+__global__ void sliding_merge_kernel(const float* __restrict__ lg, int64_t N, int T, int h, int w, int k, int stride,
+                                     int nb, int out_res, float* __restrict__ out) {
+  const int L = nb * nb + 1;
+  const int64_t total = N * T * (int64_t)out_res * out_res;
+  const float sg = (float)k / (float)out_res;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int X = (int)(i % out_res), Y = (int)((i / out_res) % out_res);
+    const int64_t nt = i / ((int64_t)out_res * out_res);
+    const int t = (int)(nt % T);
+    const int64_t n = nt / T;
+    const int64_t plane = (int64_t)h * w;
+    // global crop: sigmoid(interp 96 -> k), then interp k -> out_res
+    const float* gp = lg + ((n * L + L - 1) * T + t) * plane;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    lin_src(Y, k, sg, y0, y1, ly);
+    lin_src(X, k, sg, x0, x1, lx);
+    const float glob = blend(up_sig(gp, h, w, k, y0, x0), up_sig(gp, h, w, k, y0, x1), up_sig(gp, h, w, k, y1, x0),
+                             up_sig(gp, h, w, k, y1, x1), ly, lx);
+    float sum = 0.f, cnt = 0.f;
+    for (int bi = 0; bi < nb; ++bi) {
+      const int yy = Y - stride * bi;
+      if (yy < 0 || yy >= k) continue;
+      for (int bj = 0; bj < nb; ++bj) {
+        const int xx = X - stride * bj;
+        if (xx < 0 || xx >= k) continue;
+        sum += up_sig(lg + ((n * L + bi * nb + bj) * T + t) * plane, h, w, k, yy, xx);
+        cnt += 1.f;
+      }
+    }
+    out[i] = (sum / cnt + glob) / 2.f;
+  }
+}
+
+}  // namespace
+
+extern "C" int catseg_avgpool_rows(const void* in, int64_t S, int H, int W, int C, int ph, int pw, void* out,
+                                   int dtype, void* stream) {
+  CATSEG_CHECK(in && out && S > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0, "avgpool_rows: bad args");
+  CATSEG_CHECK(ph > 0 && pw > 0 && H >= ph && W >= pw, "avgpool_rows: bad pooling window");
+  const int64_t total = S * (H / ph) * (W / pw) * (C / 4);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(avgpool_rows_kernel<bf16>, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)in, S, H, W, C, ph, pw, (bf16*)out);
+  else
+    hipLaunchKernelGGL(avgpool_rows_kernel<float>, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)in, S, H, W, C, ph, pw, (float*)out);
+  return catseg_launch_status("avgpool_rows");
+}
+
+extern "C" int catseg_upsample_add_rows(const void* xp, int64_t S, int Hp, int Wp, int C, void* x, int H, int W,
+                                        int dtype, void* stream) {
+  CATSEG_CHECK(xp && x && S > 0 && Hp > 0 && Wp > 0 && H > 0 && W > 0, "upsample_add_rows: bad args");
+  CATSEG_CHECK(C > 0 && C % 4 == 0, "upsample_add_rows: C must be a multiple of 4");
+  const int64_t total = S * H * W * (C / 4);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(upsample_add_rows_kernel<bf16>, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)xp, S, Hp, Wp, C, (bf16*)x, H, W);
+  else
+    hipLaunchKernelGGL(upsample_add_rows_kernel<float>, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)xp, S, Hp, Wp, C, (float*)x, H, W);
+  return catseg_launch_status("upsample_add_rows");
+}
+
+extern "C" int catseg_sliding_crops(const float* raw, const int32_t* sizes, int64_t N, int Hc, int Wc, int out_res,
+                                    int kernel, int stride, float* crops, void* stream) {
+  CATSEG_CHECK(raw && sizes && crops && N > 0 && Hc > 0 && Wc > 0, "sliding_crops: bad args");
+  CATSEG_CHECK(kernel > 0 && stride > 0 && out_res >= kernel, "sliding_crops: bad window geometry");
+  const int nb = (out_res - kernel) / stride + 1;
+  const int64_t total = N * (nb * nb + 1) * 3 * (int64_t)kernel * kernel;
+  hipLaunchKernelGGL(sliding_crops_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, raw, sizes, N, Hc,
+                     Wc, out_res, kernel, stride, nb, crops);
+  return catseg_launch_status("sliding_crops");
+}
+
+extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h, int w, int kernel, int stride,
+                                    int out_res, float* out, void* stream) {
+  CATSEG_CHECK(logits && out && N > 0 && T > 0 && h > 0 && w > 0, "sliding_merge: bad args");
+  CATSEG_CHECK(kernel > 0 && stride > 0 && out_res >= kernel, "sliding_merge: bad window geometry");
+  // every output pixel must be covered by at least one tile (Fold count > 0)
+  const int nb = (out_res - kernel) / stride + 1;
+  CATSEG_CHECK(stride * (nb - 1) + kernel == out_res && stride <= kernel, "sliding_merge: tiles must cover out_res");
+  const int64_t total = N * T * (int64_t)out_res * out_res;
+  hipLaunchKernelGGL(sliding_merge_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, logits, N, T, h, w,
+                     kernel, stride, nb, out_res, out);
+  return catseg_launch_status("sliding_merge");
+}

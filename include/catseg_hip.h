@@ -280,6 +280,39 @@ int catseg_bicubic_resize(const float* in, int S_in, int D, float* out, int S_ou
  * (cat_seg_model.py:222-227 + detectron2 sem_seg_postprocess). */
 int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
                        float* out, int H, int W, void* stream);
+/* catseg_resize_bilinear — catseg_postprocess without the sigmoid: the final
+ * sem_seg_postprocess of the sliding branch (cat_seg_model.py:215-217). */
+int catseg_resize_bilinear(const float* in, int64_t B, int T, int h, int w, int crop_h, int crop_w,
+                           float* out, int H, int W, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Class-attention pooling (POOLING_SIZES != [1,1]; ClassTransformerLayer,
+ * model.py:374-423) on the rows layout [S][H][W][C] (S = B*T slices).
+ * ------------------------------------------------------------------------- */
+/* catseg_avgpool_rows — nn.AvgPool2d(ph, pw) (stride = kernel, no padding) per slice:
+ * [S][H][W][C] -> [S][H/ph][W/pw][C]  (pool_features, model.py:374-385). */
+int catseg_avgpool_rows(const void* in, int64_t S, int H, int W, int C, int ph, int pw, void* out,
+                        int dtype, void* stream);
+/* catseg_upsample_add_rows — x[S][H][W][C] += bilinear(xp[S][Hp][Wp][C] -> H x W,
+ * align_corners=True)  (model.py:415-423: interpolate, crop padding, x + x_pool). */
+int catseg_upsample_add_rows(const void* xp, int64_t S, int Hp, int Wp, int C, void* x, int H, int W,
+                             int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Sliding-window inference (TEST.SLIDING_WINDOW, cat_seg_model.py:156-176,204-218).
+ * ------------------------------------------------------------------------- */
+/* catseg_sliding_crops — per image n of a zero-padded fp32 canvas raw[N][3][Hc][Wc] with
+ * valid sizes[n] = (h, w): bilinear resize to out_res², nn.Unfold(kernel, stride) into
+ * nb² crops (nb = (out_res - kernel) / stride + 1, row-major blocks), plus the bilinear
+ * kernel² resize of the whole image:  crops[N*(nb²+1)][3][kernel][kernel], 0-255
+ * (normalisation and the CLIP-resolution resize follow in catseg_preprocess_im2col). */
+int catseg_sliding_crops(const float* raw, const int32_t* sizes, int64_t N, int Hc, int Wc, int out_res,
+                         int kernel, int stride, float* crops, void* stream);
+/* catseg_sliding_merge — logits[N*(nb²+1)][T][h][w] -> out[N][T][out_res][out_res]:
+ * interpolate each crop to kernel² + sigmoid; Fold(tiles) / Fold(Unfold(ones));
+ * average with the global crop interpolated to out_res²  (cat_seg_model.py:204-213). */
+int catseg_sliding_merge(const float* logits, int64_t N, int T, int h, int w, int kernel, int stride,
+                         int out_res, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Text side (CLIP.encode_text, model_vpt.py:421-438)

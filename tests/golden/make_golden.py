@@ -231,7 +231,52 @@ def e2e_case(name, arch, T, shapes, seed, pad_len=256, tokens=None, sub=1):
     save(name, **kw)
 
 
+def glue_sliding(arch, clip, agg, up1, up2, image, text, height, width):
+    """TEST.SLIDING_WINDOW eval branch (cat_seg_model.py:156-176,204-218), restated with the
+    same torch ops (nn.Unfold / nn.Fold, bilinear align_corners=False) around ref_head."""
+    kernel, overlap, out_res = 384, 0.333, [640, 640]
+    stride = int(kernel * (1 - overlap))
+    unfold = nn.Unfold(kernel_size=kernel, stride=stride)
+    fold = nn.Fold(out_res, kernel_size=kernel, stride=stride)
+    img = image.float()
+    x = F.interpolate(img.unsqueeze(0), size=out_res, mode="bilinear", align_corners=False).squeeze()
+    L = unfold(x).shape[-1]
+    x = unfold(x).reshape(3, kernel, kernel, L).permute(3, 0, 1, 2)          # "(C H W) L -> L C H W"
+    g = F.interpolate(img.unsqueeze(0), size=(kernel, kernel), mode="bilinear", align_corners=False)
+    x = torch.cat((x, g), dim=0)
+    mean = torch.tensor(arch.clip_pixel_mean).view(-1, 1, 1)
+    std = torch.tensor(arch.clip_pixel_std).view(-1, 1, 1)
+    R = arch.clip_resolution
+    clip_images = F.interpolate((x - mean) / std, size=(R, R), mode="bilinear", align_corners=False)
+    out = ref_head(arch, clip, agg, up1, up2, clip_images, text)
+    out = F.interpolate(out, size=kernel, mode="bilinear", align_corners=False).sigmoid()
+    glob = F.interpolate(out[-1:], size=out_res, mode="bilinear", align_corners=False)
+    out = out[:-1]
+    out = fold(out.flatten(1).T) / fold(unfold(torch.ones([1] + out_res)))
+    out = (out + glob) / 2.0
+    r = out[0][:, : out_res[0], : out_res[1]].unsqueeze(0)                 # sem_seg_postprocess
+    return F.interpolate(r, size=(height, width), mode="bilinear", align_corners=False)[0]
+
+
+def sliding_case(name, arch, T, shape, seed, pad_len, height, width, sub=4):
+    sd = synthesize_state_dict(arch, seed=0)
+    clip, agg, up1, up2 = build_reference(arch, sd, pad_len=pad_len)
+    tokens = rand_tokens(seed, T, arch.context_length, arch.vocab_size)
+    text = ref_text(clip, tokens)
+    img = rand_images(seed, [shape])[0]
+    with torch.no_grad():
+        out = glue_sliding(arch, clip, agg, up1, up2, img, text, height, width)
+    save(name, tokens=tokens, text=text, image0=img, height=height, width=width, pad_len=pad_len, sub=sub,
+         sem_seg_sub=out[:, ::sub, ::sub], sem_seg_sum=out.double().sum())
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "sliding":
+        torch.set_num_threads(8)
+        # TEST.SLIDING_WINDOW: tiny arch, T=20 > pad_len=16 (per-crop top-k), ragged 440x360 image,
+        # output resized to 480x400 (non-default height/width)
+        sliding_case("e2e_tiny_sliding", TINY, 20, (440, 360), seed=6, pad_len=16, height=480, width=400)
+        return
     torch.manual_seed(0)
     torch.set_num_threads(8)
     tok = tok_mod.SimpleTokenizer()

@@ -48,3 +48,22 @@ def test_catseg_height_width_and_reference_mode():
     im = torch.from_numpy(g["image0"]).float().cuda()
     out = model([{"image": im, "height": 200, "width": 300}, {"image": im}])
     assert len(out) == 1 and out[0]["sem_seg"].shape == (20, 200, 300)
+
+
+def test_catseg_sliding_window_matches_golden():
+    """cfg TEST.SLIDING_WINDOW True through build_model -> CATSeg.forward (cat_seg_model.py:156-218)."""
+    g = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_sliding.npz")))
+    cfg = tiny_cfg(**{"TEST.SLIDING_WINDOW": "True"})
+    model = build_model(cfg).cuda().eval()
+    model.sem_seg_head.predictor.set_class_tokens(g["tokens"])
+    model.arch = model.arch.replace(pad_len=int(g["pad_len"]))
+    model._engine = None
+    H, W = int(g["height"]), int(g["width"])
+    out = model([{"image": torch.from_numpy(g["image0"]), "height": H, "width": W}])
+    assert len(out) == 1 and out[0]["sem_seg"].shape == (g["tokens"].shape[0], H, W)
+    sub = int(g["sub"])
+    err = (out[0]["sem_seg"][:, ::sub, ::sub].cpu() - torch.from_numpy(g["sem_seg_sub"])).abs().max().item()
+    assert err < 1e-3, err
+    # height/width default to the 640² merge resolution (cat_seg_model.py:215-216)
+    out = model([{"image": torch.from_numpy(g["image0"])}])
+    assert out[0]["sem_seg"].shape[-2:] == (640, 640)

@@ -32,11 +32,16 @@ def batch_raw(imgs, div=32):
 
 
 # fp32 gate: 1e-3 (BASELINE.md parity gates); bf16 gate: max-abs 5e-2, mean-abs 5e-3
-@pytest.mark.parametrize("name", ["e2e_tiny_pad", "e2e_tiny_eval", "e2e_tiny_topk"])
+CASES = {"e2e_tiny_pad": TINY, "e2e_tiny_eval": TINY, "e2e_tiny_topk": TINY,
+         "e2e_tiny_topk_pool": TINY.replace(pooling_size=(2, 2)),          # POOLING [2,2] + top-k
+         "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2))}            # config 1 (yaml default pooling)
+
+
+@pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_engine_vs_reference_golden(name, dtype):
     g = load(name)
-    arch = TINY.replace(pad_len=int(g["pad_len"]))
+    arch = CASES[name].replace(pad_len=int(g["pad_len"]))
     sd = synthesize_state_dict(arch, seed=0)
     eng = CatSegEngine(arch, sd, dtype=dtype)
     text = eng.encode_text(torch.from_numpy(g["tokens"]).int())
@@ -46,6 +51,9 @@ def test_engine_vs_reference_golden(name, dtype):
     imgs = [torch.from_numpy(g[k]).float() for k in sorted(k for k in g if k.startswith("image"))]
     raw, sizes = batch_raw(imgs)
     logits = eng.head_logits(raw, sizes).cpu()
+    sub = int(g["sub"])
+    if sub > 1:
+        logits = logits[:, :, ::sub, ::sub]
     ref = torch.from_numpy(g["logits"])
     err = (logits - ref).abs()
     if dtype == torch.float32:
@@ -78,3 +86,22 @@ def test_engine_b16_config2_vs_oracle(dtype):
         assert err.max().item() < 1e-3
     else:
         assert err.max().item() < 5e-2 and err.mean().item() < 5e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_engine_sliding_vs_reference_golden(dtype):
+    """TEST.SLIDING_WINDOW (cat_seg_model.py:156-176,204-218): 4 Unfold tiles + global crop,
+    per-crop top-k, Fold/count merge, resize to a non-default height/width."""
+    g = load("e2e_tiny_sliding")
+    arch = TINY.replace(pad_len=int(g["pad_len"]))
+    eng = CatSegEngine(arch, synthesize_state_dict(arch, seed=0), dtype=dtype)
+    eng.set_text(torch.from_numpy(g["text"]).cuda())
+    raw, sizes = batch_raw([torch.from_numpy(g["image0"]).float()])
+    H, W = int(g["height"]), int(g["width"])
+    out = eng.forward_sliding(raw, sizes, [(H, W)])[0].cpu()
+    assert out.shape == (g["text"].shape[0], H, W)
+    sub = int(g["sub"])
+    err = (out[:, ::sub, ::sub] - torch.from_numpy(g["sem_seg_sub"])).abs()
+    # probabilities: fp32 gate 1e-3; bf16 gate as the boundary's sigmoid-space gate
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    assert err.max().item() < tol, err.max().item()

@@ -462,3 +462,61 @@ def test_text_helpers():
     e = torch.empty(n, Wd, device=dev)
     ops.eot_gather(x, tok.to(dev), e)
     close(e, ref[torch.arange(n), tok.long().argmax(-1)], atol=1e-6, what="eot")
+
+
+# ----------------------------------------------------------------------------- pooling / sliding
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("pool", [(2, 2), (3, 2), (4, 4)])
+def test_avgpool_and_upsample_add_rows(dt, pool):
+    """ClassTransformerLayer pool_features + interpolate(align_corners=True) + residual
+    (model.py:374-385,415-423) on the rows layout, vs torch on the reference layout."""
+    S, H, W, C = 5, 24, 24, 128
+    ph, pw = pool
+    x = rnd(S, H, W, C, seed=31).to(dt)
+    xp = torch.empty(S * (H // ph) * (W // pw), C, device=dev, dtype=dt)
+    ops.avgpool_rows(x.to(dev).reshape(-1, C), xp, S=S, H=H, W=W, C=C, pool=pool)
+    ref_p = F.avg_pool2d(x.float().permute(0, 3, 1, 2), pool)                    # (S, C, Hp, Wp)
+    close(xp.reshape(S, H // ph, W // pw, C).permute(0, 3, 1, 2), ref_p,
+          atol=1e-6 if dt == torch.float32 else 1e-2, what="avgpool")
+    y = rnd(S, H // ph, W // pw, C, seed=32).to(dt)
+    xd = x.to(dev).reshape(-1, C).clone()
+    ops.upsample_add_rows(y.to(dev).reshape(-1, C), xd, S=S, Hp=H // ph, Wp=W // pw, C=C, H=H, W=W)
+    up = F.interpolate(y.float().permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=True)
+    ref = x.float() + up.permute(0, 2, 3, 1)
+    close(xd.reshape(S, H, W, C), ref, atol=1e-5 if dt == torch.float32 else 2e-2, what="upsample_add")
+
+
+def test_sliding_crops_and_merge_vs_oracle_ops():
+    """catseg_sliding_crops / catseg_sliding_merge / catseg_resize_bilinear vs the reference's
+    Unfold / Fold / interpolate sequence (cat_seg_model.py:158-168,204-217)."""
+    k, stride, res = 384, 256, 640
+    unfold = torch.nn.Unfold(kernel_size=k, stride=stride)
+    fold = torch.nn.Fold([res, res], kernel_size=k, stride=stride)
+    shapes = [(440, 360), (512, 640)]
+    imgs = [rnd(3, h, w, seed=40 + i, scale=127.5) + 127.5 for i, (h, w) in enumerate(shapes)]
+    Hc, Wc = 512, 640
+    raw = torch.zeros(2, 3, Hc, Wc)
+    for i, im in enumerate(imgs):
+        raw[i, :, :im.shape[1], :im.shape[2]] = im
+    sizes = torch.tensor(shapes, dtype=torch.int32)
+    crops = torch.empty(2 * 5, 3, k, k, device=dev)
+    ops.sliding_crops(raw.to(dev), sizes.to(dev), crops, out_res=res, kernel=k, stride=stride)
+    for i, im in enumerate(imgs):
+        x = F.interpolate(im.unsqueeze(0), size=[res, res], mode="bilinear", align_corners=False).squeeze()
+        x = unfold(x).reshape(3, k, k, -1).permute(3, 0, 1, 2)
+        gl = F.interpolate(im.unsqueeze(0), size=(k, k), mode="bilinear", align_corners=False)
+        ref = torch.cat((x, gl), 0)
+        close(crops[5 * i:5 * i + 5], ref, atol=2e-3, what=f"crops {i}")
+    T = 7
+    lg = rnd(2 * 5, T, 96, 96, seed=44, scale=4.0)
+    merged = torch.empty(2, T, res, res, device=dev)
+    ops.sliding_merge(lg.to(dev), merged, kernel=k, stride=stride, out_res=res)
+    for i in range(2):
+        o = F.interpolate(lg[5 * i:5 * i + 5], size=k, mode="bilinear", align_corners=False).sigmoid()
+        glob = F.interpolate(o[-1:], size=[res, res], mode="bilinear", align_corners=False)
+        t = fold(o[:-1].flatten(1).T) / fold(unfold(torch.ones([1, res, res])))
+        close(merged[i], ((t + glob) / 2.0)[0], atol=1e-5, what=f"merge {i}")
+    out = torch.empty(1, T, 480, 400, device=dev)
+    ops.resize_bilinear(merged[:1], out, crop=(res, res))
+    ref = F.interpolate(merged[:1].cpu(), size=(480, 400), mode="bilinear", align_corners=False)
+    close(out, ref, atol=1e-6, what="resize")

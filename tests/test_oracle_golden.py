@@ -45,3 +45,20 @@ def test_oracle_matches_reference_golden(name):
     assert abs(logits.double().sum().item() - float(g["logits_sum"])) < 1e-2
     out = O.catseg_forward(arch, sd, [{"image": i} for i in imgs], torch.from_numpy(g["text"]))
     np.testing.assert_allclose(out[0]["sem_seg"][:, ::8, ::8].numpy(), g["sem_seg0_sub"], atol=1e-5, rtol=0)
+
+
+def test_oracle_sliding_matches_reference_golden():
+    """TEST.SLIDING_WINDOW branch (cat_seg_model.py:156-176,204-218): per-crop top-k, Fold/count,
+    global average, non-default height/width."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = load("e2e_tiny_sliding")
+    arch = TINY.replace(pad_len=int(g["pad_len"]))
+    sd = synthesize_state_dict(arch, seed=0)
+    text = O.text_embeds(arch, sd, torch.from_numpy(g["tokens"]).long())
+    np.testing.assert_allclose(text.numpy(), g["text"], atol=2e-6, rtol=0)
+    inp = [{"image": torch.from_numpy(g["image0"]), "height": int(g["height"]), "width": int(g["width"])}]
+    out = O.catseg_forward_sliding(arch, sd, inp, torch.from_numpy(g["text"]))[0]["sem_seg"]
+    sub = int(g["sub"])
+    assert out.shape == (g["text"].shape[0], int(g["height"]), int(g["width"]))
+    np.testing.assert_allclose(out[:, ::sub, ::sub].numpy(), g["sem_seg_sub"], atol=1e-5, rtol=0)
+    assert abs(out.double().sum().item() - float(g["sem_seg_sum"])) < 1e-2
