@@ -30,6 +30,19 @@ def rowmap(d1=1, m1=BIG, s1=1, d2=1, m2=1, s2=0, off=0) -> RowMap:
 IDENTITY = rowmap()
 
 
+class SwinAttnArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ld_x", i64),
+        ("ln_g", vp), ("ln_b", vp), ("eps", f32),
+        ("w_qkv", vp), ("b_qkv", vp),
+        ("gqk", vp), ("ld_g", i64), ("gmap", RowMap),
+        ("out", vp), ("ld_out", i64),
+        ("S", i64), ("img_h", i32), ("img_w", i32), ("window", i32), ("shift", i32), ("n_heads", i32),
+        ("head_dim", i32), ("scale", f32),
+        ("dtype", i32),
+    ]
+
+
 class GemmArgs(C.Structure):
     _fields_ = [
         ("A", vp), ("lda", i64), ("amap", RowMap),
@@ -116,6 +129,7 @@ _SIGS = {
     "catseg_vit_embed": [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp],
     "catseg_bicubic_resize": [vp, i32, i32, vp, i32, vp],
     "catseg_postprocess": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
+    "catseg_swin_window_attention": [C.POINTER(SwinAttnArgs), vp],
     "catseg_resize_bilinear": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
     "catseg_avgpool_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
     "catseg_upsample_add_rows": [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp],

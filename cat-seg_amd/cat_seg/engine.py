@@ -56,6 +56,7 @@ class CatSegEngine:
             raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
         self.arch = arch
         self.dt = dtype
+        self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.device = torch.device(device)
         self._text = None
         with torch.no_grad():
@@ -408,6 +409,9 @@ class CatSegEngine:
         if min(H_, W_) <= ws:   # model.py:146-149
             ws, shift2 = min(H_, W_), 0
         nwin = (H_ // ws) * (W_ // ws)
+        # the fused window kernel covers CAT-Seg's geometry (24x24 map, 12x12 windows, 4 x 32 heads)
+        fused_swin = (self.fused_swin and dt == torch.bfloat16 and (H_, W_, ws) == (24, 24, 12)
+                      and a.nheads == 4 and D == 128)
         gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)     # (b, t, p) -> (b, p)
         n_pad = a.pad_len - T if a.pad_len > 0 and T < a.pad_len else 0
         for l, lay in enumerate(w.layers):
@@ -415,12 +419,18 @@ class CatSegEngine:
             for name, shift in (("block_1", 0), ("block_2", shift2)):
                 blk = lay[name]
                 ops.gemm(gn, blk.wqk_g, gqk)                   # W_g . LN(g): per image
-                # LN1 + [q|k|v] projection + guidance half, one pass over X
-                ops.rows_gemm(X, blk.wqkv, qkv, ln=(blk.n1w, blk.n1b), bias=blk.bqkv, add=gqk, addmap=gmap,
-                              add_ncols=2 * D)
-                ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, n_seq=S * nwin, seq_len=ws * ws,
-                              n_heads=a.nheads, head_dim=D // a.nheads, scale=(D // a.nheads) ** -0.5, mode=1,
-                              img_hw=(H_, W_), window=ws, shift=shift)
+                if fused_swin:
+                    # norm1 + q/k/v (+ guidance half) + window attention in one kernel per window
+                    ops.swin_window_attention(X, (blk.n1w, blk.n1b), blk.wqkv, blk.bqkv, gqk, gmap, o, S=S,
+                                              img_hw=(H_, W_), window=ws, shift=shift, n_heads=a.nheads,
+                                              head_dim=D // a.nheads, scale=(D // a.nheads) ** -0.5)
+                else:
+                    # LN1 + [q|k|v] projection + guidance half, one pass over X
+                    ops.rows_gemm(X, blk.wqkv, qkv, ln=(blk.n1w, blk.n1b), bias=blk.bqkv, add=gqk, addmap=gmap,
+                                  add_ncols=2 * D)
+                    ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, n_seq=S * nwin,
+                                  seq_len=ws * ws, n_heads=a.nheads, head_dim=D // a.nheads,
+                                  scale=(D // a.nheads) ** -0.5, mode=1, img_hw=(H_, W_), window=ws, shift=shift)
                 ops.rows_gemm(o, blk.wproj, X, bias=blk.bproj, res=X)          # x = shortcut + proj(attn)
                 ops.rows_mlp(X, blk.wfc1, blk.bfc1, blk.wfc2, X, ln=(blk.n2w, blk.n2b), b2=blk.bfc2,
                              act=L.ACT_GELU, res=X)                              # x = x + Mlp(norm2(x))

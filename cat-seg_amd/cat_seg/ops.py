@@ -149,6 +149,26 @@ def attention(q, k, v, out, *, n_seq, seq_len, n_heads, head_dim, scale, causal=
     return out
 
 
+def swin_window_attention(x, ln, w_qkv, b_qkv, gqk, gmap, out, *, S, img_hw, window, shift, n_heads, head_dim,
+                          scale, eps=1e-5):
+    """Fused norm1 + q/k/v (+ guidance half) + shifted-window attention (catseg_swin_window_attention)."""
+    a = L.SwinAttnArgs()
+    a.x, a.ld_x = x.data_ptr(), _ld(x)
+    a.ln_g, a.ln_b, a.eps = ln[0].data_ptr(), ln[1].data_ptr(), eps
+    a.w_qkv, a.b_qkv = w_qkv.data_ptr(), b_qkv.data_ptr()
+    a.gqk, a.ld_g, a.gmap = gqk.data_ptr(), _ld(gqk), gmap
+    a.out, a.ld_out = out.data_ptr(), _ld(out)
+    a.S, a.img_h, a.img_w, a.window, a.shift = S, img_hw[0], img_hw[1], window, shift
+    a.n_heads, a.head_dim, a.scale, a.dtype = n_heads, head_dim, scale, _dt(x)
+    R = S * img_hw[0] * img_hw[1]
+    C = n_heads * head_dim
+    L_ = window * window
+    flops = 2 * R * C * 3 * C + 4 * R * L_ * C
+    with _rec("swin_window_attention", flops, x.element_size() * R * 2 * C):
+        call("catseg_swin_window_attention", a, _stream())
+    return out
+
+
 def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_pad=None, v_pad=None, eps=1e-6):
     a = L.LinAttnArgs()
     a.q, a.k, a.v, a.ld_qkv = q.data_ptr(), k.data_ptr(), v.data_ptr(), _ld(q)

@@ -1,0 +1,244 @@
+// Fused Swin window attention for the CAT-Seg spatial aggregation (bf16):
+//   LayerNorm(norm1) + [q|k|v] projection (+ the per-image guidance half of q, k)
+//   + shifted-window multi-head attention, one workgroup per (slice, window).
+// Reference: SwinTransformerBlock.forward model.py:191-199 (norm1, concat guidance,
+// roll, window_partition) and WindowAttention.forward model.py:86-114 up to (and not
+// including) the output projection; the -100 region mask of model.py:161-183.
+//
+// The 144 x 384 q/k/v of a window never leave the CU: per head, the 144 x 96 slice is
+// produced by MFMA from the LayerNorm'd window rows held in registers, written to LDS in the
+// layouts the attention loop reads (K [key][d (+ region one-hot)], V^T [d][key],
+// Q [query][d]), and consumed at once.  HBM traffic per window: the 144 input rows,
+// the 144 output rows, the guidance rows (shared by every class of an image: L2/MALL).
+//
+// 9 waves; wave w owns rows / queries 16w .. 16w+15 of the window throughout: its rows
+// are loaded and LayerNorm'd straight into MFMA fragments (no LDS), the head's W rows are
+// staged in LDS once per workgroup.
+// Window geometry is compile-time (24 x 24 feature map, 12 x 12 windows: CAT-Seg's
+// FEATURE_RESOLUTION / window_size, host-checked).
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int IMG = 24, WS = 12, NWIN = 4, L = WS * WS;   // 144 tokens per window
+constexpr int C = 128, D = 32, NH = 4;
+constexpr int NW = 9, NT = NW * 64;
+constexpr int LDH = C + 8;            // sW row stride (272 B)
+constexpr int XD = 32;                // region one-hot dims appended to K / -100 dims to Q
+constexpr int KP = D + XD + 8;        // K row stride
+constexpr int KB = 160;               // key columns of V^T (5 x 32-key MFMA steps)
+constexpr int VP = KB + 4;            // V^T row stride
+constexpr int QP = D + 8;             // Q row stride
+constexpr int KTV = L / 16;           // 9 key tiles
+
+struct SwinP {
+  const bf16* x; int64_t ld_x;
+  const float* ln_g; const float* ln_b; float eps;
+  const bf16* w; const float* bias;
+  const bf16* g; int64_t ld_g; RowMap gmap;
+  bf16* out; int64_t ld_out;
+  int shift; float scale;
+};
+
+DEV int win_row(int slice, int wloc, int i, int shift) {       // roll(-shift) + partition
+  const int Y = (wloc >> 1) * WS + i / WS, X = (wloc & 1) * WS + i % WS;
+  const int y = Y + shift < IMG ? Y + shift : Y + shift - IMG;
+  const int x = X + shift < IMG ? X + shift : X + shift - IMG;
+  return slice * IMG * IMG + y * IMG + x;
+}
+
+DEV int region(int wloc, int i, int shift) {                    // model.py:161-176 label
+  const int Y = (wloc >> 1) * WS + i / WS, X = (wloc & 1) * WS + i % WS;
+  const int hb = Y < IMG - WS ? 0 : (Y < IMG - shift ? 1 : 2);
+  const int wb = X < IMG - WS ? 0 : (X < IMG - shift ? 1 : 2);
+  return hb * 3 + wb;
+}
+
+template <bool SWM>
+__global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p) {
+  __shared__ __attribute__((aligned(16))) bf16 sW[3 * D * LDH];   // W rows of one head: q | k | v
+  __shared__ __attribute__((aligned(16))) bf16 Ks[L * KP];
+  __shared__ __attribute__((aligned(16))) bf16 Vt[D * VP];
+  __shared__ __attribute__((aligned(16))) bf16 Qs[L * QP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int slice = blockIdx.x / NWIN, wloc = blockIdx.x % NWIN;
+  const int qi = wave * 16 + r16;                           // this lane's row / query
+  const int64_t qrow = win_row(slice, wloc, qi, p.shift);
+
+  // ---- LayerNorm of the wave's 16 rows straight into MFMA B fragments: lane (r16, g)
+  // loads chunks g, 4+g, 8+g, 12+g of row r16 = exactly its fragments for k-steps 0..3 ----
+  s16x8 hf[4];
+  {
+    float v[4][8], s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 u = ld16(p.x + qrow * p.ld_x + ks * 32 + 8 * g);
+      const bf16* e = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[ks][j] = bf2f(e[j]); s += v[ks][j]; }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[ks][j] -= mean; q += v[ks][j] * v[ks][j]; }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rstd = rsqrtf(q * (1.f / C) + p.eps);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c0 = ks * 32 + 8 * g;
+      float o8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o8[j] = v[ks][j] * rstd * p.ln_g[c0 + j] + p.ln_b[c0 + j];
+      uint4 u = make_uint4(f2bf2(o8[0], o8[1]), f2bf2(o8[2], o8[3]), f2bf2(o8[4], o8[5]), f2bf2(o8[6], o8[7]));
+      hf[ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  }
+  // region one-hot of every key (the same for all heads) and the zero V^T tail columns
+  if constexpr (SWM) {
+    for (int i = tid; i < L * XD; i += NT) {
+      const int key = i / XD, e = i % XD;
+      Ks[key * KP + D + e] = f2bf(e == region(wloc, key, p.shift) ? 1.f : 0.f);
+    }
+  }
+  for (int i = tid; i < D * (KB - L); i += NT) Vt[(i / (KB - L)) * VP + L + i % (KB - L)] = 0;
+  s16x8 qmask;
+  if constexpr (SWM) {      // -100/scale on the dims of every other region (raw-score units)
+    const int qreg = region(wloc, qi, p.shift);
+    const float neg = -100.f / p.scale;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int dim = 8 * g + j;
+      qmask[j] = (short)f2bf(dim < 9 && dim != qreg ? neg : 0.f);
+    }
+  }
+  s16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
+  const bf16* grow_p = p.g + rowmap(p.gmap, qrow) * p.ld_g;    // guidance row of this lane's row
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  for (int h = 0; h < NH; ++h) {
+    // ---- stage W rows of head h (q, k, v: 3 x 32 rows of 128) ----
+    for (int c = tid; c < 3 * D * 16; c += NT) {
+      const int lr = c >> 4, ch = c & 15;
+      const int n = (lr / D) * C + h * D + lr % D;
+      st16(&sW[lr * LDH + ch * 8], ld16(p.w + (int64_t)n * C + ch * 8));
+    }
+    __syncthreads();
+    // ---- q, k, v of head h for this wave's rows: D^T = W_h . H^T (4 consecutive d per lane) ----
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {          // 0 = q, 1 = k, 2 = v
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int lr0 = part * D + dt * 16;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          a = mfma_bf16(*reinterpret_cast<const s16x8*>(&sW[(lr0 + r16) * LDH + ks * 32 + 8 * g]), hf[ks], a);
+        const int n = part * C + h * D + dt * 16 + 4 * g;     // this lane's 4 output features
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = a[r] + p.bias[n + r];
+        if (part < 2) {                             // + W_g . LN(guidance) (per image, per pixel)
+          float gv[4];
+          load4<bf16>(grow_p + n, gv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += gv[r];
+        }
+        const int d = dt * 16 + 4 * g;
+        if (part == 0) {
+          *reinterpret_cast<uint2*>(&Qs[qi * QP + d]) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+        } else if (part == 1) {
+          *reinterpret_cast<uint2*>(&Ks[qi * KP + d]) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Vt[(d + r) * VP + qi] = f2bf(v[r]);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- attention of this wave's 16 queries over the 144 keys (one block) ----
+    s16x8 qf = *reinterpret_cast<const s16x8*>(&Qs[qi * QP + 8 * g]);
+    f32x4 st[KTV + 1];
+#pragma unroll
+    for (int kt = 0; kt < KTV; ++kt) {
+      const int kr = kt * 16 + r16;
+      f32x4 a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + 8 * g]), qf, f32x4{0.f, 0.f, 0.f, 0.f});
+      if constexpr (SWM) a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + D + 8 * g]), qmask, a);
+      st[kt] = a;
+    }
+    float mx = -1e30f;
+#pragma unroll
+    for (int kt = 0; kt < KTV; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kt][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float nb = -mx * sl2;
+#pragma unroll
+    for (int kt = 0; kt < KTV; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+    st[KTV] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KB / 32; ++u) {
+      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16* vr = &Vt[(dt * 16 + r16) * VP + 32 * u + 4 * g];
+        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+        uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
+      }
+      osum = mfma_bf16(ones, pb, osum);
+    }
+    const float inv = 1.f / osum[0];
+    bf16* O = p.out + qrow * p.ld_out + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+      *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
+          make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+    __syncthreads();      // sW / Ks / Vt / Qs are rewritten for the next head
+  }
+}
+
+}  // namespace
+
+extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->x && a->ln_g && a->ln_b && a->w_qkv && a->b_qkv && a->gqk && a->out,
+               "swin_window_attention: null pointer");
+  CATSEG_CHECK(a->dtype == CATSEG_BF16, "swin_window_attention: bf16 only");
+  CATSEG_CHECK(a->img_h == IMG && a->img_w == IMG && a->window == WS, "swin_window_attention: 24x24 map, 12x12 windows");
+  CATSEG_CHECK(a->n_heads == NH && a->head_dim == D, "swin_window_attention: 4 heads x 32");
+  CATSEG_CHECK(a->shift >= 0 && a->shift < WS, "swin_window_attention: bad shift");
+  CATSEG_CHECK(a->S > 0 && a->S * NWIN < (1LL << 31), "swin_window_attention: bad slice count");
+  CATSEG_CHECK(a->ld_x % 8 == 0 && a->ld_g % 4 == 0 && a->ld_out % 4 == 0, "swin_window_attention: row alignment");
+  CATSEG_CHECK(a->gmap.d1 > 0 && a->gmap.m1 > 0 && a->gmap.d2 > 0 && a->gmap.m2 > 0, "swin_window_attention: bad gmap");
+  SwinP p;
+  p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
+  p.ln_g = a->ln_g; p.ln_b = a->ln_b; p.eps = a->eps;
+  p.w = (const bf16*)a->w_qkv; p.bias = a->b_qkv;
+  p.g = (const bf16*)a->gqk; p.ld_g = a->ld_g;
+  p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
+  p.out = (bf16*)a->out; p.ld_out = a->ld_out;
+  p.shift = a->shift; p.scale = a->scale;
+  const dim3 grid((unsigned)(a->S * NWIN));
+  if (a->shift > 0)
+    hipLaunchKernelGGL(swin_fused_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(swin_fused_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, p);
+  return catseg_launch_status("swin_window_attention");
+}

@@ -286,6 +286,27 @@ int catseg_resize_bilinear(const float* in, int64_t B, int T, int h, int w, int 
                            float* out, int H, int W, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * catseg_swin_window_attention — fused LayerNorm(norm1) + [q|k|v] projection (+ the
+ * per-image guidance half of q and k) + shifted-window multi-head attention, one
+ * workgroup per (slice, window); q/k/v never reach HBM.  Replaces, per Swin block,
+ * model.py:191-199 (norm1, concat guidance_norm(guidance), roll, window_partition) and
+ * WindowAttention.forward model.py:86-114 up to the output projection (which stays a
+ * catseg_rows_gemm with the residual).  bf16; 24x24 map, 12x12 windows, 4 heads x 32.
+ *   out[row] = attention rows (heads concatenated), same row order as x;
+ *   q|k|v[row] = LN(x[row]) . w_qkv^T + b_qkv (+ gqk[gmap(row)] on the q and k columns)
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const void* x; int64_t ld_x;
+  const float* ln_g; const float* ln_b; float eps;
+  const void* w_qkv; const float* b_qkv;          /* [3*128][128], [3*128] */
+  const void* gqk; int64_t ld_g; CatsegRowMap gmap; /* [.][256] guidance halves of q, k */
+  void* out; int64_t ld_out;
+  int64_t S; int img_h, img_w, window, shift, n_heads, head_dim; float scale;
+  int dtype;
+} CatsegSwinAttnArgs;
+int catseg_swin_window_attention(const CatsegSwinAttnArgs* args, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Class-attention pooling (POOLING_SIZES != [1,1]; ClassTransformerLayer,
  * model.py:374-423) on the rows layout [S][H][W][C] (S = B*T slices).
  * ------------------------------------------------------------------------- */

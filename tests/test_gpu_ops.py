@@ -520,3 +520,52 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
     ops.resize_bilinear(merged[:1], out, crop=(res, res))
     ref = F.interpolate(merged[:1].cpu(), size=(480, 400), mode="bilinear", align_corners=False)
     close(out, ref, atol=1e-6, what="resize")
+
+
+@pytest.mark.parametrize("shift", [0, 6])
+def test_swin_window_attention_fused_vs_unfused(shift):
+    """catseg_swin_window_attention == catseg_rows_gemm(LN1 + q/k/v + guidance) followed by
+    catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry."""
+    B, T, HW, D = 2, 3, 576, 128
+    S = B * T
+    R = S * HW
+    dt = torch.bfloat16
+    X = rnd(R, D, seed=51, scale=2.0).to(dev, dt)
+    g1, b1 = (1 + rnd(D, seed=52, scale=0.2)).to(dev), rnd(D, seed=53, scale=0.2).to(dev)
+    W = (rnd(3 * D, D, seed=54) / math.sqrt(D)).to(dev, dt)
+    bias = rnd(3 * D, seed=55, scale=0.1).to(dev)
+    gqk = rnd(B * HW, 2 * D, seed=56, scale=0.5).to(dev, dt)
+    gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)
+    qkv = torch.empty(R, 3 * D, device=dev, dtype=dt)
+    ops.rows_gemm(X, W, qkv, ln=(g1, b1), bias=bias, add=gqk, addmap=gmap, add_ncols=2 * D)
+    ref = torch.empty(R, D, device=dev, dtype=dt)
+    ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], ref, n_seq=S * 4, seq_len=144, n_heads=4,
+                  head_dim=32, scale=32 ** -0.5, mode=1, img_hw=(24, 24), window=12, shift=shift)
+    out = torch.empty(R, D, device=dev, dtype=dt)
+    ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, out, S=S, img_hw=(24, 24), window=12, shift=shift,
+                              n_heads=4, head_dim=32, scale=32 ** -0.5)
+    err = (out.float() - ref.float()).abs()
+    # both are bf16 pipelines over the same math (q/k/v rounded to bf16 in both): equal to bf16 noise
+    assert err.max().item() < 3e-2 and err.mean().item() < 2e-3, (err.max().item(), err.mean().item())
+    # and against an fp32 torch restatement of the reference ops on the same bf16 inputs
+    from oracle import catseg_oracle as O
+    xf = X.float().cpu().reshape(S, 24, 24, D)
+    h = F.layer_norm(xf, (D,), g1.cpu(), b1.cpu())
+    gi = gqk.float().cpu().reshape(B, 1, 24, 24, 2 * D).expand(B, T, 24, 24, 2 * D).reshape(S, 24, 24, 2 * D)
+    qkv_f = h @ W.float().cpu().T + bias.cpu()
+    qkv_f[..., :2 * D] += gi
+    if shift:
+        qkv_f = torch.roll(qkv_f, shifts=(-shift, -shift), dims=(1, 2))
+    win = O.window_partition(qkv_f, 12).reshape(-1, 144, 3, 4, 32).permute(2, 0, 3, 1, 4)   # (3, nW*S, H, L, d)
+    q, k, v = win[0] * 32 ** -0.5, win[1], win[2]
+    attn = q @ k.transpose(-2, -1)
+    if shift:
+        m = O.shift_mask(24, 24, 12, shift)                  # (nW, L, L)
+        attn = attn.reshape(S, 4, 4, 144, 144) + m.reshape(1, 4, 1, 144, 144)
+        attn = attn.reshape(-1, 4, 144, 144)
+    o = (attn.softmax(-1) @ v).transpose(1, 2).reshape(-1, 12, 12, D)
+    o = O.window_reverse(o, 12, 24, 24)
+    if shift:
+        o = torch.roll(o, shifts=(shift, shift), dims=(1, 2))
+    e2 = (out.float().cpu().reshape(S, 24, 24, D) - o).abs()
+    assert e2.max().item() < 5e-2 and e2.mean().item() < 5e-3, (e2.max().item(), e2.mean().item())

@@ -50,6 +50,19 @@ for name, (N, K, act, has_res) in shapes.items():
                 run()
             e1.record(); torch.cuda.synchronize()
             res[(name, v)]["t"].append(e0.elapsed_time(e1) / 20)
+    # hipBLASLt (torch.mm, bf16 out, no fused epilogue) as the library reference point
+    Ab, Wt = A, W.t()
+    torch.mm(Ab, Wt); torch.cuda.synchronize()
+    tl = []
+    for rnd in range(7):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            torch.mm(Ab, Wt)
+        e1.record(); torch.cuda.synchronize()
+        tl.append(e0.elapsed_time(e1) / 20)
+    t = sorted(tl)[3]
+    print(f"{name:5s} N={N:5d} K={K:5d} torch.mm   : {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  (hipBLASLt)")
     for v in variants:
         t = sorted(res[(name, v)]["t"])[3]
         print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  "
