@@ -18,7 +18,15 @@ namespace {
 constexpr int KD = 128;          // row width
 constexpr int NW = 8, NT = NW * 64;
 constexpr int BM = 32;           // rows per tile
-constexpr int LDX = KD + 8;      // LDS row stride of sX (272 B: conflict-free ds_read_b128)
+// LDS images of bf16 row tiles are chunk-major with a row XOR swizzle: 16-byte chunk c of
+// tile row r lives at 16-byte slot  c * BM + (r ^ (c & 15)).  An MFMA fragment read (16
+// rows x one chunk per 16 lanes, chunks 4ks+q) and a row-chunk write (8 lanes = 8 chunks
+// of one row) then touch 16 (8) distinct bank slots: conflict-free (a padded row-major
+// image left ~45 % of the LDS cycles of these kernels as bank conflicts, rocprofv3
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
+template <int ROWS>
+DEV int cslot(int c, int r) { return (c * ROWS + (r ^ (c & 15))) * 8; }   // element offset
+constexpr int LDX = KD;          // sX holds BM rows x 16 chunks (no padding)
 constexpr int CPT = BM * 16 / NT; // 16-byte chunks of a tile per thread (= 1)
 constexpr int DEPTH = 3;          // tiles of input rows in flight per workgroup
 constexpr int DEPTH_MLP = 1;      // (the MLP holds both weight matrices in registers: no room)
@@ -64,7 +72,7 @@ DEV void put_chunk(uint4 u, const float* g, const float* b, float eps, bf16* sX)
 #pragma unroll
     for (int j = 0; j < 8; ++j) e[j] = f2bf(v[j] * rstd * gg[j] + bb[j]);
   }
-  st16(&sX[r * LDX + ch * 8], u);
+  st16(&sX[cslot<BM>(ch, r)], u);
 }
 
 DEV void add8(float* v, uint4 u) {
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
     for (int ks = 0; ks < 4; ++ks) {
       s16x8 xf[FM];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[(16 * j + r16) * LDX + ks * 32 + 8 * q]);
+      for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[cslot<BM>(ks * 4 + q, 16 * j + r16)]);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
 // out = Y + act(LN(Y) . W1^T + b1) . W2^T + b2 (+ R2), hidden = 512.
 // wave w: GEMM1 hidden rows [64w, 64w+64) (W1 fragments in registers),
 //         GEMM2 output rows [16w, 16w+16) over all 512 hidden (W2 fragments in registers).
-constexpr int HID = 512, LDH = HID + 8;
+constexpr int HID = 512, LDH = HID + 8;   // sH row stride (A/B: the cslot image measured slower here)
 
 template <int ACT, bool RES2>
 __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
       for (int ks = 0; ks < 4; ++ks) {
         s16x8 xf[FM];
 #pragma unroll
-        for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[(16 * j + r16) * LDX + ks * 32 + 8 * q]);
+        for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[cslot<BM>(ks * 4 + q, 16 * j + r16)]);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll

@@ -11,9 +11,9 @@
 // Q [query][d]), and consumed at once.  HBM traffic per window: the 144 input rows,
 // the 144 output rows, the guidance rows (shared by every class of an image: L2/MALL).
 //
-// 9 waves; wave w owns rows / queries 16w .. 16w+15 of the window throughout: its rows
-// are loaded and LayerNorm'd straight into MFMA fragments (no LDS), the head's W rows are
-// staged in LDS once per workgroup.
+// Persistent: one 9-wave workgroup per CU stages all of W_qkv in LDS once and walks the
+// windows; wave w owns rows / queries 16w .. 16w+15 of every window: its rows (prefetched
+// one window ahead) are LayerNorm'd straight into MFMA B fragments (no LDS).
 // Window geometry is compile-time (24 x 24 feature map, 12 x 12 windows: CAT-Seg's
 // FEATURE_RESOLUTION / window_size, host-checked).
 #include "common.h"
@@ -24,12 +24,10 @@ namespace {
 constexpr int IMG = 24, WS = 12, NWIN = 4, L = WS * WS;   // 144 tokens per window
 constexpr int C = 128, D = 32, NH = 4;
 constexpr int NW = 9, NT = NW * 64;
-constexpr int LDH = C + 8;            // sW row stride (272 B)
 constexpr int XD = 32;                // region one-hot dims appended to K / -100 dims to Q
-constexpr int KP = D + XD + 8;        // K row stride
+constexpr int KC = (D + XD) / 8;      // 16-byte chunks of a K row (d | region one-hot)
 constexpr int KB = 160;               // key columns of V^T (5 x 32-key MFMA steps)
 constexpr int VP = KB + 4;            // V^T row stride
-constexpr int QP = D + 8;             // Q row stride
 constexpr int KTV = L / 16;           // 9 key tiles
 
 struct SwinP {
@@ -40,6 +38,17 @@ struct SwinP {
   bf16* out; int64_t ld_out;
   int shift; float scale;
 };
+
+// LDS images of bf16 rows are chunk-major with a row XOR swizzle (16-byte chunk c of row r
+// at slot c * ROWS + (r ^ (c & 15))): MFMA fragment reads (16 rows x 1 chunk per 16 lanes)
+// and row writes hit distinct bank slots (the padded row-major images ran ~35 % bank
+// conflicts, rocprofv3 SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
+template <int ROWS>
+DEV int cslot(int c, int r) { return (c * ROWS + (r ^ (c & 15))) * 8; }
+// the same slot for r = rbase + rlo (rbase % 16 == 0, rlo < 16): the swizzle stays in the
+// low 4 bits, so per-tile addresses are one base + immediate offsets
+template <int ROWS>
+DEV int cslot16(int c, int rbase, int rlo) { return (c * ROWS + rbase + (rlo ^ (c & 15))) * 8; }
 
 DEV int win_row(int slice, int wloc, int i, int shift) {       // roll(-shift) + partition
   const int Y = (wloc >> 1) * WS + i / WS, X = (wloc & 1) * WS + i % WS;
@@ -56,162 +65,183 @@ DEV int region(int wloc, int i, int shift) {                    // model.py:161-
 }
 
 template <bool SWM>
-__global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p) {
-  __shared__ __attribute__((aligned(16))) bf16 sW[3 * D * LDH];   // W rows of one head: q | k | v
-  __shared__ __attribute__((aligned(16))) bf16 Ks[L * KP];
+__global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p, int nwin_total) {
+  __shared__ __attribute__((aligned(16))) bf16 sW[3 * C * C];      // all of W_qkv, staged once
+  __shared__ __attribute__((aligned(16))) bf16 Ks[L * KC * 8];
   __shared__ __attribute__((aligned(16))) bf16 Vt[D * VP];
-  __shared__ __attribute__((aligned(16))) bf16 Qs[L * QP];
+  __shared__ __attribute__((aligned(16))) bf16 Qs[L * D];
+  // LN gamma | beta | qkv bias, read from LDS inside the window loop (as loop-invariant
+  // global loads the compiler hoisted ~100 of them into VGPRs and spilled)
+  __shared__ __attribute__((aligned(16))) float sP[2 * C + 3 * C];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int slice = blockIdx.x / NWIN, wloc = blockIdx.x % NWIN;
-  const int qi = wave * 16 + r16;                           // this lane's row / query
-  const int64_t qrow = win_row(slice, wloc, qi, p.shift);
+  const int qi = wave * 16 + r16;                           // this lane's row / query in a window
+  for (int i = tid; i < 5 * C; i += NT) sP[i] = i < C ? p.ln_g[i] : i < 2 * C ? p.ln_b[i - C] : p.bias[i - 2 * C];
 
-  // ---- LayerNorm of the wave's 16 rows straight into MFMA B fragments: lane (r16, g)
-  // loads chunks g, 4+g, 8+g, 12+g of row r16 = exactly its fragments for k-steps 0..3 ----
-  s16x8 hf[4];
-  {
-    float v[4][8], s = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const uint4 u = ld16(p.x + qrow * p.ld_x + ks * 32 + 8 * g);
-      const bf16* e = reinterpret_cast<const bf16*>(&u);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { v[ks][j] = bf2f(e[j]); s += v[ks][j]; }
-    }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    const float mean = s * (1.f / C);
-    float q = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { v[ks][j] -= mean; q += v[ks][j] * v[ks][j]; }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
-    const float rstd = rsqrtf(q * (1.f / C) + p.eps);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int c0 = ks * 32 + 8 * g;
-      float o8[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o8[j] = v[ks][j] * rstd * p.ln_g[c0 + j] + p.ln_b[c0 + j];
-      uint4 u = make_uint4(f2bf2(o8[0], o8[1]), f2bf2(o8[2], o8[3]), f2bf2(o8[4], o8[5]), f2bf2(o8[6], o8[7]));
-      hf[ks] = *reinterpret_cast<s16x8*>(&u);
-    }
-  }
-  // region one-hot of every key (the same for all heads) and the zero V^T tail columns
-  if constexpr (SWM) {
-    for (int i = tid; i < L * XD; i += NT) {
-      const int key = i / XD, e = i % XD;
-      Ks[key * KP + D + e] = f2bf(e == region(wloc, key, p.shift) ? 1.f : 0.f);
-    }
+  for (int c = tid; c < 3 * C * 16; c += NT) {
+    const int lr = c >> 4, ch = c & 15;
+    st16(&sW[cslot<3 * C>(ch, lr)], ld16(p.w + (int64_t)lr * C + ch * 8));
   }
   for (int i = tid; i < D * (KB - L); i += NT) Vt[(i / (KB - L)) * VP + L + i % (KB - L)] = 0;
-  s16x8 qmask;
-  if constexpr (SWM) {      // -100/scale on the dims of every other region (raw-score units)
-    const int qreg = region(wloc, qi, p.shift);
-    const float neg = -100.f / p.scale;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int dim = 8 * g + j;
-      qmask[j] = (short)f2bf(dim < 9 && dim != qreg ? neg : 0.f);
-    }
-  }
+  __syncthreads();
   s16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
-  const bf16* grow_p = p.g + rowmap(p.gmap, qrow) * p.ld_g;    // guidance row of this lane's row
   const float sl2 = p.scale * 1.4426950408889634f;
 
-  for (int h = 0; h < NH; ++h) {
-    // ---- stage W rows of head h (q, k, v: 3 x 32 rows of 128) ----
-    for (int c = tid; c < 3 * D * 16; c += NT) {
-      const int lr = c >> 4, ch = c & 15;
-      const int n = (lr / D) * C + h * D + lr % D;
-      st16(&sW[lr * LDH + ch * 8], ld16(p.w + (int64_t)n * C + ch * 8));
-    }
-    __syncthreads();
-    // ---- q, k, v of head h for this wave's rows: D^T = W_h . H^T (4 consecutive d per lane) ----
+  // rows of the next window are prefetched into registers while this one computes:
+  // lane (r16, g) holds chunks g, 4+g, 8+g, 12+g of its row = its MFMA B fragments
+  uint4 nx[4];
+  auto fetch = [&](int win) {
+    const int64_t row = win_row(win / NWIN, win % NWIN, qi, p.shift);
 #pragma unroll
-    for (int part = 0; part < 3; ++part) {          // 0 = q, 1 = k, 2 = v
+    for (int ks = 0; ks < 4; ++ks) nx[ks] = ld16(p.x + row * p.ld_x + ks * 32 + 8 * g);
+  };
+  int win = blockIdx.x;
+  if (win < nwin_total) fetch(win);
+  for (; win < nwin_total; win += gridDim.x) {
+    const int slice = win / NWIN, wloc = win % NWIN;
+    const int64_t qrow = win_row(slice, wloc, qi, p.shift);
+    // ---- LayerNorm of this lane's row into MFMA B fragments ----
+    s16x8 hf[4];
+    {
+      float v[4][8], s = 0.f;
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int lr0 = part * D + dt * 16;
-        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16* e = reinterpret_cast<const bf16*>(&nx[ks]);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          a = mfma_bf16(*reinterpret_cast<const s16x8*>(&sW[(lr0 + r16) * LDH + ks * 32 + 8 * g]), hf[ks], a);
-        const int n = part * C + h * D + dt * 16 + 4 * g;     // this lane's 4 output features
-        float v[4];
+        for (int j = 0; j < 8; ++j) { v[ks][j] = bf2f(e[j]); s += v[ks][j]; }
+      }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean = s * (1.f / C);
+      float q = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = a[r] + p.bias[n + r];
-        if (part < 2) {                             // + W_g . LN(guidance) (per image, per pixel)
-          float gv[4];
-          load4<bf16>(grow_p + n, gv);
+      for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += gv[r];
-        }
-        const int d = dt * 16 + 4 * g;
-        if (part == 0) {
-          *reinterpret_cast<uint2*>(&Qs[qi * QP + d]) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
-        } else if (part == 1) {
-          *reinterpret_cast<uint2*>(&Ks[qi * KP + d]) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
-        } else {
+        for (int j = 0; j < 8; ++j) { v[ks][j] -= mean; q += v[ks][j] * v[ks][j]; }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float rstd = rsqrtf(q * (1.f / C) + p.eps);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Vt[(d + r) * VP + qi] = f2bf(v[r]);
-        }
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c0 = ks * 32 + 8 * g;
+        float o8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o8[j] = v[ks][j] * rstd * sP[c0 + j] + sP[C + c0 + j];
+        uint4 u = make_uint4(f2bf2(o8[0], o8[1]), f2bf2(o8[2], o8[3]), f2bf2(o8[4], o8[5]), f2bf2(o8[6], o8[7]));
+        hf[ks] = *reinterpret_cast<s16x8*>(&u);
       }
     }
-    __syncthreads();
+    if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
+    // region one-hot of every key of this window (the previous window's last barrier retired its reads)
+    if constexpr (SWM) {
+      for (int i = tid; i < L * XD; i += NT) {
+        const int key = i / XD, e = i % XD;
+        Ks[cslot<L>((D + e) >> 3, key) + (e & 7)] = f2bf(e == region(wloc, key, p.shift) ? 1.f : 0.f);
+      }
+    }
+    s16x8 qmask;
+    if constexpr (SWM) {    // -100/scale on the dims of every other region (raw-score units)
+      const int qreg = region(wloc, qi, p.shift);
+      const float neg = -100.f / p.scale;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int dim = 8 * g + j;
+        qmask[j] = (short)f2bf(dim < 9 && dim != qreg ? neg : 0.f);
+      }
+    }
+    const bf16* grow_p = p.g + rowmap(p.gmap, qrow) * p.ld_g;  // guidance row of this lane's row
 
-    // ---- attention of this wave's 16 queries over the 144 keys (one block) ----
-    s16x8 qf = *reinterpret_cast<const s16x8*>(&Qs[qi * QP + 8 * g]);
-    f32x4 st[KTV + 1];
+#pragma unroll 1
+    for (int h = 0; h < NH; ++h) {
+      // lane ids made opaque per head: the LDS addresses below are recomputed each head
+      // (a few VALU) instead of being hoisted as ~30 loop-invariant VGPRs and spilled
+      int r16 = lane & 15, g = lane >> 4;
+      asm volatile("" : "+v"(r16), "+v"(g));
+      // ---- q, k, v of head h for this wave's rows: D^T = W_h . H^T (4 consecutive d per lane) ----
+#pragma unroll 1
+      for (int part = 0; part < 3; ++part) {          // 0 = q, 1 = k, 2 = v (rolled: bounds VGPRs)
 #pragma unroll
-    for (int kt = 0; kt < KTV; ++kt) {
-      const int kr = kt * 16 + r16;
-      f32x4 a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + 8 * g]), qf, f32x4{0.f, 0.f, 0.f, 0.f});
-      if constexpr (SWM) a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + D + 8 * g]), qmask, a);
-      st[kt] = a;
-    }
-    float mx = -1e30f;
+        for (int dt = 0; dt < 2; ++dt) {
+          const int n0 = part * C + h * D + dt * 16;  // weight row block
+          f32x4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kt = 0; kt < KTV; ++kt)
+          for (int ks = 0; ks < 4; ++ks)
+            a = mfma_bf16(*reinterpret_cast<const s16x8*>(&sW[cslot16<3 * C>(ks * 4 + g, n0, r16)]), hf[ks], a);
+          const int n = n0 + 4 * g;                   // this lane's 4 output features
+          float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kt][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float nb = -mx * sl2;
+          for (int r = 0; r < 4; ++r) v[r] = a[r] + sP[2 * C + n + r];
+          if (part < 2) {                             // + W_g . LN(guidance) (per image, per pixel)
+            float gv[4];
+            load4<bf16>(grow_p + n, gv);
 #pragma unroll
-    for (int kt = 0; kt < KTV; ++kt)
+            for (int r = 0; r < 4; ++r) v[r] += gv[r];
+          }
+          const int d = dt * 16 + 4 * g;
+          if (part == 0) {
+            *reinterpret_cast<uint2*>(&Qs[cslot16<L>(d >> 3, wave * 16, r16) + (d & 7)]) =
+                make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+          } else if (part == 1) {
+            *reinterpret_cast<uint2*>(&Ks[cslot16<L>(d >> 3, wave * 16, r16) + (d & 7)]) =
+                make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+          } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
-    st[KTV] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < KB / 32; ++u) {
-      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
-                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
-      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const bf16* vr = &Vt[(dt * 16 + r16) * VP + 32 * u + 4 * g];
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-        uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
+            for (int r = 0; r < 4; ++r) Vt[(d + r) * VP + qi] = f2bf(v[r]);
+          }
+        }
       }
-      osum = mfma_bf16(ones, pb, osum);
-    }
-    const float inv = 1.f / osum[0];
-    bf16* O = p.out + qrow * p.ld_out + h * D;
+      __syncthreads();
+
+      // ---- attention of this wave's 16 queries over the 144 keys (one block) ----
+      const s16x8 qf = *reinterpret_cast<const s16x8*>(&Qs[cslot16<L>(g, wave * 16, r16)]);
+      f32x4 st[KTV + 1];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-      *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
-          make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
-    __syncthreads();      // sW / Ks / Vt / Qs are rewritten for the next head
+      for (int kt = 0; kt < KTV; ++kt) {
+          f32x4 a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[cslot16<L>(g, kt * 16, r16)]), qf,
+                            f32x4{0.f, 0.f, 0.f, 0.f});
+        if constexpr (SWM) a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[cslot16<L>(4 + g, kt * 16, r16)]), qmask, a);
+        st[kt] = a;
+      }
+      float mx = -1e30f;
+#pragma unroll
+      for (int kt = 0; kt < KTV; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float nb = -mx * sl2;
+#pragma unroll
+      for (int kt = 0; kt < KTV; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+      st[KTV] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < KB / 32; ++u) {
+        uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                              f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+        const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16* vr = &Vt[(dt * 16 + r16) * VP + 32 * u + 4 * g];
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
+        }
+        osum = mfma_bf16(ones, pb, osum);
+      }
+      const float inv = 1.f / osum[0];
+      bf16* O = p.out + qrow * p.ld_out + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
+            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+      __syncthreads();    // Ks / Vt / Qs are rewritten for the next head / window
+    }
   }
 }
 
@@ -235,10 +265,18 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
   p.out = (bf16*)a->out; p.ld_out = a->ld_out;
   p.shift = a->shift; p.scale = a->scale;
-  const dim3 grid((unsigned)(a->S * NWIN));
+  // persistent: one workgroup per CU (W_qkv staged once per CU), windows strided over them
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  const int nwin_total = (int)(a->S * NWIN);
+  const dim3 grid((unsigned)std::min(nwin_total, n_cu));
   if (a->shift > 0)
-    hipLaunchKernelGGL(swin_fused_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(swin_fused_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);
   else
-    hipLaunchKernelGGL(swin_fused_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(swin_fused_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);
   return catseg_launch_status("swin_window_attention");
 }
