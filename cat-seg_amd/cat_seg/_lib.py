@@ -70,6 +70,19 @@ class AttnArgs(C.Structure):
     ]
 
 
+class ClassAttnArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ld_x", i64),
+        ("ln_g", vp), ("ln_b", vp), ("eps", f32),
+        ("w_qkv", vp), ("b_qkv", vp),
+        ("tg", vp), ("ld_tg", i64), ("tg_bstride", i64),
+        ("n_pad", i32), ("k_pad", vp), ("v_pad", vp), ("attn_eps", f32),
+        ("y", vp), ("ld_y", i64),
+        ("B", i64), ("T", i32), ("HW", i32), ("n_heads", i32), ("head_dim", i32),
+        ("dtype", i32),
+    ]
+
+
 class LinAttnArgs(C.Structure):
     _fields_ = [
         ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
@@ -130,6 +143,7 @@ _SIGS = {
     "catseg_bicubic_resize": [vp, i32, i32, vp, i32, vp],
     "catseg_postprocess": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
     "catseg_swin_window_attention": [C.POINTER(SwinAttnArgs), vp],
+    "catseg_class_attention": [C.POINTER(ClassAttnArgs), vp],
     "catseg_resize_bilinear": [vp, i64, i32, i32, i32, i32, i32, vp, i32, i32, vp],
     "catseg_avgpool_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
     "catseg_upsample_add_rows": [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp],

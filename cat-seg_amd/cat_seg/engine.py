@@ -57,6 +57,7 @@ class CatSegEngine:
         self.arch = arch
         self.dt = dtype
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
+        self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
         self.device = torch.device(device)
         self._text = None
         with torch.no_grad():
@@ -391,9 +392,11 @@ class CatSegEngine:
                 ops.gather_rows(t, idx, o)
                 tgqk.append(o)
             tmap = rowmap(d1=HWc)
+            tg_bstride = T
         else:
             tgqk = tx.tgqk
             tmap = rowmap(d1=HWc, m1=T)
+            tg_bstride = 0
         # ---- aggregation layers (model.py:717-718) ----
         qkv = torch.empty(R, 3 * D, device=dev, dtype=dt)
         o = torch.empty(R, D, device=dev, dtype=dt)
@@ -413,6 +416,7 @@ class CatSegEngine:
         fused_swin = (self.fused_swin and dt == torch.bfloat16 and (H_, W_, ws) == (24, 24, 12)
                       and a.nheads == 4 and D == 128)
         gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)     # (b, t, p) -> (b, p)
+        fused_class = self.fused_class and dt == torch.bfloat16 and a.nheads == 4 and D == 128
         n_pad = a.pad_len - T if a.pad_len > 0 and T < a.pad_len else 0
         for l, lay in enumerate(w.layers):
             ops.layernorm(G3, lay.gnw, lay.gnb, gn)           # guidance_norm, once per image
@@ -436,23 +440,33 @@ class CatSegEngine:
                              act=L.ACT_GELU, res=X)                              # x = x + Mlp(norm2(x))
             ca = lay.ca
             if not pooled:
-                ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
-                              add_ncols=2 * D)
-                ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
-                                     n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
-                                     k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                if fused_class:
+                    ops.class_attention(X, (ca.n1w, ca.n1b), ca.wqkv, ca.bqkv, tgqk[l], Y, B=B, T=T, HW=HW,
+                                        n_heads=a.nheads, head_dim=D // a.nheads, tg_bstride=tg_bstride,
+                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                else:
+                    ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
+                                  add_ncols=2 * D)
+                    ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
+                                         n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                                         k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
                 # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
                 ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y,
                              res2=X)
             else:
                 # x_pool = AvgPool(x); x_pool += attn; x_pool += MLP; x += interp_ac(x_pool) (model.py:387-423)
                 ops.avgpool_rows(X, Xp, S=S, H=H_, W=W_, C=D, pool=(ph, pw))
-                qkvp = qkv[:Rp]
-                ops.rows_gemm(Xp, ca.wqkv, qkvp, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
-                              add_ncols=2 * D)
-                ops.linear_attention(qkvp[:, :D], qkvp[:, D:2 * D], qkvp[:, 2 * D:], Xp, Yp, B=B, T=T, HW=HWc,
-                                     n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
-                                     k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                if fused_class:
+                    ops.class_attention(Xp, (ca.n1w, ca.n1b), ca.wqkv, ca.bqkv, tgqk[l], Yp, B=B, T=T, HW=HWc,
+                                        n_heads=a.nheads, head_dim=D // a.nheads, tg_bstride=tg_bstride,
+                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                else:
+                    qkvp = qkv[:Rp]
+                    ops.rows_gemm(Xp, ca.wqkv, qkvp, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
+                                  add_ncols=2 * D)
+                    ops.linear_attention(qkvp[:, :D], qkvp[:, D:2 * D], qkvp[:, 2 * D:], Xp, Yp, B=B, T=T,
+                                         HW=HWc, n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                                         k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
                 ops.rows_mlp(Yp, ca.w0, ca.b0, ca.w2, Yp, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Yp)
                 ops.upsample_add_rows(Yp, X, S=S, Hp=H_ // ph, Wp=W_ // pw, C=D, H=H_, W=W_)
         del qkv, o, Y, gn, gqk

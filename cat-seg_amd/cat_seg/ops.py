@@ -169,6 +169,26 @@ def swin_window_attention(x, ln, w_qkv, b_qkv, gqk, gmap, out, *, S, img_hw, win
     return out
 
 
+def class_attention(x, ln, w_qkv, b_qkv, tg, y, *, B, T, HW, n_heads, head_dim, tg_bstride=0, n_pad=0,
+                    k_pad=None, v_pad=None, eps=1e-5, attn_eps=1e-6):
+    """Fused norm1 + q/k/v (+ text-guidance half) + linear class attention + residual
+    (catseg_class_attention): y = x + LinearAttention(...)."""
+    a = L.ClassAttnArgs()
+    a.x, a.ld_x = x.data_ptr(), _ld(x)
+    a.ln_g, a.ln_b, a.eps = ln[0].data_ptr(), ln[1].data_ptr(), eps
+    a.w_qkv, a.b_qkv = w_qkv.data_ptr(), b_qkv.data_ptr()
+    a.tg, a.ld_tg, a.tg_bstride = tg.data_ptr(), _ld(tg), tg_bstride
+    a.n_pad, a.k_pad, a.v_pad, a.attn_eps = n_pad, _p(k_pad), _p(v_pad), attn_eps
+    a.y, a.ld_y = y.data_ptr(), _ld(y)
+    a.B, a.T, a.HW, a.n_heads, a.head_dim, a.dtype = B, T, HW, n_heads, head_dim, _dt(x)
+    R = B * T * HW
+    C = n_heads * head_dim
+    flops = 2 * R * C * 3 * C + 4 * R * n_heads * head_dim * head_dim
+    with _rec("class_attention", flops, x.element_size() * R * 2 * C):
+        call("catseg_class_attention", a, _stream())
+    return y
+
+
 def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_pad=None, v_pad=None, eps=1e-6):
     a = L.LinAttnArgs()
     a.q, a.k, a.v, a.ld_qkv = q.data_ptr(), k.data_ptr(), v.data_ptr(), _ld(q)

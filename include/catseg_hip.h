@@ -307,6 +307,30 @@ typedef struct {
 int catseg_swin_window_attention(const CatsegSwinAttnArgs* args, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * catseg_class_attention — fused LayerNorm(norm1) + [q|k|v] projection (+ the
+ * per-class text-guidance half of q and k) + linear class attention + the attention
+ * residual, persistent workgroups over pixels; q/k/v never reach HBM.  Replaces, per
+ * class layer, model.py:397-413 up to `x_pool + attention(norm1(x_pool), guidance)`
+ * (AttentionLayer model.py:338-354, LinearAttention model.py:256-286), i.e. the
+ * catseg_rows_gemm + catseg_linear_attention pair.  bf16; 4 heads x 32.
+ *   rows of pixel (b, p): (b*T + t)*HW + p, t < T;  tg row of class t: b*tg_bstride + t
+ *   (tg = [.][256] guidance halves of q | k, without bias; tg_bstride 0 = shared);
+ *   y[row] = x[row] + LinearAttention(q, k, v)[row] with the n_pad learned padding
+ *   tokens' constant projections k_pad / v_pad (fp32) in the sums, S = T + n_pad.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const void* x; int64_t ld_x;
+  const float* ln_g; const float* ln_b; float eps;
+  const void* w_qkv; const float* b_qkv;          /* [3*128][128], [3*128] */
+  const void* tg; int64_t ld_tg; int64_t tg_bstride;
+  int n_pad; const float* k_pad; const float* v_pad; float attn_eps;
+  void* y; int64_t ld_y;
+  int64_t B; int T; int HW; int n_heads; int head_dim;
+  int dtype;
+} CatsegClassAttnArgs;
+int catseg_class_attention(const CatsegClassAttnArgs* args, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Class-attention pooling (POOLING_SIZES != [1,1]; ClassTransformerLayer,
  * model.py:374-423) on the rows layout [S][H][W][C] (S = B*T slices).
  * ------------------------------------------------------------------------- */

@@ -209,6 +209,56 @@ def test_linear_attention(dt, T, n_pad):
     close(y, x.to(dt).double() + o, atol=2e-5 if dt == torch.float32 else 3e-2, what="linattn")
 
 
+@pytest.mark.parametrize("T,n_pad,per_image", [(150, 106, False), (20, 236, False), (256, 0, True), (37, 0, False),
+                                               (33, 5, True)])
+def test_class_attention_fused(T, n_pad, per_image):
+    """catseg_class_attention == norm1 + AttentionLayer q/k/v (+ text guidance) + LinearAttention
+    + residual (model.py:397-413, 338-354, 256-286) against an fp64 restatement on the same bf16
+    inputs, and against the unfused rows_gemm + linear_attention pair.  per_image: guidance rows
+    gathered per image (the top-k path, tg_bstride = T)."""
+    B, HW, D = 2, 24, 128
+    dt = torch.bfloat16
+    R = B * T * HW
+    X = rnd(R, D, seed=61, scale=2.0).to(dev, dt)
+    g1, b1 = (1 + rnd(D, seed=62, scale=0.2)).to(dev), rnd(D, seed=63, scale=0.2).to(dev)
+    W = (rnd(3 * D, D, seed=64) / math.sqrt(D)).to(dev, dt)
+    bias = rnd(3 * D, seed=65, scale=0.1).to(dev)
+    ntg = B * T if per_image else T
+    tg = rnd(ntg, 2 * D, seed=66, scale=0.5).to(dev, dt)
+    kp, vp = rnd(D, seed=67).to(dev), rnd(D, seed=68).to(dev)
+    y = torch.empty_like(X)
+    ops.class_attention(X, (g1, b1), W, bias, tg, y, B=B, T=T, HW=HW, n_heads=4, head_dim=32,
+                        tg_bstride=T if per_image else 0, n_pad=n_pad, k_pad=kp, v_pad=vp)
+    # fp64 restatement on the same bf16 inputs
+    xf = X.double().cpu()
+    h = F.layer_norm(xf, (D,), g1.double().cpu(), b1.double().cpu())
+    qkv = h @ W.double().cpu().T + bias.double().cpu()
+    tgf = tg.double().cpu()
+    if per_image:
+        tg_rows = tgf.reshape(B, T, 1, 2 * D).expand(B, T, HW, 2 * D).reshape(R, 2 * D)
+    else:
+        tg_rows = tgf.reshape(1, T, 1, 2 * D).expand(B, T, HW, 2 * D).reshape(R, 2 * D)
+    qkv[:, :2 * D] += tg_rows
+    z = qkv.reshape(B, T, HW, 3, 4, 32).permute(3, 0, 2, 1, 4, 5).reshape(3, B * HW, T, 4, 32)
+    q, k, v = z[0], z[1], z[2]
+    if n_pad:
+        k = torch.cat([k, kp.double().cpu().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+        v = torch.cat([v, vp.double().cpu().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+    o = O.linear_attention(q, k, v).reshape(B, HW, T, D).permute(0, 2, 1, 3).reshape(-1, D)
+    ref = xf + o
+    err = (y.double().cpu() - ref).abs()
+    assert err.max().item() < 5e-2 and err.mean().item() < 5e-3, (err.max().item(), err.mean().item())
+    # the unfused bf16 pair (q/k/v rounded to bf16 in HBM) on the same inputs
+    qkv_d = torch.empty(R, 3 * D, device=dev, dtype=dt)
+    tmap = rowmap(d1=HW) if per_image else rowmap(d1=HW, m1=T)
+    ops.rows_gemm(X, W, qkv_d, ln=(g1, b1), bias=bias, add=tg, addmap=tmap, add_ncols=2 * D)
+    y2 = torch.empty_like(X)
+    ops.linear_attention(qkv_d[:, :D], qkv_d[:, D:2 * D], qkv_d[:, 2 * D:], X, y2, B=B, T=T, HW=HW, n_heads=4,
+                         head_dim=32, n_pad=n_pad, k_pad=kp, v_pad=vp)
+    e2 = (y.float() - y2.float()).abs()
+    assert e2.max().item() < 5e-2 and e2.mean().item() < 5e-3, (e2.max().item(), e2.mean().item())
+
+
 # ----------------------------------------------------------------------------- conv + GN
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_conv3x3_dual_source_gn(dt):
