@@ -148,6 +148,100 @@ __global__ void corr_embed_kernel(const float* corr, int64_t ts, int64_t bs, con
   }
 }
 
+// corr_embed on the MFMA (bf16 output, hidden = 128): the 7x7 conv of a cost slice is the
+// GEMM out[pix][c] = sum_k patch[pix][k] . W[c][k] over the 49 taps (K padded to 64).  fp32
+// operands enter as bf16 hi + lo pairs (hi.hi + hi.lo + lo.hi: ~16-bit mantissa products,
+// fp32 accumulation), so the result matches the fp32 conv to well below the bf16 output
+// rounding.  One 4-wave workgroup per slice: the zero-padded slice sits in LDS, every wave
+// keeps all 128 x 64 weights as MFMA A fragments in registers and walks 16-pixel tiles:
+// D[c][pix] with 4 consecutive channels per lane (8-byte stores).
+int g_corr_mfma = 1;   // A/B switch (catseg_set_corr_mfma)
+
+DEV void split_bf16(float v, bf16& hi, bf16& lo) {
+  hi = f2bf(v);
+  lo = f2bf(v - bf2f(hi));
+}
+
+__global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr, int64_t ts, int64_t bs,
+                                                              const int32_t* classes, int Tn, int H, int W,
+                                                              const float* w, const float* bias, bf16* out) {
+  constexpr int HID = 128;
+  __shared__ float sin[1024];          // (H + 6) x (W + 6) zero-padded slice (host-checked)
+  const int PW = W + 6, PH = H + 6;
+  const int64_t s = blockIdx.x;
+  const int64_t b = s / Tn;
+  const int t = (int)(s % Tn);
+  const int cls = classes ? classes[s] : t;
+  const float* src = corr + (int64_t)cls * ts + b * bs;
+  for (int i = threadIdx.x; i < PH * PW; i += blockDim.x) {
+    const int y = i / PW - 3, x = i % PW - 3;
+    sin[i] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  s16x8 whi[8][2], wlo[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16 h[8], l[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * ks + 8 * q + j;
+        split_bf16(k < 49 ? w[(16 * i + r16) * 49 + k] : 0.f, h[j], l[j]);
+      }
+      whi[i][ks] = *reinterpret_cast<const s16x8*>(h);
+      wlo[i][ks] = *reinterpret_cast<const s16x8*>(l);
+    }
+  int toff[2][8];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * ks + 8 * q + j;
+      toff[ks][j] = k < 49 ? (k / 7) * PW + k % 7 : -1;
+    }
+  __syncthreads();
+  const int HW = H * W;
+  const int ntiles = (HW + 15) / 16;
+  for (int tile = wave; tile < ntiles; tile += 4) {
+    const int pix = tile * 16 + r16;
+    const bool valid = pix < HW;
+    const int y = valid ? pix / W : 0, x = valid ? pix % W : 0;
+    const int base = y * PW + x;
+    s16x8 bhi[2], blo[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16 h[8], l[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split_bf16(toff[ks][j] >= 0 ? sin[base + toff[ks][j]] : 0.f, h[j], l[j]);
+      bhi[ks] = *reinterpret_cast<const s16x8*>(h);
+      blo[ks] = *reinterpret_cast<const s16x8*>(l);
+    }
+    f32x4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        acc[i] = mfma_bf16(whi[i][ks], bhi[ks], acc[i]);
+        acc[i] = mfma_bf16(whi[i][ks], blo[ks], acc[i]);
+        acc[i] = mfma_bf16(wlo[i][ks], bhi[ks], acc[i]);
+      }
+    }
+    if (valid) {
+      bf16* o = out + (s * HW + pix) * HID;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = 16 * i + 4 * q;
+        const float4 bb = *reinterpret_cast<const float4*>(bias + c);
+        *reinterpret_cast<uint2*>(o + c) = make_uint2(f2bf2(acc[i][0] + bb.x, acc[i][1] + bb.y),
+                                                      f2bf2(acc[i][2] + bb.z, acc[i][3] + bb.w));
+      }
+    }
+  }
+}
+
 // ---------------- top-k classes per image (bitonic sort of (max corr, idx)) ---------
 __global__ void topk_kernel(const float* corr, int64_t ts, int64_t bs, int Tn, int HW, int k, int32_t* classes) {
   __shared__ float sv[2048];
@@ -431,6 +525,8 @@ extern "C" int catseg_l2normalize(const void* in, int64_t ld_in, CatsegRowMap in
   return rownorm<false>(in, ld_in, inmap, dtype_in, out, ld_out, dtype_out, nullptr, nullptr, rows, cols, eps, stream);
 }
 
+extern "C" void catseg_set_corr_mfma(int enable) { g_corr_mfma = enable != 0; }
+
 extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
                                  const int32_t* classes, int64_t B, int T, int H, int W, const float* weight,
                                  const float* bias, int hidden, void* out, int dtype, void* stream) {
@@ -439,7 +535,10 @@ extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64
   const size_t sh = ((H + 6) * (W + 6) + 49 * hidden) * sizeof(float);
   CATSEG_CHECK(sh <= 64 * 1024, "corr_embed: slice too large for LDS");
   const unsigned grid = (unsigned)(B * T);
-  if (dtype == CATSEG_BF16)
+  if (dtype == CATSEG_BF16 && hidden == 128 && (H + 6) * (W + 6) <= 1024 && g_corr_mfma)
+    hipLaunchKernelGGL(corr_embed_mfma_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
+                       corr_b_stride, classes, T, H, W, weight, bias, (bf16*)out);
+  else if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(corr_embed_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, corr, corr_t_stride,
                        corr_b_stride, classes, T, H, W, weight, bias, hidden, (bf16*)out);
   else

@@ -333,6 +333,20 @@ def test_corr_embed_topk(dt):
     ref = F.conv2d(sel.reshape(B * k, 1, H, W).double(), w.double(), b.double(), padding=3)
     close(X.reshape(B * k, H, W, hid).permute(0, 3, 1, 2), ref, atol=1e-5 if dt == torch.float32 else 2e-2,
           what="corr_embed")
+    if dt == torch.bfloat16:
+        # both bf16 kernels (MFMA hi/lo split, VALU) land within bf16 output rounding of fp64
+        lib = L.load()
+        try:
+            for mode in (1, 0):
+                lib.catseg_set_corr_mfma(mode)
+                X.zero_()
+                ops.corr_embed(cd, t_stride=B * H * W, b_stride=H * W, B=B, T=k, H=H, W=W,
+                               weight=w.reshape(hid, 49).to(dev), bias=b.to(dev), out=X, classes=cls)
+                got = X.reshape(B * k, H, W, hid).permute(0, 3, 1, 2).double().cpu()
+                err = (got - ref).abs() - 2.0 ** -8 * ref.abs()
+                assert err.max().item() <= 1e-6, (mode, err.max().item())
+        finally:
+            lib.catseg_set_corr_mfma(1)
 
 
 def test_preprocess_im2col():
