@@ -115,6 +115,7 @@ class ConvArgs(C.Structure):
         ("gn_mean", vp), ("gn_rstd", vp), ("gn_gamma", vp), ("gn_beta", vp), ("gn_cpg", i32),
         ("out", vp), ("stats", vp), ("stats_cpg", i32),
         ("dtype", i32),
+        ("addend", vp), ("addend_slice_stride", i64), ("addend_div", i64),
     ]
 
 
@@ -128,7 +129,9 @@ _SIGS = {
     "catseg_attention": [C.POINTER(AttnArgs), vp],
     "catseg_linear_attention": [C.POINTER(LinAttnArgs), vp],
     "catseg_conv3x3": [C.POINTER(ConvArgs), vp],
+    "catseg_conv3x3_partial": [vp, i64, i32, i32, i32, vp, i32, vp, i32, vp],
     "catseg_conv_tile_rows": [],
+    "catseg_conv3x3_stats_tile": [C.POINTER(ConvArgs)],
     "catseg_groupnorm_stats": [vp, i64, i32, i32, i64, f32, vp, vp, vp],
     "catseg_groupnorm_relu": [vp, vp, i64, i64, i32, i32, vp, vp, vp, vp, i32, vp],
     "catseg_conv3x3_head": [vp, i64, i32, i32, i32, i32, vp, f32, vp, i32, vp, i32, vp],

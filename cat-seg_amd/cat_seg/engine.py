@@ -58,6 +58,7 @@ class CatSegEngine:
         self.dt = dtype
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
+        self.split_guidance = True      # bf16: decoder conv guidance half once per image (A/B switch)
         self.device = torch.device(device)
         self._text = None
         with torch.no_grad():
@@ -180,9 +181,14 @@ class CatSegEngine:
         for i in (1, 2):
             q = f"{AGG}decoder{i}."
             ww, bb = self._convt_w(sd[q + "up.weight"], sd[q + "up.bias"])
+            cu = sd[q + "up.weight"].shape[1]
+            c0 = sd[q + "conv.double_conv.0.weight"]
             w.dec.append(_NS(
-                up_w=self._W(ww), up_b=self._F(bb), up_c=sd[q + "up.weight"].shape[1],
-                c0=self._W(self._conv_w(sd[q + "conv.double_conv.0.weight"])),
+                up_w=self._W(ww), up_b=self._F(bb), up_c=cu,
+                c0=self._W(self._conv_w(c0)),
+                # [x | g] split of the first conv (model.py:551-554): the guidance half runs
+                # once per image (fp32, catseg_conv3x3_partial), the class half per slice
+                c0_x=self._W(self._conv_w(c0[:, :cu])), c0_g=self._F(self._conv_w(c0[:, cu:])),
                 g0=(self._F(sd[q + "conv.double_conv.1.weight"]), self._F(sd[q + "conv.double_conv.1.bias"])),
                 c3=self._W(self._conv_w(sd[q + "conv.double_conv.3.weight"])),
                 g3=(self._F(sd[q + "conv.double_conv.4.weight"]), self._F(sd[q + "conv.double_conv.4.bias"])),
@@ -472,7 +478,6 @@ class CatSegEngine:
         del qkv, o, Y, gn, gqk
         # ---- guided upsampler (model.py:674-681, 540-555) ----
         src, Hc, src_gn = X, G, None
-        tile = ops.conv_tile_rows()
         for i, dec in enumerate(w.dec):
             cu = dec.up_c
             Ho = Hc * 2
@@ -493,19 +498,30 @@ class CatSegEngine:
                     ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
             cout = dec.c0.shape[0]
             groups = cout // 16
-            tiles = Ho * Ho // tile
             c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
-            st = torch.empty(S * tiles * groups * 2, device=dev, dtype=_f32)
             gd = GD[i]
-            ops.conv3x3(up, dec.c0, c1, S=S, H=Ho, W=Ho, c1=cu, src2=gd, c2=gd.shape[1], src2_div=T, stats=st)
+            if self.split_guidance and dt == torch.bfloat16 and (cu, Ho) in ((96, 48), (48, 96)) and cout in (64, 32):
+                gpart = torch.empty(B * Ho * Ho, cout, device=dev, dtype=_f32)
+                ops.conv3x3_partial(gd, dec.c0_g, gpart, B=B, H=Ho, W=Ho)
+                kw = dict(S=S, H=Ho, W=Ho, c1=cu, addend=gpart, addend_div=T)
+                wc0 = dec.c0_x
+            else:
+                kw = dict(S=S, H=Ho, W=Ho, c1=cu, src2=gd, c2=gd.shape[1], src2_div=T)
+                wc0 = dec.c0
+            tile = ops.conv3x3_stats_tile(up, wc0, **kw)
+            st = torch.empty(S * (Ho * Ho // tile) * groups * 2, device=dev, dtype=_f32)
+            ops.conv3x3(up, wc0, c1, stats=st, **kw)
             m1 = torch.empty(S * groups, device=dev, dtype=_f32)
             r1 = torch.empty_like(m1)
-            ops.groupnorm_stats(st, S, tiles, groups, tile * 16, m1, r1)
+            ops.groupnorm_stats(st, S, Ho * Ho // tile, groups, tile * 16, m1, r1)
             c2 = torch.empty_like(c1)
-            ops.conv3x3(c1, dec.c3, c2, S=S, H=Ho, W=Ho, c1=cout, gn=(m1, r1, *dec.g0, 16), stats=st)
+            kw2 = dict(S=S, H=Ho, W=Ho, c1=cout, gn=(m1, r1, *dec.g0, 16))
+            tile = ops.conv3x3_stats_tile(c1, dec.c3, **kw2)
+            st = torch.empty(S * (Ho * Ho // tile) * groups * 2, device=dev, dtype=_f32)
+            ops.conv3x3(c1, dec.c3, c2, stats=st, **kw2)
             m2 = torch.empty_like(m1)
             r2 = torch.empty_like(m1)
-            ops.groupnorm_stats(st, S, tiles, groups, tile * 16, m2, r2)
+            ops.groupnorm_stats(st, S, Ho * Ho // tile, groups, tile * 16, m2, r2)
             if i == 0:
                 src, Hc, src_gn = c2, Ho, (m2, r2, dec.g3[0], dec.g3[1], 16)
             else:

@@ -10,6 +10,8 @@ from typing import Optional
 
 import torch
 
+import ctypes as C
+
 from . import _lib as L
 from ._lib import rowmap, IDENTITY
 
@@ -202,9 +204,8 @@ def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_p
     return y
 
 
-def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0,
-            src2=None, c2=0, s2_slice_stride=0, s2_offset=0, src2_div=1,
-            bias=None, act=L.ACT_NONE, gn=None, stats=None, stats_cpg=16):
+def _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, s1_offset, src2, c2, s2_slice_stride, s2_offset,
+               src2_div, bias, act, gn, stats, stats_cpg, addend, addend_div):
     a = L.ConvArgs()
     a.src1, a.s1_slice_stride, a.s1_offset, a.c1 = (src1.data_ptr(),
                                                    s1_slice_stride if s1_slice_stride is not None else H * W * c1,
@@ -221,11 +222,46 @@ def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0
         mean, rstd, gamma, beta, cpg = gn
         a.gn_mean, a.gn_rstd, a.gn_gamma, a.gn_beta, a.gn_cpg = (mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                                                                  beta.data_ptr(), cpg)
-    a.out = out.data_ptr()
+    a.out = _p(out)
     a.stats, a.stats_cpg = _p(stats), stats_cpg
-    a.dtype = _dt(out)
+    a.dtype = _dt(out if out is not None else weight)
+    if addend is not None:
+        assert addend.dtype == torch.float32 and addend.is_contiguous()
+        a.addend, a.addend_slice_stride, a.addend_div = addend.data_ptr(), H * W * weight.shape[0], addend_div
+    return a
+
+
+def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0,
+            src2=None, c2=0, s2_slice_stride=0, s2_offset=0, src2_div=1,
+            bias=None, act=L.ACT_NONE, gn=None, stats=None, stats_cpg=16, addend=None, addend_div=1):
+    """3x3 / pad-1 conv over NHWC (catseg_conv3x3).  `stats` receives GroupNorm partials per
+    conv3x3_stats_tile(...) pixels (query it with the same arguments to size the buffer)."""
+    a = _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, s1_offset, src2, c2, s2_slice_stride, s2_offset,
+                   src2_div, bias, act, gn, stats, stats_cpg, addend, addend_div)
     with _rec("conv3x3", 2 * S * H * W * weight.shape[0] * weight.shape[1]):
         call("catseg_conv3x3", a, _stream())
+    return out
+
+
+def conv3x3_stats_tile(src1, weight, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0,
+                       src2=None, c2=0, s2_slice_stride=0, s2_offset=0, src2_div=1,
+                       bias=None, act=L.ACT_NONE, gn=None, stats_cpg=16, addend=None, addend_div=1) -> int:
+    """Pixels per GroupNorm partial of the conv kernel catseg_conv3x3 picks for these arguments."""
+    a = _conv_args(src1, weight, None, S, H, W, c1, s1_slice_stride, s1_offset, src2, c2, s2_slice_stride, s2_offset,
+                   src2_div, bias, act, gn, None, stats_cpg, addend, addend_div)
+    a.stats = 1   # any non-null: the query only inspects whether statistics are requested
+    return L.load().catseg_conv3x3_stats_tile(C.byref(a))
+
+
+def conv3x3_partial(g, weight, out, *, B, H, W):
+    """out[b][pix][co] = conv3x3 of g (NHWC [B][H][W][cin]) with fp32 weight [cout][9][cin], no bias:
+    the per-image guidance half of a conv over [x | g] (catseg_conv3x3_partial)."""
+    cout, k = weight.shape
+    cin = k // 9
+    assert g.shape[-1] == cin and out.dtype == torch.float32 and weight.dtype == torch.float32
+    with _rec("conv3x3_partial", 2 * B * H * W * cout * k):
+        call("catseg_conv3x3_partial", g.data_ptr(), B, H, W, cin, weight.data_ptr(), cout, out.data_ptr(), _dt(g),
+             _stream())
     return out
 
 

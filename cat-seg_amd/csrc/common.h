@@ -80,6 +80,22 @@ DEV float warp_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Full-wave sum on the DPP crossbar (no LDS-pipe ds_bpermute round trips): butterflies
+// inside quads and rows, then row broadcasts; lane 63 holds the total, read back uniformly.
+// Fixed order: deterministic.
+template <int CTRL, int ROWMASK = 0xF>
+DEV float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false));
+}
+DEV float wave_sum(float v) {
+  v += dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);          // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);         // row_half_mirror
+  v += dpp_mov<0x140>(v);         // row_mirror: every lane holds its row's sum
+  v += dpp_mov<0x142, 0xA>(v);    // row_bcast:15 into rows 1, 3
+  v += dpp_mov<0x143, 0xC>(v);    // row_bcast:31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
 DEV float warp_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -26,6 +26,7 @@ struct ConvP {
   const float* bias; int act;
   const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
   void* out; float* stats; int scpg;
+  const float* add; int64_t add_ss, add_div;
 };
 
 // GroupNorm + ReLU on a loaded chunk with the block's per-channel scale/shift (LDS):
@@ -190,6 +191,8 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = acc[i][j][r] + ((p.bias && n + r < p.cout) ? p.bias[n + r] : 0.f);
+        if (p.add && m < M && n + r < p.cout)
+          v += p.add[(m / HW / p.add_div) * p.add_ss + (m % HW) * p.cout + n + r];
         acc[i][j][r] = apply_act(v, p.act);
       }
       if (m < M && n < p.cout) {
@@ -272,23 +275,37 @@ int launch_conv(const ConvP& p, hipStream_t st) {
 }
 
 // ---------------- GroupNorm stats combine (Chan et al. pairwise, fixed order) ----
-__global__ void gn_stats_kernel(const float* part, int64_t S, int tiles, int groups, float tile_n,
-                                float eps, float* mean, float* rstd) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per (slice, group).  Every partial covers the same tile_n values, so the
+// combined mean is the mean of the tile means and M2 = sum M2_t + tile_n * sum (mean_t -
+// mean)^2 (exact two-pass form); lane sums reduce in a fixed butterfly order (deterministic).
+DEV double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void gn_stats_kernel(const float* part, int64_t S, int tiles, int groups,
+                                                       float tile_n, float eps, float* mean, float* rstd) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (i >= S * groups) return;
   const int64_t s = i / groups;
   const int g = (int)(i % groups);
-  double n = 0, mu = 0, m2 = 0;
-  for (int t = 0; t < tiles; ++t) {
-    const float* q = part + ((s * tiles + t) * groups + g) * 2;
-    const double nb = tile_n, mb = q[0], m2b = q[1];
-    const double nn = n + nb, d = mb - mu;
-    mu += d * nb / nn;
-    m2 += m2b + d * d * n * nb / nn;
-    n = nn;
+  const float* q = part + (s * tiles * groups + g) * 2;
+  double sm = 0;
+  for (int t = lane; t < tiles; t += 64) sm += q[(int64_t)t * groups * 2];
+  const double mu = wave_sum_f64(sm) / tiles;
+  double sd = 0, s2 = 0;
+  for (int t = lane; t < tiles; t += 64) {
+    const double d = q[(int64_t)t * groups * 2] - mu;
+    sd += d * d;
+    s2 += q[(int64_t)t * groups * 2 + 1];
   }
-  mean[i] = (float)mu;
-  rstd[i] = (float)(1.0 / sqrt(m2 / n + (double)eps));
+  const double m2 = wave_sum_f64(s2) + (double)tile_n * wave_sum_f64(sd);
+  if (lane == 0) {
+    mean[i] = (float)mu;
+    rstd[i] = (float)(1.0 / sqrt(m2 / ((double)tile_n * tiles) + (double)eps));
+  }
 }
 
 template <typename T>
@@ -469,6 +486,16 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st);   // conv_ring
 static int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = im2col only
 extern "C" void catseg_set_conv_lds(int mode) { g_conv_mode = mode; }
 
+int catseg_conv3x3_ring_tile(const CatsegConvArgs* a);   // conv_ring.hip
+extern "C" int catseg_conv3x3_stats_tile(const CatsegConvArgs* a) {
+  if (!a) return 0;
+  if (g_conv_mode >= 2) {
+    const int t = catseg_conv3x3_ring_tile(a);
+    if (t) return t;
+  }
+  return BM;   // the LDS-tile and im2col kernels emit 128-pixel partials
+}
+
 extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a && a->src1 && a->weight && a->out, "conv3x3: null pointer");
   CATSEG_CHECK(a->S > 0 && a->H > 0 && a->W > 0 && a->c1 > 0 && a->c_out > 0, "conv3x3: empty shape");
@@ -490,6 +517,7 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   p.S = a->S; p.H = a->H; p.W = a->W; p.w = a->weight; p.cout = a->c_out; p.bias = a->bias; p.act = a->act;
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.out = a->out; p.stats = a->stats; p.scpg = a->stats_cpg;
+  p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
   hipStream_t st = (hipStream_t)stream;
   if (g_conv_mode >= 2 && catseg_conv3x3_ring(a, st) == 0) return catseg_launch_status("conv3x3_ring");
   if (g_conv_mode >= 1 && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
@@ -502,7 +530,7 @@ extern "C" int catseg_groupnorm_stats(const float* partials, int64_t S, int tile
                                       float eps, float* mean, float* rstd, void* stream) {
   CATSEG_CHECK(partials && mean && rstd && S > 0 && tiles > 0 && groups > 0, "groupnorm_stats: bad args");
   const int64_t n = S * groups;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(gn_stats_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      partials, S, tiles, groups, (float)tile_count, eps, mean, rstd);
   return catseg_launch_status("groupnorm_stats");
 }

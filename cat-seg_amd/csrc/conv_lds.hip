@@ -269,6 +269,7 @@ int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st) {
   const int64_t HW = (int64_t)a->H * a->W;
   if (HW % TP != 0 || a->W < 48 || a->W > 96) return 1;
   if (a->s1_offset != 0 || a->s2_offset != 0) return 1;
+  if (a->addend) return 1;                      // (the epilogue addend is ring / im2col only)
   if (a->stats && a->stats_cpg != 16) return 1;
   if (a->gn_mean && (a->c1 % 8 != 0)) return 1;
   LdsConvP p;

@@ -10,22 +10,29 @@
 // after the chunk's barrier.  Channels [0, c1) come from the per-slice tensor
 // (GroupNorm+ReLU'd on the way in when the conv consumes relu(GN(x))), [c1, C) from the
 // per-image guidance tensor (the concat + repeat of Up.forward, model.py:551-554, never
-// materialised).  The 16-byte channel chunks of a ring pixel are XOR-swizzled by its
-// position so the 16 pixels of a fragment read hit distinct LDS bank slots.
+// materialised).  An optional fp32 per-image addend (the guidance half of the conv,
+// computed once per image by catseg_conv3x3_partial) joins in the epilogue instead.
+//
+// Ring layout: pixel-major with a pixel stride PS of C*2 rounded up to 32 (mod 64) bytes.
+// With that stride the 16 pixels x 4 k-chunks of a ds_read_b128 fragment read fall in 16
+// distinct 16-byte bank slots in every lane group (checked exhaustively for the gfx950
+// b128 lane grouping), and every fragment address is one per-(pixel tile, row) base plus a
+// compile-time offset (dx * PS + k), so the tap loop issues LDS reads with immediate
+// offsets and no per-read VALU (the XOR-swizzled image this replaces spent ~7 VALU per
+// read and still measured 25-35 % SQ_LDS_BANK_CONFLICT).
 //
 // Each wave keeps ITS slice of the weights for all 9 taps as MFMA A fragments in
 // registers for the life of the workgroup (WCO waves split COUT, WPX split the chunk's
-// pixels), so the LDS traffic is the pixel fragments only.  D = W_tap . X_tap^T; the
-// epilogue adds bias, applies the activation, emits the per-(128-pixel tile, group)
-// GroupNorm mean / M2 partials in the layout of conv.hip, and stores bf16 rows.
+// pixels), so the LDS traffic is the pixel fragments only.  D = W_tap . X_tap^T; C need
+// not be a multiple of 32: the trailing 16 channels of two taps share one K=32 step.  The
+// epilogue adds bias / addend, applies the activation, emits the per-(128-pixel tile,
+// group) GroupNorm mean / M2 partials in the layout of conv.hip, and stores bf16 rows.
 #include "common.h"
 #include "capi.h"
 
 namespace {
 
-constexpr int CH = 128;          // output pixels per chunk (= GroupNorm partial tile)
 constexpr int NT = 256;          // 4 waves
-constexpr int NR = 6;            // ring rows (a chunk spans <= 4 rows + 2 halo at W >= 48)
 
 struct RingP {
   const bf16* s1; int64_t s1_ss; int c1;
@@ -33,31 +40,39 @@ struct RingP {
   int64_t S; int H; int W; int chunks_per_band; int bands;
   const bf16* w; const float* bias; int act;
   const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
+  const float* add; int64_t add_ss; int64_t add_div;
   bf16* out; float* stats;
 };
 
 template <int C>
-DEV int ring_off(int pos, int ch) {        // element offset of 16-byte chunk ch of ring position pos
-  constexpr int CPX = C / 8;               // chunks per pixel
-  constexpr int PPB = CPX >= 16 ? 1 : 16 / CPX;   // pixels per 256-byte bank row
-  return pos * C + ((ch ^ ((pos / PPB) % CPX)) << 3);
-}
+struct RingGeom {
+  static_assert(C % 16 == 0, "channels in 16-channel steps");
+  static constexpr int PSB = (C * 2) % 64 == 32 ? C * 2 : C * 2 + 32;   // pixel stride, bytes
+  static constexpr int PS = PSB / 2;                                     // ... elements
+};
 
-template <int C, int COUT, int WPX, int WCO, int NPOS>
-__global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
+
+// OCC: waves per SIMD the register budget is sized for (2 = 256 VGPRs; 1 = 512 with AGPRs,
+// for the 96-channel variant whose 108 weight VGPRs leave no room at 2)
+// NR: ring rows = rows a chunk can span + 2 halo rows (CH = 128: 4 + 2 at W >= 48, 3 + 2 at
+// W >= 64; CH = 64: 3 + 2 at W >= 48)
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD>
+__global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   constexpr int CPX = C / 8;
+  constexpr int PS = RingGeom<C>::PS;
   constexpr int MAXPF = (NPOS * CPX + NT - 1) / NT;     // prefetch chunks per thread
   constexpr int PXW = CH / WPX, FM = PXW / 16;          // pixels per wave, their 16-px tiles
   constexpr int COW = COUT / WCO, FN = COW / 16;        // output channels per wave
-  constexpr int KC = C / 32;                            // MFMA k-steps per tap
+  constexpr int KC = C / 32;                            // full MFMA k-steps per tap
+  constexpr bool KT = (C % 32) == 16;                   // trailing 16 channels per tap
+  constexpr int NTP = KT ? 5 : 0;                       // tap pairs (0,1) (2,3) (4,5) (6,7) (8,-)
   static_assert(WPX * WCO == 4 && FM >= 1 && FN >= 1, "wave grid");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* ring = reinterpret_cast<bf16*>(smem);
   const int W = p.W, WP = W + 2, H = p.H;
-  const int ring_elems = NR * WP * C;
+  const int ring_elems = NR * WP * PS;
   float* gsc = reinterpret_cast<float*>(smem + (size_t)ring_elems * 2);   // [C]
   float* gsh = gsc + C;                                                    // [C]
-  float* red = gsh + C;                                                    // [4][4]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
@@ -71,17 +86,29 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
   if (c_begin >= c_end) return;
 
   // ---- weights of this wave's output channels, all taps, in registers ----
-  s16x8 wf[9][KC][FN];
+  // The trailing 16 channels of two taps share one K=32 step: lanes q < 2 carry tap 2p's
+  // channels KC*32 + 8q.., lanes q >= 2 tap 2p+1's (zero weights past tap 8) -- the k order
+  // inside an MFMA step is free as long as A and B agree.
+  s16x8 wf[9][KC > 0 ? KC : 1][FN];
+  s16x8 wt[NTP > 0 ? NTP : 1][FN];
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+  for (int i = 0; i < FN; ++i) {
+    const int n = wco * COW + 16 * i + r16;
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int n = wco * COW + 16 * i + r16;
+      for (int kc = 0; kc < KC; ++kc) {
         uint4 u = ld16(p.w + ((int64_t)n * 9 + tap) * C + kc * 32 + 8 * q);
         wf[tap][kc][i] = *reinterpret_cast<s16x8*>(&u);
       }
+#pragma unroll
+    for (int tp = 0; tp < NTP; ++tp) {
+      const int tap = 2 * tp + (q >> 1);
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (tap < 9) u = ld16(p.w + ((int64_t)n * 9 + tap) * C + KC * 32 + 8 * (q & 1));
+      wt[tp][i] = *reinterpret_cast<s16x8*>(&u);
+    }
+  }
   if (p.gmean) {
     const int ngroups = p.c1 / p.gcpg;
     for (int c = tid; c < p.c1; c += NT) {
@@ -108,7 +135,7 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
       for (int k = 0; k < 8; ++k) e[k] = f2bf(fmaxf(fmaf(bf2f(e[k]), gsc[ci + k], gsh[ci + k]), 0.f));
     }
     const int pos = ((y + 1) % NR) * WP + xc;
-    st16(&ring[ring_off<C>(pos, ch)], u);
+    st16(&ring[pos * PS + ch * 8], u);
   };
   const int row_items = WP * CPX;
 
@@ -158,24 +185,38 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
                   ? gload(loaded_to + 1 + (pf_code[k] >> 16), (pf_code[k] >> 4) & 0xfff, pf_code[k] & 15)
                   : make_uint4(0, 0, 0, 0);
 
-    // ---- MFMAs: 9 taps x KC k-steps over the ring ----
+    // the per-image addend of this chunk (L2-resident), in flight during the MFMAs
+    float4 ad[FN][FM];
+    if constexpr (ADD) {
+      const float* addb = p.add ? p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT + wco * COW
+                                : nullptr;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          ad[i][j] = addb ? *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT + 16 * i + 4 * q)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // ---- MFMAs: 9 taps x (KC + tail) k-steps over the ring ----
     int prow[FM], pcol[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int pp = p0 + wpx * PXW + 16 * j + r16;
       prow[j] = pp / W;
-      pcol[j] = pp - prow[j] * W + 1;        // ring column of the centre tap
+      pcol[j] = pp - prow[j] * W;            // ring column of the left tap (x - 1 + 1)
     }
     f32x4 acc[FN][FM];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int rb[3][FM];                            // pixel (row y+dy-1, column x-1) of each tile row
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) rb[dy][j] = (((prow[j] + dy) % NR) * WP + pcol[j]) * PS;
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
-      int rbase[FM];
-#pragma unroll
-      for (int j = 0; j < FM; ++j) rbase[j] = ((prow[j] + dy) % NR) * WP + pcol[j] - 1;   // slot of row y+dy-1
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int tap = dy * 3 + dx;
@@ -183,8 +224,7 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
         for (int kc = 0; kc < KC; ++kc) {
           s16x8 xf[FM];
 #pragma unroll
-          for (int j = 0; j < FM; ++j)
-            xf[j] = *reinterpret_cast<const s16x8*>(&ring[ring_off<C>(rbase[j] + dx, kc * 4 + q)]);
+          for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(ring + rb[dy][j] + 8 * q + dx * PS + kc * 32);
 #pragma unroll
           for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -192,22 +232,41 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
         }
       }
     }
+#pragma unroll
+    for (int tp = 0; tp < NTP; ++tp) {
+      // lanes q < 2: tap 2tp, q >= 2: tap 2tp+1 (tap 9 reads tap 8's pixels against zero weights)
+      const int ta = 2 * tp, tb = 2 * tp + 1 < 9 ? 2 * tp + 1 : 8;
+      const bool hi = q >= 2;
+      s16x8 xf[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int a0 = rb[ta / 3][j] + (ta % 3) * PS, b0 = rb[tb / 3][j] + (tb % 3) * PS;
+        xf[j] = *reinterpret_cast<const s16x8*>(ring + (hi ? b0 : a0) + KC * 32 + 8 * (q & 1));
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wt[tp][i], xf[j], acc[i][j]);
+    }
 
-    // ---- epilogue: bias / act, GroupNorm partials, bf16 stores ----
+    // ---- epilogue: bias / addend / act, GroupNorm partials, bf16 stores ----
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int j = 0; j < FM; ++j)
+      for (int j = 0; j < FM; ++j) {
+        float adv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (ADD) { adv[0] = ad[i][j].x; adv[1] = ad[i][j].y; adv[2] = ad[i][j].z; adv[3] = ad[i][j].w; }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r];
+          float v = acc[i][j][r] + adv[r];
           if (p.bias) v += p.bias[wco * COW + 16 * i + 4 * q + r];
           acc[i][j][r] = apply_act(v, p.act);
         }
+      }
     if (p.stats) {
-      // group of 16 channels = one n-tile; reduce the wave's PXW pixels, then the WPX
-      // waves that share the wave's channel range
-      float gs[FN];
+      // GroupNorm partials per (wave pixel block = PXW pixels, group of 16 channels = one
+      // n-tile): mean and M2 of the wave's own accumulators, no cross-wave reduction
+      const int ntiles = HW / PXW, tile = c * WPX + wpx;
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         float a = 0.f;
@@ -215,45 +274,19 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
         for (int j = 0; j < FM; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) a += acc[i][j][r];
-        gs[i] = warp_sum(a);
-      }
-      if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < FN; ++i) red[wave * 4 + i] = gs[i];
-      __syncthreads();
-      float gm[FN];
-#pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < WPX; ++w2) a += red[(wco * WPX + w2) * 4 + i];
-        gm[i] = a * (1.f / (CH * 16));
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        float a = 0.f;
+        const float gm = wave_sum(a) * (1.f / (PXW * 16));
+        float m2 = 0.f;
 #pragma unroll
         for (int j = 0; j < FM; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) { const float d = acc[i][j][r] - gm[i]; a += d * d; }
-        gs[i] = warp_sum(a);
-      }
-      if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < FN; ++i) red[wave * 4 + i] = gs[i];
-      __syncthreads();
-      if (wpx == 0 && lane < FN) {
-        float m2 = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < WPX; ++w2) m2 += red[(wco * WPX + w2) * 4 + lane];
-        float gml = gm[0];
-#pragma unroll
-        for (int i = 1; i < FN; ++i) if (lane == i) gml = gm[i];
-        const int grp = (wco * COW) / 16 + lane;
-        float* o = p.stats + (((int64_t)s * nchunks + c) * (COUT / 16) + grp) * 2;
-        o[0] = gml;
-        o[1] = m2;
+          for (int r = 0; r < 4; ++r) { const float d = acc[i][j][r] - gm; m2 += d * d; }
+        m2 = wave_sum(m2);
+        if (lane == 0) {
+          const int grp = (wco * COW) / 16 + i;
+          float* o = p.stats + (((int64_t)s * ntiles + tile) * (COUT / 16) + grp) * 2;
+          o[0] = gm;
+          o[1] = m2;
+        }
       }
     }
     bf16* ob = p.out + ((int64_t)s * HW + p0 + wpx * PXW) * COUT + wco * COW;
@@ -276,52 +309,150 @@ __global__ __launch_bounds__(NT, 2) void conv_ring_kernel(RingP p) {
 }
 
 template <int C>
-size_t ring_lds(int W) { return (size_t)NR * (W + 2) * C * 2 + (2 * C + 16) * 4; }
+size_t ring_lds(int W, int NR) { return (size_t)NR * (W + 2) * RingGeom<C>::PS * 2 + 2 * C * 4; }
 
-// NPOS bounds the ring positions one chunk adds: ceil(128 / W) rows of W + 2 columns,
-// <= 156 for 48 <= W <= 50 and <= 198 for any 48 <= W <= 96.
-template <int C, int COUT, int WPX, int WCO, int NPOS>
-int launch_ring(const RingP& p0, hipStream_t st) {
+// NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
+// <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
+// adds <= 2 rows (104).
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD>
+int launch_ring_t(const RingP& p0, hipStream_t st) {
   RingP p = p0;
   const int nchunks = p.H * p.W / CH;
-  // bands of ~24 chunks (a band re-primes its ring once), at least 2 workgroups per CU
-  int bands = (nchunks + 23) / 24;
+  // bands of ~3072 pixels (a band re-primes its ring once), at least 2 workgroups per CU
+  const int per_band = 3072 / CH;
+  int bands = (nchunks + per_band - 1) / per_band;
   while (p.S * bands < 2048 && bands * 4 <= nchunks) bands *= 2;
   p.bands = bands;
   p.chunks_per_band = (nchunks + bands - 1) / bands;
-  const size_t sh = ring_lds<C>(p.W);
+  const size_t sh = ring_lds<C>(p.W, NR);
   static size_t configured = 0;
   if (sh > configured) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS>), dim3((unsigned)(p.S * bands)), dim3(NT), sh, st, p);
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD>), dim3((unsigned)(p.S * bands)), dim3(NT), sh, st, p);
   return 0;
+}
+
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH = 128, int OCC = 2, int NR = 6>
+int launch_ring(const RingP& p0, hipStream_t st) {
+  if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true>(p0, st);
+  return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false>(p0, st);
+}
+
+// ---- per-image partial conv (fp32 out): the guidance half of a conv over [x | g] ----
+// out[b][pix][co] = sum_{tap, ci} w[co][tap][ci] * g[b][pix + tap][ci]  (zero padded),
+// one thread per (pixel, 4 output channels); weights staged in LDS as [tap][ci][co].
+template <typename T>
+__global__ __launch_bounds__(256) void conv_partial_kernel(const T* __restrict__ g, int64_t B, int H, int W, int cin,
+                                                           const float* __restrict__ w, int cout, float* out) {
+  extern __shared__ float sw[];        // [9][cin][cout]
+  for (int i = threadIdx.x; i < 9 * cin * cout; i += blockDim.x) {
+    const int co = i % cout, ci = (i / cout) % cin, tap = i / (cout * cin);
+    sw[i] = w[((int64_t)co * 9 + tap) * cin + ci];
+  }
+  __syncthreads();
+  const int groups = cout / 4;
+  const int64_t total = B * H * W * groups;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(idx % groups);
+    const int64_t pixg = idx / groups;
+    const int64_t b = pixg / (H * W);
+    const int pix = (int)(pixg % (H * W));
+    const int y = pix / W, x = pix % W;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+      if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+      const T* src = g + ((b * H + yy) * W + xx) * cin;
+      const float* wt = sw + tap * cin * cout + cg * 4;
+      for (int ci = 0; ci < cin; ++ci) {
+        const float v = to_f<T>(src[ci]);
+        const float4 ww = *reinterpret_cast<const float4*>(wt + ci * cout);
+        a0 += v * ww.x; a1 += v * ww.y; a2 += v * ww.z; a3 += v * ww.w;
+      }
+    }
+    *reinterpret_cast<float4*>(out + pixg * cout + cg * 4) = make_float4(a0, a1, a2, a3);
+  }
 }
 
 }  // namespace
 
-// bf16 fast path of catseg_conv3x3 (conv.hip): 0 = launched, 1 = not applicable.
-int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
-  if (a->dtype != CATSEG_BF16) return 1;
+// Variant table of the ring kernel: 0 = not applicable, else an id; *tile = pixels per
+// GroupNorm partial (the wave pixel block PXW = CH / WPX).
+static int ring_variant(const CatsegConvArgs* a, int* tile) {
+  if (a->dtype != CATSEG_BF16) return 0;
   const int C = a->c1 + a->c2;
   const int64_t HW = (int64_t)a->H * a->W;
-  if (HW % CH != 0 || a->W < 48 || a->W > 96) return 1;
-  if (a->s1_offset != 0 || a->s2_offset != 0) return 1;
-  if (a->stats && a->stats_cpg != 16) return 1;
-  if (a->gn_mean && (a->c1 % 8 != 0)) return 1;
+  if (HW % 128 != 0 || a->W < 48 || a->W > 96) return 0;
+  if (a->s1_offset != 0 || a->s2_offset != 0) return 0;
+  if (a->stats && a->stats_cpg != 16) return 0;
+  if (a->gn_mean && (a->c1 % 8 != 0)) return 0;
+  if (a->addend && ((uintptr_t)a->addend % 16 != 0 || a->addend_slice_stride % 4 != 0)) return 0;
+  const bool narrow = a->W < 64;      // CH = 128 spans <= 3 rows only from W >= 64 on
+  int v = 0, t = 0;
+  if (C == 64 && a->c_out == 32) { v = narrow ? 1 : 2; t = 32; }
+  else if (C == 48 && a->c_out == 32) { v = narrow ? 3 : 4; t = narrow ? 32 : 64; }
+  else if (C == 32 && a->c_out == 32) { v = narrow ? 5 : 6; t = 32; }
+  else if (C == 64 && a->c_out == 64 && a->W <= 50) { v = 7; t = 128; }
+  else if (C == 96 && a->c_out == 64 && a->W <= 50) { v = 8; t = 64; }
+  if (tile) *tile = t;
+  return v;
+}
+
+// Pixels per GroupNorm partial ("tile") of the conv catseg_conv3x3 would run for these args.
+int catseg_conv3x3_ring_tile(const CatsegConvArgs* a) {
+  int t = 0;
+  return ring_variant(a, &t) ? t : 0;
+}
+
+// bf16 fast path of catseg_conv3x3 (conv.hip): 0 = launched, 1 = not applicable.
+int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
+  const int v = ring_variant(a, nullptr);
+  if (!v) return 1;
   RingP p;
   p.s1 = (const bf16*)a->src1; p.s1_ss = a->s1_slice_stride; p.c1 = a->c1;
   p.s2 = (const bf16*)a->src2; p.s2_ss = a->s2_slice_stride; p.c2 = a->c2; p.s2_div = a->src2_div > 0 ? a->src2_div : 1;
   p.S = a->S; p.H = a->H; p.W = a->W;
   p.w = (const bf16*)a->weight; p.bias = a->bias; p.act = a->act;
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
+  p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
   p.out = (bf16*)a->out; p.stats = a->stats;
-  // weights in registers: 9 taps x C/32 x COUT/WCO/16 fragments (<= 36 = 144 VGPRs)
-  const bool narrow = a->W <= 50;
-  if (C == 64 && a->c_out == 32) return narrow ? launch_ring<64, 32, 4, 1, 156>(p, st) : launch_ring<64, 32, 4, 1, 198>(p, st);
-  if (C == 32 && a->c_out == 32) return narrow ? launch_ring<32, 32, 4, 1, 156>(p, st) : launch_ring<32, 32, 4, 1, 198>(p, st);
-  if (C == 64 && a->c_out == 64 && narrow) return launch_ring<64, 64, 1, 4, 156>(p, st);
-  return 1;
+  // weights in registers: 9 taps x C/16 half-steps x COUT/WCO/16 fragments
+  switch (v) {
+    case 1: return launch_ring<64, 32, 4, 1, 156>(p, st);
+    case 2: return launch_ring<64, 32, 4, 1, 198, 128, 2, 5>(p, st);
+    case 3: return launch_ring<48, 32, 4, 1, 156>(p, st);
+    case 4: return launch_ring<48, 32, 2, 2, 198, 128, 2, 5>(p, st);
+    case 5: return launch_ring<32, 32, 4, 1, 156>(p, st);
+    case 6: return launch_ring<32, 32, 4, 1, 198, 128, 2, 5>(p, st);
+    case 7: return launch_ring<64, 64, 1, 4, 156>(p, st);
+    case 8: return launch_ring<96, 64, 1, 4, 104, 64, 2, 5>(p, st);
+    default: return 1;
+  }
+}
+
+extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, int cin, const float* weight, int cout,
+                                      float* out, int dtype, void* stream) {
+  CATSEG_CHECK(g && weight && out && B > 0 && H > 0 && W > 0 && cin > 0, "conv3x3_partial: bad args");
+  CATSEG_CHECK(cout % 4 == 0 && (size_t)9 * cin * cout * 4 <= 128 * 1024, "conv3x3_partial: cout % 4, weights <= 128 KB");
+  const size_t sh = (size_t)9 * cin * cout * 4;
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_kernel<bf16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_kernel<float>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    configured = true;
+  }
+  const int64_t total = B * H * W * (cout / 4);
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(conv_partial_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B, H,
+                       W, cin, weight, cout, out);
+  else
+    hipLaunchKernelGGL(conv_partial_kernel<float>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const float*)g, B,
+                       H, W, cin, weight, cout, out);
+  return catseg_launch_status("conv3x3_partial");
 }

@@ -193,11 +193,26 @@ typedef struct {
   const float* gn_mean; const float* gn_rstd; const float* gn_gamma; const float* gn_beta; int gn_cpg;
   void* out; float* stats; int stats_cpg;
   int dtype;
+  /* optional fp32 addend joined before the activation / statistics (the guidance half
+   * of the conv computed once per image): addend[(s / addend_div) * addend_slice_stride
+   * + pixel * c_out + co] */
+  const float* addend; int64_t addend_slice_stride; int64_t addend_div;
 } CatsegConvArgs;
 int catseg_conv3x3(const CatsegConvArgs* args, void* stream);
-/* Rows per conv tile (the `tile` axis of the stats buffer): stats is
- * [S][H*W/catseg_conv_tile_rows()][c_out/stats_cpg][2]. */
+
+/* catseg_conv3x3_partial — the conv over a channel subset, fp32 out, once per image:
+ * out[b][pix][co] = sum_{tap, ci} weight[co][tap][ci] * g[b][pix + tap][ci] (zero pad, no
+ * bias).  With g = the decoder guidance (model.py:551-554, repeated over classes by the
+ * reference) this is the class-independent half of conv(concat[x, g]); it enters the
+ * per-class conv over x as its `addend`.  g: NHWC [B][H][W][cin]; weight fp32 [cout][9][cin]. */
+int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, int cin, const float* weight, int cout,
+                           float* out, int dtype, void* stream);
+/* Rows per conv tile of the im2col / LDS-tile kernels (128). */
 int catseg_conv_tile_rows(void);
+/* Pixels per GroupNorm partial ("tile") of the kernel catseg_conv3x3 picks for `args`:
+ * stats is [S][H*W/tile][c_out/stats_cpg][2] (the row-ring kernel emits one partial per
+ * wave pixel block, 32-128 pixels; the others 128). */
+int catseg_conv3x3_stats_tile(const CatsegConvArgs* args);
 
 /* catseg_groupnorm_stats — combine the conv partials into mean / rstd per
  * (slice, group) (nn.GroupNorm statistics, model.py:529,532; eps 1e-5). */

@@ -311,6 +311,55 @@ def test_conv3x3_dual_source_gn(dt):
             close(logits[bi, cls[bi, t]], rh[bi, t], atol=1e-4 if dt == torch.float32 else 5e-2, what="head")
 
 
+@pytest.mark.parametrize("c1,c2,co,H", [(96, 32, 64, 48), (48, 16, 32, 96), (64, 0, 64, 48), (32, 0, 32, 96)])
+def test_conv3x3_ring_guidance_split(c1, c2, co, H):
+    """The decoder convs on the ring kernel (bf16): conv over [x | g] (g per image, repeated over
+    T; model.py:551-554) computed as conv(x) + the per-image fp32 partial conv of g
+    (catseg_conv3x3_partial) joined as the epilogue addend, vs fp64 and vs the unsplit path;
+    GroupNorm partial statistics included."""
+    B, T, W = 2, 3, H
+    S = B * T
+    dt = torch.bfloat16
+    x1 = rnd(S, c1, H, W, seed=71)
+    x2 = rnd(B, max(c2, 1), H, W, seed=72)[:, :c2]
+    w = rnd(co, c1 + c2, 3, 3, seed=73) / 8
+    xin = torch.cat([x1, x2.repeat_interleave(T, 0)], 1) if c2 else x1
+    ref = F.conv2d(xin.to(dt).double(), w.to(dt).double(), padding=1)
+    a1 = x1.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    out = torch.empty(S * H * W, co, device=dev, dtype=dt)
+    if c2:
+        a2 = x2.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+        wx = w[:, :c1].permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+        wg = w[:, c1:].to(dt).float().permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev)
+        part = torch.empty(B * H * W, co, device=dev)
+        ops.conv3x3_partial(a2, wg, part, B=B, H=H, W=W)
+        refp = F.conv2d(x2.to(dt).double(), w[:, c1:].to(dt).double(), padding=1)
+        close(part.reshape(B, H, W, co).permute(0, 3, 1, 2), refp, atol=1e-4, what="partial conv")
+        kw, wc = dict(S=S, H=H, W=W, c1=c1, addend=part, addend_div=T), wx
+    else:
+        kw, wc = dict(S=S, H=H, W=W, c1=c1), w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+    tile = ops.conv3x3_stats_tile(a1, wc, **kw)
+    tiles = H * W // tile
+    st = torch.empty(S * tiles * (co // 16) * 2, device=dev)
+    ops.conv3x3(a1, wc, out, stats=st, **kw)
+    got = out.reshape(S, H, W, co).permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs() - 2.0 ** -8 * ref.abs()
+    assert err.max().item() <= 1e-5, err.max().item()
+    mean = torch.empty(S * (co // 16), device=dev)
+    rstd = torch.empty_like(mean)
+    ops.groupnorm_stats(st, S, tiles, co // 16, tile * 16, mean, rstd)
+    g = ref.reshape(S, co // 16, -1)
+    close(mean, g.mean(-1).reshape(-1), atol=1e-4, what="gn mean")
+    close(rstd, (1 / torch.sqrt(g.var(-1, unbiased=False) + 1e-5)).reshape(-1), atol=0, rtol=2e-3, what="gn rstd")
+    if c2:
+        # the unsplit path (guidance channels read per class) on the same inputs
+        out2 = torch.empty_like(out)
+        wk = w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+        ops.conv3x3(a1, wk, out2, S=S, H=H, W=W, c1=c1, src2=a2, c2=c2, src2_div=T)
+        e2 = (out.float() - out2.float()).abs()
+        assert e2.max().item() < 2e-2, e2.max().item()
+
+
 # ----------------------------------------------------------------------------- small ops
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_corr_embed_topk(dt):
@@ -479,15 +528,18 @@ def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
     L.load().catseg_set_conv_lds(lds)
     try:
         out = torch.empty(S * H * W_, co, device=dev, dtype=dt)
-        tiles = H * W_ // ops.conv_tile_rows()
+        xs = x1.reshape(-1, c1).contiguous().to(dev, dt)
+        wk = w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+        kw = dict(S=S, H=H, W=W_, c1=c1, src2=x2.reshape(-1, c2).contiguous().to(dev, dt) if c2 else None, c2=c2,
+                  src2_div=T, gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16) if gn else None)
+        tile = ops.conv3x3_stats_tile(xs, wk, **kw)
+        tiles = H * W_ // tile
         st = torch.empty(S * tiles * (co // 16) * 2, device=dev)
-        ops.conv3x3(x1.reshape(-1, c1).contiguous().to(dev, dt), w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt),
-                    out, S=S, H=H, W=W_, c1=c1, src2=x2.reshape(-1, c2).contiguous().to(dev, dt) if c2 else None, c2=c2,
-                    src2_div=T, stats=st, gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16) if gn else None)
+        ops.conv3x3(xs, wk, out, stats=st, **kw)
         close(out.reshape(S, H, W_, co).permute(0, 3, 1, 2), ref, atol=3e-2, rtol=1e-2, what="conv decoder")
         m_ = torch.empty(S * (co // 16), device=dev)
         r_ = torch.empty_like(m_)
-        ops.groupnorm_stats(st, S, tiles, co // 16, ops.conv_tile_rows() * 16, m_, r_)
+        ops.groupnorm_stats(st, S, tiles, co // 16, tile * 16, m_, r_)
         gref = ref.reshape(S, co // 16, 16, H * W_)
         close(m_, gref.mean((-1, -2)).reshape(-1), atol=2e-3, what="gn mean")
     finally:
