@@ -116,6 +116,7 @@ class ConvArgs(C.Structure):
         ("out", vp), ("stats", vp), ("stats_cpg", i32),
         ("dtype", i32),
         ("addend", vp), ("addend_slice_stride", i64), ("addend_div", i64),
+        ("workspace", vp), ("workspace_bytes", i64),
     ]
 
 
@@ -132,6 +133,7 @@ _SIGS = {
     "catseg_conv3x3_partial": [vp, i64, i32, i32, i32, vp, i32, vp, i32, vp],
     "catseg_conv_tile_rows": [],
     "catseg_conv3x3_stats_tile": [C.POINTER(ConvArgs)],
+    "catseg_conv3x3_workspace": [C.POINTER(ConvArgs)],
     "catseg_groupnorm_stats": [vp, i64, i32, i32, i64, f32, vp, vp, vp],
     "catseg_groupnorm_relu": [vp, vp, i64, i64, i32, i32, vp, vp, vp, vp, i32, vp],
     "catseg_conv3x3_head": [vp, i64, i32, i32, i32, i32, vp, f32, vp, i32, vp, i32, vp],
@@ -182,7 +184,8 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = (C.c_char_p if name == "catseg_last_error" else
-                      None if name.startswith("catseg_set_") else C.c_int)
+                      None if name.startswith("catseg_set_") else
+                      C.c_int64 if name == "catseg_conv3x3_workspace" else C.c_int)
     _lib = lib
     return lib
 

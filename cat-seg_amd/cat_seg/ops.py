@@ -238,6 +238,11 @@ def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0
     conv3x3_stats_tile(...) pixels (query it with the same arguments to size the buffer)."""
     a = _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, s1_offset, src2, c2, s2_slice_stride, s2_offset,
                    src2_div, bias, act, gn, stats, stats_cpg, addend, addend_div)
+    ws_bytes = L.load().catseg_conv3x3_workspace(C.byref(a))
+    ws = None
+    if ws_bytes > 0:   # split-K scratch of small-grid convs (caching allocator; graph-capturable)
+        ws = torch.empty(ws_bytes // 4, device=out.device, dtype=torch.float32)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), ws_bytes
     with _rec("conv3x3", 2 * S * H * W * weight.shape[0] * weight.shape[1]):
         call("catseg_conv3x3", a, _stream())
     return out

@@ -27,6 +27,7 @@ struct ConvP {
   const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
   void* out; float* stats; int scpg;
   const float* add; int64_t add_ss, add_div;
+  float* ws; int ksplit;       // split-K: fp32 partials [ksplit][M][cout], reduced by conv_splitk_reduce
 };
 
 // GroupNorm + ReLU on a loaded chunk with the block's per-channel scale/shift (LDS):
@@ -129,7 +130,10 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int ktiles = (int)((K + BK - 1) / BK);
+  const int ktiles_all = (int)((K + BK - 1) / BK);
+  const int kper = (ktiles_all + p.ksplit - 1) / p.ksplit;
+  const int kt0 = blockIdx.z * kper;
+  const int ktiles = max(0, min(ktiles_all - kt0, kper));
   if (p.gmean) {
     const int64_t s0 = (m0 < M ? m0 : 0) / HW;
     const int ngroups = p.c1 / p.gcpg;
@@ -141,12 +145,12 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
     }
     __syncthreads();
   }
-  gload(0);
+  gload((int64_t)kt0 * BK);
   sstore(0);
   __syncthreads();
   for (int kt = 0; kt < ktiles; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BK);
+    if (kt + 1 < ktiles) gload((int64_t)(kt0 + kt + 1) * BK);
     const T* As = sA[buf];
     const T* Ws = sW[buf];
     if constexpr (sizeof(T) == 2) {
@@ -181,6 +185,22 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
 
   // ---- epilogue: bias, act, store, GroupNorm partials ----
   const int col = lane & 15, rq = (lane >> 4) * 4;
+  if (p.ksplit > 1) {          // raw fp32 partial of this K slice (bias / act in the reduce)
+    float* Wp = p.ws + (int64_t)blockIdx.z * M * p.cout;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn + 16 * i + rq;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int64_t m = m0 + wm + 16 * j + col;
+        if (m < M && n < p.cout) {
+          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          store4<float>(Wp + m * p.cout + n, v);
+        }
+      }
+    }
+    return;
+  }
   T* O = reinterpret_cast<T*>(p.out);
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
@@ -260,16 +280,59 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
   }
 }
 
+// split-K factor for the im2col kernel: grids far below the CU count (the per-image guidance
+// projections: 36-144 tiles over K = 9 x 256..768) split K so >= ~512 workgroups run;
+// never with GroupNorm statistics (partials are per output tile).
+int conv_ksplit(const CatsegConvArgs* a) {
+  if (a->stats) return 1;
+  const int64_t M = a->S * (int64_t)a->H * a->W;
+  const int64_t tiles = ((M + BM - 1) / BM) * ((a->c_out + 127) / 128);
+  const int64_t ktiles = (9LL * (a->c1 + a->c2) + BK - 1) / BK;
+  int ks = 1;
+  while (tiles * ks < 512 && ktiles / (2 * ks) >= 8 && ks < 16) ks *= 2;
+  return ks;
+}
+
+template <typename T>
+__global__ void conv_splitk_reduce(const float* ws, int ksplit, int64_t total4, int cout, const float* bias, int act,
+                                   const float* add, int64_t add_ss, int64_t add_div, int64_t HW, T* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    float4 a = *reinterpret_cast<const float4*>(ws + e);
+    for (int z = 1; z < ksplit; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(ws + (int64_t)z * total4 * 4 + e);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    const int n = (int)(e % cout);
+    const int64_t m = e / cout;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (bias) v[r] += bias[n + r];
+      if (add) v[r] += add[(m / HW / add_div) * add_ss + (m % HW) * cout + n + r];
+      v[r] = apply_act(v[r], act);
+    }
+    store4<T>(out + e, v);
+  }
+}
+
 template <typename T>
 int launch_conv(const ConvP& p, hipStream_t st) {
   const int64_t M = p.S * p.H * p.W;
   const unsigned gx = (unsigned)((M + BM - 1) / BM);
+  const unsigned gz = (unsigned)p.ksplit;
   if (p.cout <= 32) {
-    hipLaunchKernelGGL((conv3x3_kernel<T, 32>), dim3(gx, 1), dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((conv3x3_kernel<T, 32>), dim3(gx, 1, gz), dim3(NT), 0, st, p);
   } else if (p.cout <= 64) {
-    hipLaunchKernelGGL((conv3x3_kernel<T, 64>), dim3(gx, 1), dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((conv3x3_kernel<T, 64>), dim3(gx, 1, gz), dim3(NT), 0, st, p);
   } else {
-    hipLaunchKernelGGL((conv3x3_kernel<T, 128>), dim3(gx, (unsigned)((p.cout + 127) / 128)), dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((conv3x3_kernel<T, 128>), dim3(gx, (unsigned)((p.cout + 127) / 128), gz), dim3(NT), 0, st, p);
+  }
+  if (p.ksplit > 1) {
+    const int64_t total4 = M * p.cout / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>((total4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(conv_splitk_reduce<T>, dim3(grid), dim3(256), 0, st, p.ws, p.ksplit, total4, p.cout, p.bias,
+                       p.act, p.add, p.add_ss, p.add_div, (int64_t)p.H * p.W, reinterpret_cast<T*>(p.out));
   }
   return 0;
 }
@@ -487,6 +550,14 @@ static int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = i
 extern "C" void catseg_set_conv_lds(int mode) { g_conv_mode = mode; }
 
 int catseg_conv3x3_ring_tile(const CatsegConvArgs* a);   // conv_ring.hip
+// fp32 workspace the im2col kernel would use for split-K on these args (0 = none needed)
+extern "C" int64_t catseg_conv3x3_workspace(const CatsegConvArgs* a) {
+  if (!a) return 0;
+  if (g_conv_mode >= 2 && catseg_conv3x3_ring_tile(a)) return 0;
+  const int ks = conv_ksplit(a);
+  return ks > 1 ? (int64_t)ks * a->S * a->H * a->W * a->c_out * 4 : 0;
+}
+
 extern "C" int catseg_conv3x3_stats_tile(const CatsegConvArgs* a) {
   if (!a) return 0;
   if (g_conv_mode >= 2) {
@@ -518,9 +589,16 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.out = a->out; p.stats = a->stats; p.scpg = a->stats_cpg;
   p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
+  p.ksplit = 1; p.ws = nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (g_conv_mode >= 2 && catseg_conv3x3_ring(a, st) == 0) return catseg_launch_status("conv3x3_ring");
   if (g_conv_mode >= 1 && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
+  const int ks = conv_ksplit(a);
+  const int64_t Mtot = a->S * (int64_t)a->H * a->W;
+  if (ks > 1 && a->workspace && a->workspace_bytes >= (int64_t)ks * Mtot * a->c_out * 4 && a->c_out % 4 == 0) {
+    p.ksplit = ks;
+    p.ws = (float*)a->workspace;
+  }
   if (a->dtype == CATSEG_BF16) launch_conv<bf16>(p, st);
   else launch_conv<float>(p, st);
   return catseg_launch_status("conv3x3");

@@ -197,6 +197,9 @@ typedef struct {
    * of the conv computed once per image): addend[(s / addend_div) * addend_slice_stride
    * + pixel * c_out + co] */
   const float* addend; int64_t addend_slice_stride; int64_t addend_div;
+  /* optional caller-allocated scratch (catseg_conv3x3_workspace bytes) for split-K of
+   * small-grid convs; without it the conv runs unsplit */
+  void* workspace; int64_t workspace_bytes;
 } CatsegConvArgs;
 int catseg_conv3x3(const CatsegConvArgs* args, void* stream);
 
@@ -213,6 +216,8 @@ int catseg_conv_tile_rows(void);
  * stats is [S][H*W/tile][c_out/stats_cpg][2] (the row-ring kernel emits one partial per
  * wave pixel block, 32-128 pixels; the others 128). */
 int catseg_conv3x3_stats_tile(const CatsegConvArgs* args);
+/* Bytes of split-K scratch catseg_conv3x3 would use for `args` (0 = none). */
+int64_t catseg_conv3x3_workspace(const CatsegConvArgs* args);
 
 /* catseg_groupnorm_stats — combine the conv partials into mean / rstd per
  * (slice, group) (nn.GroupNorm statistics, model.py:529,532; eps 1e-5). */

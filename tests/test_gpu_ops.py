@@ -311,6 +311,28 @@ def test_conv3x3_dual_source_gn(dt):
             close(logits[bi, cls[bi, t]], rh[bi, t], atol=1e-4 if dt == torch.float32 else 5e-2, what="head")
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("S,H,c1,co", [(2, 24, 768, 128), (3, 48, 256, 32), (1, 24, 512, 128)])
+def test_conv3x3_splitk_guidance_projection(dt, S, H, c1, co):
+    """The per-image guidance projections (model.py:616-630: conv3x3 + bias + ReLU on res3/4/5):
+    small grids over long K run split-K (fp32 partials + reduce) when the op provides the
+    workspace; equal to fp64 conv2d."""
+    lib = L.load()
+    x = rnd(S, c1, H, H, seed=81)
+    w = rnd(co, c1, 3, 3, seed=82) / math.sqrt(9 * c1)
+    b = rnd(co, seed=83) * 0.1
+    ref = F.relu(F.conv2d(x.to(dt).double(), w.to(dt).double(), b.double(), padding=1))
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    wk = w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
+    out = torch.empty(S * H * H, co, device=dev, dtype=dt)
+    a = ops._conv_args(xd, wk, out, S, H, H, c1, None, 0, None, 0, 0, 0, 1, b.to(dev), L.ACT_RELU, None, None, 16,
+                       None, 1)
+    assert lib.catseg_conv3x3_workspace(ops.C.byref(a)) > 0      # these shapes do split
+    ops.conv3x3(xd, wk, out, S=S, H=H, W=H, c1=c1, bias=b.to(dev), act=L.ACT_RELU)
+    close(out.reshape(S, H, H, co).permute(0, 3, 1, 2), ref, atol=1e-5 if dt == torch.float32 else 2e-2,
+          rtol=0 if dt == torch.float32 else 1e-2, what="split-K conv")
+
+
 @pytest.mark.parametrize("c1,c2,co,H", [(96, 32, 64, 48), (48, 16, 32, 96), (64, 0, 64, 48), (32, 0, 32, 96)])
 def test_conv3x3_ring_guidance_split(c1, c2, co, H):
     """The decoder convs on the ring kernel (bf16): conv over [x | g] (g per image, repeated over
@@ -356,8 +378,8 @@ def test_conv3x3_ring_guidance_split(c1, c2, co, H):
         out2 = torch.empty_like(out)
         wk = w.permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev, dt)
         ops.conv3x3(a1, wk, out2, S=S, H=H, W=W, c1=c1, src2=a2, c2=c2, src2_div=T)
-        e2 = (out.float() - out2.float()).abs()
-        assert e2.max().item() < 2e-2, e2.max().item()
+        e2 = (out.float() - out2.float()).abs() - 2.0 ** -7 * out2.float().abs()   # one bf16 rounding apart
+        assert e2.max().item() < 1e-2, e2.max().item()
 
 
 # ----------------------------------------------------------------------------- small ops
