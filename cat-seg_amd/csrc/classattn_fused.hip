@@ -120,14 +120,12 @@ __global__ __launch_bounds__(NT, 2) void classattn_kernel(ClsP a) {
       float v[8], sum = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) { v[j] = bf2f(e[j]); sum += v[j]; }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      sum = row16_sum(sum);
       const float mean = sum * (1.f / C);
       float qs = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) { v[j] -= mean; qs += v[j] * v[j]; }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) qs += __shfl_xor(qs, o, 64);
+      qs = row16_sum(qs);
       const float rstd = rsqrtf(qs * (1.f / C) + a.eps);
       {
         const float4 g0 = *reinterpret_cast<const float4*>(a.ln_g + lc * 8), g1 = *reinterpret_cast<const float4*>(a.ln_g + lc * 8 + 4);

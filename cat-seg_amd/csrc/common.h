@@ -75,18 +75,23 @@ DEV f32x4 mfma_f32(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-DEV float warp_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-// Full-wave sum on the DPP crossbar (no LDS-pipe ds_bpermute round trips): butterflies
-// inside quads and rows, then row broadcasts; lane 63 holds the total, read back uniformly.
-// Fixed order: deterministic.
+// Reductions on the DPP crossbar (no LDS-pipe ds_bpermute round trips, which cost ~100+
+// cycles each in the LayerNorm prologues of the row kernels).  Every step adds a value to
+// its partner's, so all lanes of a group end with bit-identical sums; fixed order:
+// deterministic.
 template <int CTRL, int ROWMASK = 0xF>
 DEV float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false));
 }
+// sum over the 16 lanes of each DPP row (lanes 16r .. 16r+15), result in all 16
+DEV float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);          // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);         // row_half_mirror
+  v += dpp_mov<0x140>(v);         // row_mirror
+  return v;
+}
+// full-wave sum: row sums, then row broadcasts into lane 63, read back uniformly
 DEV float wave_sum(float v) {
   v += dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);          // quad_perm [2,3,0,1]
@@ -96,6 +101,7 @@ DEV float wave_sum(float v) {
   v += dpp_mov<0x143, 0xC>(v);    // row_bcast:31 into rows 2, 3
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+DEV float warp_sum(float v) { return wave_sum(v); }
 DEV float warp_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

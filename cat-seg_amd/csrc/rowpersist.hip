@@ -56,14 +56,12 @@ DEV void put_chunk(uint4 u, const float* g, const float* b, float eps, bf16* sX)
     float v[8], s = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { v[j] = bf2f(e[j]); s += v[j]; }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = row16_sum(s);
     const float mean = s * (1.f / KD);
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { v[j] -= mean; q += v[j] * v[j]; }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    q = row16_sum(q);
     const float rstd = rsqrtf(q * (1.f / KD) + eps);
     const float4 g0 = *reinterpret_cast<const float4*>(g + ch * 8), g1 = *reinterpret_cast<const float4*>(g + ch * 8 + 4);
     const float4 b0 = *reinterpret_cast<const float4*>(b + ch * 8), b1 = *reinterpret_cast<const float4*>(b + ch * 8 + 4);
