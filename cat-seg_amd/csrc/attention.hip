@@ -211,8 +211,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
       for (int kt = 0; kt < KTV; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, st[kt][r]);
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      bmax = xrow4_max(bmax);
       const float m_new = fmaxf(m_run[t], bmax);
       const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * sl2);
       m_run[t] = m_new;

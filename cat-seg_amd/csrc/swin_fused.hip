@@ -113,16 +113,14 @@ __global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p, int nwin_total)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { v[ks][j] = bf2f(e[j]); s += v[ks][j]; }
       }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xrow4_sum(s);
       const float mean = s * (1.f / C);
       float q = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { v[ks][j] -= mean; q += v[ks][j] * v[ks][j]; }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xrow4_sum(q);
       const float rstd = rsqrtf(q * (1.f / C) + p.eps);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -210,8 +208,7 @@ __global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p, int nwin_total)
       for (int kt = 0; kt < KTV; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xrow4_max(mx);
       const float nb = -mx * sl2;
 #pragma unroll
       for (int kt = 0; kt < KTV; ++kt)
