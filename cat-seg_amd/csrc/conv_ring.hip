@@ -117,6 +117,11 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
       gsh[c] = p.gbeta[c] - p.gmean[s * ngroups + c / p.gcpg] * sc;
     }
   }
+  float bv[FN][4];                      // bias of this lane's output channels (0 without)
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[wco * COW + 16 * i + 4 * q + r] : 0.f;
   const bf16* s1base = p.s1 + s * p.s1_ss;
   const bf16* s2base = p.s2 ? p.s2 + (s / p.s2_div) * p.s2_ss : nullptr;
 
@@ -172,31 +177,38 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 
   for (int c = c_begin; c < c_end; ++c) {
     const int p0 = c * CH;
-    // ---- prefetch the rows the next chunk adds ----
+    // the per-image addend of this chunk (L2-resident) first, so that waiting for it does
+    // not also wait for the row prefetch issued after it (vmcnt retires in issue order)
+    float4 ad[FN][FM];
+    if constexpr (ADD) {
+      const float* addb = p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT + wco * COW;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          ad[i][j] = *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT + 16 * i + 4 * q);
+    }
+    // ---- prefetch the rows the next chunk adds: unconditional loads from clamped addresses
+    // (zero-selected at the ring write), so the code is straight-line and every wait is an
+    // exact vmcnt count ----
     uint4 pf[MAXPF];
     int nnew = 0;
     if (c + 1 < c_end) {
       const int yb_next = min((p0 + 2 * CH - 1) / W + 1, H);
       nnew = yb_next - loaded_to;
     }
+    unsigned pf_ok = 0;
 #pragma unroll
-    for (int k = 0; k < MAXPF; ++k)
-      pf[k] = (pf_code[k] >> 16) < nnew
-                  ? gload(loaded_to + 1 + (pf_code[k] >> 16), (pf_code[k] >> 4) & 0xfff, pf_code[k] & 15)
-                  : make_uint4(0, 0, 0, 0);
-
-    // the per-image addend of this chunk (L2-resident), in flight during the MFMAs
-    float4 ad[FN][FM];
-    if constexpr (ADD) {
-      const float* addb = p.add ? p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT + wco * COW
-                                : nullptr;
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-          ad[i][j] = addb ? *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT + 16 * i + 4 * q)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < MAXPF; ++k) {
+      const int dy = pf_code[k] >> 16, xc = (pf_code[k] >> 4) & 0xfff, ch = pf_code[k] & 15;
+      const int y = loaded_to + 1 + dy, x = xc - 1, ci = ch * 8;
+      const bool ok = dy < nnew && y < H && x >= 0 && x < W;
+      const int pix = ok ? y * W + x : 0;
+      const bf16* src = ci < p.c1 ? s1base + pix * p.c1 + ci : s2base + pix * p.c2 + (ci - p.c1);
+      pf[k] = ld16(src);
+      pf_ok |= (ok ? 1u : 0u) << k;
     }
+
     // ---- MFMAs: 9 taps x (KC + tail) k-steps over the ring ----
     int prow[FM], pcol[FM];
 #pragma unroll
@@ -257,11 +269,10 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         float adv[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (ADD) { adv[0] = ad[i][j].x; adv[1] = ad[i][j].y; adv[2] = ad[i][j].z; adv[3] = ad[i][j].w; }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r] + adv[r];
-          if (p.bias) v += p.bias[wco * COW + 16 * i + 4 * q + r];
-          acc[i][j][r] = apply_act(v, p.act);
-        }
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += adv[r] + bv[i][r];
+        if (p.act != ACT_NONE)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = apply_act(acc[i][j][r], p.act);
       }
     if (p.stats) {
       // GroupNorm partials per (wave pixel block = PXW pixels, group of 16 channels = one
@@ -302,7 +313,9 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < MAXPF; ++k)
-      if ((pf_code[k] >> 16) < nnew) lput(loaded_to + 1 + (pf_code[k] >> 16), (pf_code[k] >> 4) & 0xfff, pf_code[k] & 15, pf[k]);
+      if ((pf_code[k] >> 16) < nnew)
+        lput(loaded_to + 1 + (pf_code[k] >> 16), (pf_code[k] >> 4) & 0xfff, pf_code[k] & 15,
+             (pf_ok >> k) & 1 ? pf[k] : make_uint4(0, 0, 0, 0));
     loaded_to += nnew > 0 ? nnew : 0;
     __syncthreads();
   }
