@@ -200,7 +200,10 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
 // out = Y + act(LN(Y) . W1^T + b1) . W2^T + b2 (+ R2), hidden = 512.
 // wave w: GEMM1 hidden rows [64w, 64w+64) (W1 fragments in registers),
 //         GEMM2 output rows [16w, 16w+16) over all 512 hidden (W2 fragments in registers).
-constexpr int HID = 512, LDH = HID + 8;   // sH row stride (A/B: the cslot image measured slower here)
+// sH row stride: 264 dwords = 66 x 16 B makes the 16-B slot of GEMM2 fragment reads
+// (2 r16 + q) mod 16 -- conflict-free in every ds_read_b128 lane group (+8 measured 42 %
+// SQ_LDS_BANK_CONFLICT: slot r16 + q collides once per group)
+constexpr int HID = 512, LDH = HID + 16;
 
 template <int ACT, bool RES2>
 __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
