@@ -91,6 +91,7 @@ template <int NOUT, bool ADD, bool RES, bool SCATTER>
 __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X, int64_t ldx, int64_t M,
                                                       const float* ln_g, const float* ln_b, float eps,
                                                       const bf16* __restrict__ W, PEpi e) {
+  static_assert(!(ADD && RES), "the add rows use the residual ring slots");
   constexpr int WN = NOUT / NW, FN = WN / 16, FM = BM / 16;
   constexpr int SLD = NOUT + 4;
   constexpr int CH = NOUT / 8;                    // 8-column items per row
@@ -98,6 +99,16 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
   static_assert(ITEMS % NT == 0, "");
   __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
   __shared__ __attribute__((aligned(16))) float st[BM * SLD];
+  // LayerNorm gamma / beta and the bias live in LDS: a global load of them inside the tile
+  // loop would be younger than the row prefetch (and the previous tile's stores), and
+  // vmcnt retires in issue order, so waiting for it would expose the prefetch latency
+  __shared__ __attribute__((aligned(16))) float sPar[2 * KD + NOUT];
+  for (int i = threadIdx.x; i < 2 * KD + NOUT; i += NT)
+    sPar[i] = i < KD ? (ln_g ? ln_g[i] : 0.f) : i < 2 * KD ? (ln_b ? ln_b[i - KD] : 0.f) : e.bias[i - 2 * KD];
+  __syncthreads();
+  const float* lg = ln_g ? sPar : nullptr;
+  const float* lb = sPar + KD;
+  const float* bias = sPar + 2 * KD;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int wn = wave * WN;
@@ -117,6 +128,14 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
   uint4 rres[DEPTH][PER];
   auto fetch = [&](uint4& x, uint4* rr, int64_t t) {
     x = fetch_chunk(X, ldx, t * BM, M);
+    if constexpr (ADD) {       // the gathered guidance rows ride in the residual ring slots
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * NT, r = i / CH, c = (i % CH) * 8;
+        const int64_t m = t * BM + r;
+        rr[k] = (c < e.add_ncols && m < M) ? ld16(e.add + rowmap(e.addmap, m) * e.ld_add + c) : make_uint4(0, 0, 0, 0);
+      }
+    }
     if constexpr (RES) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
@@ -135,9 +154,9 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
     const int64_t tile = base + d * G;
     if (tile >= ntiles) break;
     const int64_t m0 = tile * BM;
-    put_chunk(rx[d], ln_g, ln_b, eps, sX);
+    put_chunk(rx[d], lg, lb, eps, sX);
     uint4 res_cur[PER];
-    if constexpr (RES) {
+    if constexpr (RES || ADD) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) res_cur[k] = rres[d][k];
     }
@@ -168,16 +187,14 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
     for (int k = 0; k < PER; ++k) {
       const int i = threadIdx.x + k * NT, r = i / CH, c = (i % CH) * 8;
       const int64_t m = m0 + r;
-      uint4 ad = make_uint4(0, 0, 0, 0);
       const bool do_add = ADD && c < e.add_ncols && m < M;
-      if (do_add) ad = ld16(e.add + rowmap(e.addmap, m) * e.ld_add + c);
       float v[8];
       *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c]);
       *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c + 4]);
-      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + c), b1 = *reinterpret_cast<const float4*>(e.bias + c + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + c), b1 = *reinterpret_cast<const float4*>(bias + c + 4);
       v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
       v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-      if (do_add) add8(v, ad);
+      if (do_add) add8(v, res_cur[k]);
       if constexpr (RES) add8(v, res_cur[k]);
       if (m < M) {
         int64_t off;
@@ -214,6 +231,13 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
   __shared__ __attribute__((aligned(16))) bf16 sH[BM * LDH];
   __shared__ __attribute__((aligned(16))) float st[BM * SLD];
+  // gamma / beta / b1 / b2 in LDS (see pgemm_kernel: no global loads behind the prefetch)
+  __shared__ __attribute__((aligned(16))) float sPar[2 * KD + HID + KD];
+  for (int i = threadIdx.x; i < 3 * KD + HID; i += NT)
+    sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD] : e.bias[i - 2 * KD - HID];
+  __syncthreads();
+  const float* sb1 = sPar + 2 * KD;
+  const float* sb2 = sPar + 2 * KD + HID;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   s16x8 w1f[4][4], w2f[16];
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     if (tile >= ntiles) break;
     const int64_t m0 = tile * BM;
     const uint4 y_raw = ry[d], r2_cur = rr2[d];     // residuals of this tile stay in registers
-    put_chunk(ry[d], ln_g, ln_b, eps, sX);
+    put_chunk(ry[d], sPar, sPar + KD, eps, sX);
     __syncthreads();
     if (tile + DEPTH_MLP * G < ntiles) fetch(ry[d], rr2[d], tile + DEPTH_MLP * G);
 #pragma unroll
@@ -270,7 +294,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int hh = 64 * wave + 16 * (2 * hf + i) + 4 * q;
-        const float4 bv = *reinterpret_cast<const float4*>(b1 + hh);
+        const float4 bv = *reinterpret_cast<const float4*>(sb1 + hh);
         const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
@@ -308,7 +332,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
       float v[8];
       *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec]);
       *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec + 4]);
-      const float4 c0 = *reinterpret_cast<const float4*>(e.bias + ec), c1 = *reinterpret_cast<const float4*>(e.bias + ec + 4);
+      const float4 c0 = *reinterpret_cast<const float4*>(sb2 + ec), c1 = *reinterpret_cast<const float4*>(sb2 + ec + 4);
       v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
       v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
       add8(v, y_raw);

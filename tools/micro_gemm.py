@@ -11,7 +11,7 @@ import torch
 from cat_seg import ops
 from cat_seg import _lib as L
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "-1,0,1,2,3,4,5,6,7,8").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").split(",")]
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True)}
