@@ -88,6 +88,36 @@ def test_engine_b16_config2_vs_oracle(dtype):
         assert err.max().item() < 5e-2 and err.mean().item() < 5e-3
 
 
+@pytest.mark.parametrize("T", [150, 847])
+def test_engine_l14_configs_3_4_vs_oracle(T):
+    """Config 3 (ViT-L/14 @336, 150 classes, bf16) and config 4's class count (847 -> top-256,
+    the class-attention tile at its maximum T' = 256) on one image against the CPU oracle;
+    bf16 gate max-abs 5e-2 / mean-abs 5e-3 on logits, untouched top-k classes exactly -100."""
+    arch = VIT_L14_336
+    sd = synthesize_state_dict(arch, seed=0)
+    gen = torch.Generator().manual_seed(11)
+    text = torch.nn.functional.normalize(torch.randn(T, arch.embed_dim, generator=gen), dim=-1)
+    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float()]
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    clip_images, _ = O.preprocess(arch, imgs)
+    ref = O.head_logits(arch, sd, clip_images, text.unsqueeze(1))
+    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    assert got.shape == ref.shape
+    live = ref > -99
+    if T > arch.pad_len:
+        # the selected classes agree (ties aside) and the rest are exactly -100
+        agree = (live == (got > -99)).float().mean().item()
+        assert agree > 0.99, agree
+        live = live & (got > -99)
+        assert torch.equal(got[~(ref > -99) & ~(got > -99)], ref[~(ref > -99) & ~(got > -99)])
+    err = (got[live] - ref[live]).abs()
+    print(f"L/14 T={T}: max {err.max().item():.3e} mean {err.mean().item():.3e}")
+    assert err.max().item() < 5e-2 and err.mean().item() < 5e-3, (err.max().item(), err.mean().item())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_engine_sliding_vs_reference_golden(dtype):
     """TEST.SLIDING_WINDOW (cat_seg_model.py:156-176,204-218): 4 Unfold tiles + global crop,
