@@ -289,10 +289,21 @@ void launch_win(const AttnP& p, hipStream_t st) {
   else launch<T, D, NW, KB, QT, GEO, false, false>(p, st);
 }
 
+int g_attn_variant = 0;   // dense-path tiling (catseg_set_attn_variant; 0 = default)
+
 template <typename T, int D>
 void launch_dense(const AttnP& p, hipStream_t st) {
-  if (p.causal) launch<T, D, 4, 64, 2, 0, false, true>(p, st);
-  else launch<T, D, 4, 64, 2, 0, false, false>(p, st);
+  if (p.causal) { launch<T, D, 4, 64, 2, 0, false, true>(p, st); return; }
+  // measured on the ViT-L/14 shape (tools/micro_attn.py): 8 waves x 16 queries per
+  // workgroup, 64-key blocks: 35.3 us vs 40.3 for 4 waves x 2 query tiles (more waves in
+  // flight hide the per-block softmax chain)
+  switch (g_attn_variant) {
+    case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;
+    case 2: launch<T, D, 4, 128, 2, 0, false, false>(p, st); break;
+    case 3: launch<T, D, 8, 128, 1, 0, false, false>(p, st); break;
+    case 4: launch<T, D, 8, 64, 2, 0, false, false>(p, st); break;
+    default: launch<T, D, 8, 64, 1, 0, false, false>(p, st); break;
+  }
 }
 
 template <typename T>
@@ -309,6 +320,8 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
 }
 
 }  // namespace
+
+extern "C" void catseg_set_attn_variant(int v) { g_attn_variant = v; }
 
 extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");

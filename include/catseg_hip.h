@@ -156,6 +156,9 @@ typedef struct {
   int dtype;
 } CatsegAttnArgs;
 int catseg_attention(const CatsegAttnArgs* args, void* stream);
+/* Tiling of the dense (mode 0, non-causal) bf16/fp32 path, for A/B tests (process-wide):
+ * 0 = default; 1..5 = alternative waves / key-block / query-tile configurations. */
+void catseg_set_attn_variant(int variant);
 
 /* catseg_linear_attention — class aggregation attention (LinearAttention,
  * model.py:256-286, inside AttentionLayer model.py:338-354 and the padding of

@@ -162,6 +162,25 @@ def test_attention_dense(dt, L_, H, causal):
     close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_attention_dense_tilings(variant):
+    """Every A/B tiling of the dense path (catseg_set_attn_variant) == the default tiling."""
+    B, L_, H, d = 2, 577, 4, 64
+    q = (rnd(B * L_, 3 * H * d, seed=19) * 2).to(dev, torch.bfloat16)
+    args = (q[:, :H * d], q[:, H * d:2 * H * d], q[:, 2 * H * d:])
+    kw = dict(n_seq=B, seq_len=L_, n_heads=H, head_dim=d, scale=d ** -0.5)
+    ref = torch.empty(B * L_, H * d, device=dev, dtype=torch.bfloat16)
+    ops.attention(*args, ref, **kw)
+    lib = L.load()
+    try:
+        lib.catseg_set_attn_variant(variant)
+        out = torch.empty_like(ref)
+        ops.attention(*args, out, **kw)
+    finally:
+        lib.catseg_set_attn_variant(0)
+    close(out, ref, atol=8e-3, what=f"attention tiling {variant}")
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shift", [0, 6])
 def test_attention_swin_windows(dt, shift):
