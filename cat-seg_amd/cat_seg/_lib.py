@@ -161,6 +161,7 @@ _SIGS = {
     "catseg_set_corr_mfma": [i32],
     "catseg_set_gemm_variant": [i32],
     "catseg_set_attn_variant": [i32],
+    "catseg_set_ring_variant": [i32],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
     "catseg_abi_version": [],
     "catseg_last_error": [],

@@ -33,6 +33,7 @@
 namespace {
 
 constexpr int NT = 256;          // 4 waves
+int g_ring_variant = 0;          // A/B tiling / band knobs (catseg_set_ring_variant; 0 = default)
 
 struct RingP {
   const bf16* s1; int64_t s1_ss; int c1;
@@ -331,8 +332,11 @@ template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, 
 int launch_ring_t(const RingP& p0, hipStream_t st) {
   RingP p = p0;
   const int nchunks = p.H * p.W / CH;
-  // bands of ~3072 pixels (a band re-primes its ring once), at least 2 workgroups per CU
-  const int per_band = 3072 / CH;
+  // bands of ~3072 pixels on narrow maps, ~6144 on wide ones (a band re-primes its ring once:
+  // the measured sweep, tools/micro_ring.py, favours longer bands at W = 96), at least 2
+  // workgroups per CU
+  const int base = p.W >= 64 ? 6144 : 3072;
+  const int per_band = (g_ring_variant == 3 ? base / 2 : g_ring_variant == 4 ? base * 2 : base) / CH;
   int bands = (nchunks + per_band - 1) / per_band;
   while (p.S * bands < 2048 && bands * 4 <= nchunks) bands *= 2;
   p.bands = bands;
@@ -406,8 +410,13 @@ static int ring_variant(const CatsegConvArgs* a, int* tile) {
   const bool narrow = a->W < 64;      // CH = 128 spans <= 3 rows only from W >= 64 on
   int v = 0, t = 0;
   if (C == 64 && a->c_out == 32) { v = narrow ? 1 : 2; t = 32; }
-  else if (C == 48 && a->c_out == 32) { v = narrow ? 3 : 4; t = narrow ? 32 : 64; }
-  else if (C == 32 && a->c_out == 32) { v = narrow ? 5 : 6; t = 32; }
+  else if (C == 48 && a->c_out == 32) {
+    v = narrow ? 3 : (g_ring_variant == 1 ? 4 : 9);
+    t = narrow || g_ring_variant != 1 ? 32 : 64;
+  } else if (C == 32 && a->c_out == 32) {
+    v = narrow ? 5 : (g_ring_variant == 2 ? 10 : 6);
+    t = !narrow && g_ring_variant == 2 ? 64 : 32;
+  }
   else if (C == 64 && a->c_out == 64 && a->W <= 50) { v = 7; t = 128; }
   else if (C == 96 && a->c_out == 64 && a->W <= 50) { v = 8; t = 64; }
   if (tile) *tile = t;
@@ -442,6 +451,8 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
     case 6: return launch_ring<32, 32, 4, 1, 198, 128, 2, 5>(p, st);
     case 7: return launch_ring<64, 64, 1, 4, 156>(p, st);
     case 8: return launch_ring<96, 64, 1, 4, 104, 64, 2, 5>(p, st);
+    case 9: return launch_ring<48, 32, 4, 1, 198, 128, 2, 5>(p, st);
+    case 10: return launch_ring<32, 32, 2, 2, 198, 128, 2, 5>(p, st);
     default: return 1;
   }
 }
@@ -469,3 +480,5 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
                        H, W, cin, weight, cout, out);
   return catseg_launch_status("conv3x3_partial");
 }
+
+extern "C" void catseg_set_ring_variant(int v) { g_ring_variant = v; }

@@ -116,6 +116,10 @@ int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const float* mean, c
  * with register-resident weights (default), 1 = LDS-tile kernel, 0 = im2col only.  Shapes a
  * family does not cover fall through to the next one down. */
 void catseg_set_conv_lds(int mode);
+/* Row-ring conv A/B knobs (process-wide, for tools/micro_ring.py): 0 = default; 1 / 2 =
+ * alternative wave splits of the 48- / 32-channel wide-map variants; 3 / 4 = half / double
+ * band length. */
+void catseg_set_ring_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */
