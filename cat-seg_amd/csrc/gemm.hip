@@ -405,8 +405,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   constexpr int NT3 = 64 * WGM * WGN;
   using SW = Swz<BK>;
   constexpr int BKC = SW::BKC;
-  constexpr int AG = BM * BKC / NT3, WG = BN * BKC / NT3, G = AG + WG;
-  static_assert(AG * NT3 == BM * BKC && WG * NT3 == BN * BKC, "tile / thread mismatch");
+  // A chunks may leave a partial last group (160 / 224-row tiles at 8 waves): it is issued by
+  // whole waves only, and only with S = 2, where every wait is vmcnt(0)
+  constexpr int AG = (BM * BKC + NT3 - 1) / NT3, WG = BN * BKC / NT3, G = AG + WG;
+  constexpr int AREM = BM * BKC - (AG - 1) * NT3;      // chunks of the last A group
+  static_assert(WG * NT3 == BN * BKC, "tile / thread mismatch");
+  static_assert(AREM == NT3 || (AREM % 64 == 0 && S == 2), "partial A group needs whole waves and S = 2");
   constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
   constexpr int STAGE = (BM + BN) * BK;           // elements per stage
   __shared__ __attribute__((aligned(16))) bf16 smem[S * STAGE];
@@ -439,7 +443,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
     const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
     for (int g = 0; g < AG; ++g)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[g] + k0), (lds_void_t*)(sa + (g * NT3 + wave * 64) * 8), 16, 0, 0);
+      if (AREM == NT3 || g < AG - 1 || wave * 64 < AREM)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[g] + k0), (lds_void_t*)(sa + (g * NT3 + wave * 64) * 8), 16, 0, 0);
 #pragma unroll
     for (int g = 0; g < WG; ++g)
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(wsrc[g] + k0), (lds_void_t*)(sw + (g * NT3 + wave * 64) * 8), 16, 0, 0);
@@ -488,7 +493,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   // ---- epilogue through LDS: rounds of 64 tile rows (JR m-fragments per wave row) are
   // staged as fp32, then every thread walks whole output rows (coalesced stores); the
   // accumulator indices stay compile-time constants (no scratch) ----
-  constexpr int JR = 4 / WGM, ROWS = 64, SLD = BN + 4;
+  // JR = the largest divisor of FM that keeps a round <= 64 rows (FM = 5 for 160-row tiles)
+  constexpr int JR0 = 4 / WGM, JR = FM % JR0 == 0 ? JR0 : (JR0 >= 2 && FM % 2 == 0 ? 2 : 1);
+  constexpr int ROWS = WGM * JR * 16, SLD = BN + 4;
   static_assert(JR >= 1 && FM % JR == 0, "epilogue rounds");
   static_assert(ROWS * SLD * 4 <= S * STAGE * 2, "epilogue stage exceeds LDS");
   float* stg = reinterpret_cast<float*>(smem);
@@ -740,12 +747,20 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (v < 0) return false;
   if (v == 0) {
     if (g->M < 1024 || g->K < 256) return false;
-    // Measured on ViT-L/14 shapes (M = 4616, tools/micro_gemm.py): the 256x256 tile wins
-    // when its tiles fit one round on the 256 CUs (QKV: 40 us vs 45), otherwise the
-    // 128x128 BK=64 tile at two blocks per CU (fc1 78 us vs 94, fc2 69 vs 115).
+    // Tile choice by wave quantization over the 256 CUs, measured on the ViT-L/14 shapes
+    // (M = 4616, tools/micro_gemm.py; hipBLASLt in brackets):
+    //  * a 224x256 tile when its tiles fill one round (QKV: 35.1 us vs 38.0 for 256x256 [32.3]);
+    //  * at K >= 2048, a 160x128 8-wave BK=128 tile when its tiles fit one round, one
+    //    workgroup per CU (fc2: 47.9 us vs 61.9 for 128x128 [42.2]);
+    //  * otherwise 160x128 with 8 waves at two workgroups per CU (fc1: 54.2 us vs 71.3 [55.4];
+    //    out-proj: 20.3 vs 24.7 [20.0]).
+    const int64_t t224 = ((g->M + 223) / 224) * (g->N / 256);
     const int64_t t256 = ((g->M + 255) / 256) * (g->N / 256);
-    if (g->N % 256 == 0 && t256 >= 160 && t256 <= 256) v = 1;
-    else if (g->N % 128 == 0) v = 5;
+    const int64_t t160 = ((g->M + 159) / 160) * (g->N / 128);
+    if (g->N % 256 == 0 && t224 >= 200 && t224 <= 256) v = 20;
+    else if (g->N % 256 == 0 && t256 >= 160 && t256 <= 256) v = 1;
+    else if (g->N % 128 == 0 && g->K >= 2048 && g->K % 128 == 0 && t160 >= 160 && t160 <= 256) v = 15;
+    else if (g->N % 128 == 0) v = 17;
     else return false;
   }
   switch (v) {
@@ -759,6 +774,12 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     case 8: return launch3<TO, 256, 128, 4, 2, 4, 32>(g, st);
     case 9: return launch8<TO>(g, st);
     case 10: return launch8<TO, true>(g, st);      // diagnostics only (no output)
+    case 11: return launch3<TO, 160, 128, 2, 2, 2, 64>(g, st);
+    case 15: return launch3<TO, 160, 128, 2, 4, 2, 128>(g, st);
+    case 17: return launch3<TO, 160, 128, 2, 4, 2, 64>(g, st);
+    case 18: return launch3<TO, 160, 256, 2, 4, 2, 64>(g, st);
+    case 19: return launch3<TO, 128, 128, 2, 4, 2, 64>(g, st);
+    case 20: return launch3<TO, 224, 256, 2, 4, 2, 64>(g, st);
     default: return false;
   }
 }
