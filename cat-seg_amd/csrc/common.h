@@ -139,39 +139,38 @@ DEV float fast_erf(float x) {
   return copysignf(y, x);
 }
 
-// GELU(x) = 0.5 x (1 + erf(x / sqrt 2)) with erf(x / sqrt 2) = x Q(x^2) for |x| < 3 sqrt 2
-// (Q: 10-term minimax-fitted polynomial, |erf error| <= 4e-6) and +-1 beyond (erf(3) =
-// 1 - 2.2e-5): no transcendental at all (v_exp / v_rcp are quarter rate), and written on
-// float2 so the Horner chain maps to packed v_pk_fma_f32.  |GELU error| <= 1e-5.
+// GELU(x) = 0.5 x (1 + erf(x / sqrt 2)), erf(x / sqrt 2) ~= xc P(xc^2), xc = clamp(x, +-3 sqrt 2):
+// P is a degree-8 minimax fit of the GELU error (x/2)|dt| (linear program on a 3000-point grid),
+// max 3.0e-5 inside the clamp evaluated in fp32; no transcendental (v_exp / v_rcp cost 8 issue
+// cycles).  Written on scalars: whether the fp32 chain is packed (v_pk_fma_f32) is left to the
+// compiler's SLP pass, which measured neutral for the MLP and positive for most kernels.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// erf(x / sqrt 2) ~= xc * P(xc^2), xc = clamp(x, +-3 sqrt 2): degree-8 minimax fit of the
-// GELU error (x/2) |dt| (linear program on a 3000-point grid), max 3.0e-5 inside the clamp
-// evaluated in fp32
-DEV f32x2 erf_t2(f32x2 x) {
+DEV float erf_t1(float x) {
   constexpr float XC = 4.242640495f;
-  const f32x2 xc = f32x2{__builtin_amdgcn_fmed3f(x.x, -XC, XC), __builtin_amdgcn_fmed3f(x.y, -XC, XC)};
-  const f32x2 s = xc * xc;
-  f32x2 p = f32x2{9.1976350e-11f, 9.1976350e-11f};
-  p = p * s - 9.1081507e-09f;
-  p = p * s + 3.9963419e-07f;
-  p = p * s - 1.0334782e-05f;
-  p = p * s + 1.7735695e-04f;
-  p = p * s - 2.1602388e-03f;
-  p = p * s + 1.9443829e-02f;
-  p = p * s - 1.3238958e-01f;
-  p = p * s + 7.9764283e-01f;
+  const float xc = __builtin_amdgcn_fmed3f(x, -XC, XC);
+  const float s = xc * xc;
+  float p = 9.1976350e-11f;
+  p = __builtin_fmaf(p, s, -9.1081507e-09f);
+  p = __builtin_fmaf(p, s, 3.9963419e-07f);
+  p = __builtin_fmaf(p, s, -1.0334782e-05f);
+  p = __builtin_fmaf(p, s, 1.7735695e-04f);
+  p = __builtin_fmaf(p, s, -2.1602388e-03f);
+  p = __builtin_fmaf(p, s, 1.9443829e-02f);
+  p = __builtin_fmaf(p, s, -1.3238958e-01f);
+  p = __builtin_fmaf(p, s, 7.9764283e-01f);
   return xc * p;
 }
+DEV f32x2 erf_t2(f32x2 x) { return f32x2{erf_t1(x.x), erf_t1(x.y)}; }
 // GELU for the bf16 paths: beyond the clamp t = xc P(xc^2) ~= erf(3) = 1 - 2.2e-5 instead of +-1,
-// a relative error < 1e-4 (bf16 keeps 3.9e-3): no saturation select (14 packed / med3 ops per pair)
-DEV f32x2 gelu2(f32x2 x) {
-  const f32x2 t = erf_t2(x);
-  const f32x2 h = x * 0.5f;
-  return h + h * t;
+// a relative error < 1e-4 (bf16 keeps 3.9e-3): no saturation select (12 VALU per value)
+DEV float gelu1(float x) {
+  const float h = 0.5f * x;
+  return __builtin_fmaf(h, erf_t1(x), h);
 }
+DEV f32x2 gelu2(f32x2 x) { return f32x2{gelu1(x.x), gelu1(x.y)}; }
 // exact-saturation GELU (fp32 paths)
 DEV float gelu_erf(float v) {
-  float t = erf_t2(f32x2{v, v}).x;
+  float t = erf_t1(v);
   t = fabsf(v) < 4.242640495f ? t : copysignf(1.f, v);
   const float h = 0.5f * v;
   return h + h * t;
