@@ -65,8 +65,13 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   constexpr bool BF = sizeof(T) == 2;
   constexpr int VN = Vec16<T>::N;
   constexpr int XD = SWM ? (BF ? 32 : 12) : 0;          // region dims appended to K / Q
-  constexpr int KP = D + XD + (BF ? 8 : 4);             // K row stride (elements)
-  constexpr int VP = KB + 4;                            // V^T row stride
+  // bf16: K and V both staged row-major [key][d] with 16-element row padding: the K
+  // fragment reads (ds_read_b128, 16-B slot 10*row + g mod 16 for D + XD = 64) and the V
+  // transposed reads (ds_read_b64_tr_b16, 8 rows x 32 B per 32-lane half, row stride 24 or
+  // 40 dwords) are conflict-free; fp32 keeps V^T [d][key]
+  constexpr int KP = D + XD + (BF ? 16 : 4);            // K row stride (elements)
+  constexpr int VP = BF ? D + 16 : KB + 4;              // V row stride (bf16) / V^T row stride (fp32)
+  constexpr int VROWS = BF ? KB : D;
   constexpr int DT = D / 16;                            // d tiles of O^T
   constexpr int KT = KB / 16;                           // key tiles per block
   constexpr int KS = BF ? 32 : 4;                       // K depth of one MFMA
@@ -76,7 +81,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   static_assert(!LC || (LC <= KB && LC % 16 == 0), "fixed window must fill whole key tiles");
   using QFrag = typename std::conditional<BF, s16x8, float>::type;
   __shared__ __attribute__((aligned(16))) T Ks[KB * KP];
-  __shared__ __attribute__((aligned(16))) T Vt[D * VP];
+  __shared__ __attribute__((aligned(16))) T Vt[VROWS * VP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int s = blockIdx.y / p.H;
@@ -160,9 +165,13 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
         vu = ld16(Vg + r * p.ld + h * D + d0);
       }
       st16(&Ks[kk * KP + d0], ku);
-      const T* ve = reinterpret_cast<const T*>(&vu);
+      if constexpr (BF) {
+        st16(&Vt[kk * VP + d0], vu);
+      } else {
+        const T* ve = reinterpret_cast<const T*>(&vu);
 #pragma unroll
-      for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
+        for (int j = 0; j < VN; ++j) Vt[(d0 + j) * VP + kk] = ve[j];
+      }
       if constexpr (SWM) {
         if (d0 == 0) {
           const int kreg = key < L ? swin_region<GEO>(p, wloc, key) : -1;
@@ -237,11 +246,16 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
           const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
-            const T* vr = &Vt[(dt * 16 + (lane & 15)) * VP + 32 * u + 4 * g];
-            const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-            const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-            uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
-            o[t][dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[t][dt]);
+            // V^T fragment by transposed reads: lane 4q'+p' of group g addresses key row
+            // 32u + 4g + q' (and + 16), columns 16 dt + 4p' .. +3; lane i receives d = 16 dt + i
+            // over those 4 keys -- P's permuted key order (keys 32u + 4g + r, then + 16)
+            const int i16 = lane & 15;
+            const T* vr = &Vt[(32 * u + 4 * g + (i16 >> 2)) * VP + dt * 16 + 4 * (i16 & 3)];
+            typedef short s16x4 __attribute__((ext_vector_type(4)));
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * VP));
+            const s16x8 va = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[t][dt] = mfma_bf16(va, pb, o[t][dt]);
           }
           osum[t] = mfma_bf16(ones, pb, osum[t]);
         }
