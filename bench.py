@@ -180,7 +180,8 @@ def pmc_traffic(family):
     (profiles/<round>/pmc_traffic.json, written by tools/pmc_traffic.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per the gfx950 note)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    # profiles/<round>/[<version>/]pmc_traffic.json: the lexicographically last is the newest
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True))
     if not files:
         return None, None
     fam = json.load(open(files[-1]))["families"].get(family)
