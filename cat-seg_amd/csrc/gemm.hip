@@ -405,12 +405,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   constexpr int NT3 = 64 * WGM * WGN;
   using SW = Swz<BK>;
   constexpr int BKC = SW::BKC;
-  // A chunks may leave a partial last group (160 / 224-row tiles at 8 waves): it is issued by
-  // whole waves only, and only with S = 2, where every wait is vmcnt(0)
+  // A chunks may leave a partial last group (160 / 224-row tiles at 8 waves): every wave still
+  // issues it (uniform counted vmcnt), the waves past AREM re-loading the chunks of wave
+  // (wave mod AREM/64) into the same LDS slots -- identical bytes, a benign duplicate write
   constexpr int AG = (BM * BKC + NT3 - 1) / NT3, WG = BN * BKC / NT3, G = AG + WG;
   constexpr int AREM = BM * BKC - (AG - 1) * NT3;      // chunks of the last A group
   static_assert(WG * NT3 == BN * BKC, "tile / thread mismatch");
-  static_assert(AREM == NT3 || (AREM % 64 == 0 && S == 2), "partial A group needs whole waves and S = 2");
+  static_assert(AREM % 64 == 0, "partial A group must be whole waves");
   constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
   constexpr int STAGE = (BM + BN) * BK;           // elements per stage
   __shared__ __attribute__((aligned(16))) bf16 smem[S * STAGE];
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   const bf16* asrc[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
-    const int c = g * NT3 + tid, row = c / BKC, ch = SW::slot(row, c % BKC);
+    const int c = g * NT3 + (g == AG - 1 ? tid % AREM : tid), row = c / BKC, ch = SW::slot(row, c % BKC);
     int64_t m = m0 + row;
     if (m >= M) m = M - 1;
     asrc[g] = A + (ident ? m : rowmap(amap, m)) * lda + ch * 8;
@@ -442,9 +443,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
     bf16* sw = sa + BM * BK;
     const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
-    for (int g = 0; g < AG; ++g)
-      if (AREM == NT3 || g < AG - 1 || wave * 64 < AREM)
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[g] + k0), (lds_void_t*)(sa + (g * NT3 + wave * 64) * 8), 16, 0, 0);
+    for (int g = 0; g < AG; ++g) {
+      const int wv = g == AG - 1 ? wave % (AREM / 64) : wave;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[g] + k0), (lds_void_t*)(sa + (g * NT3 + wv * 64) * 8), 16, 0, 0);
+    }
 #pragma unroll
     for (int g = 0; g < WG; ++g)
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(wsrc[g] + k0), (lds_void_t*)(sw + (g * NT3 + wave * 64) * 8), 16, 0, 0);
@@ -750,16 +752,16 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     // Tile choice by wave quantization over the 256 CUs, measured on the ViT-L/14 shapes
     // (M = 4616, tools/micro_gemm.py; hipBLASLt in brackets):
     //  * a 224x256 tile when its tiles fill one round (QKV: 35.1 us vs 38.0 for 256x256 [32.3]);
-    //  * at K >= 2048, a 160x128 8-wave BK=128 tile when its tiles fit one round, one
-    //    workgroup per CU (fc2: 47.9 us vs 61.9 for 128x128 [42.2]);
-    //  * otherwise 160x128 with 8 waves at two workgroups per CU (fc1: 54.2 us vs 71.3 [55.4];
-    //    out-proj: 20.3 vs 24.7 [20.0]).
+    //  * a 160x128 8-wave BK=128 tile when its tiles fit one round, one workgroup per CU
+    //    (fc2: 47.9 us vs 61.9 for 128x128 [42.2]; out-proj: 19.8 vs 24.7 [18.2]);
+    //  * otherwise 160x128 with 8 waves at two workgroups per CU (fc1: 54.2 us vs 71.3 [55.4]).
+    // Deeper rings (S = 3 / 4 at BK = 64, variants 21 / 22) measured slower on fc2 (53 us).
     const int64_t t224 = ((g->M + 223) / 224) * (g->N / 256);
     const int64_t t256 = ((g->M + 255) / 256) * (g->N / 256);
     const int64_t t160 = ((g->M + 159) / 160) * (g->N / 128);
     if (g->N % 256 == 0 && t224 >= 200 && t224 <= 256) v = 20;
     else if (g->N % 256 == 0 && t256 >= 160 && t256 <= 256) v = 1;
-    else if (g->N % 128 == 0 && g->K >= 2048 && g->K % 128 == 0 && t160 >= 160 && t160 <= 256) v = 15;
+    else if (g->N % 128 == 0 && g->K % 128 == 0 && t160 >= 160 && t160 <= 256) v = 15;
     else if (g->N % 128 == 0) v = 17;
     else return false;
   }
@@ -780,6 +782,9 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     case 18: return launch3<TO, 160, 256, 2, 4, 2, 64>(g, st);
     case 19: return launch3<TO, 128, 128, 2, 4, 2, 64>(g, st);
     case 20: return launch3<TO, 224, 256, 2, 4, 2, 64>(g, st);
+    case 21: return launch3<TO, 160, 128, 2, 4, 3, 64>(g, st);
+    case 22: return launch3<TO, 160, 128, 2, 4, 4, 64>(g, st);
+    case 23: return launch3<TO, 224, 256, 2, 4, 4, 32>(g, st);
     default: return false;
   }
 }

@@ -90,7 +90,7 @@ def test_gemm_convtranspose_store(dt):
     close(got, ref, atol=1e-5 if dt == torch.float32 else 2e-2, what="convT")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 17, 18, 19, 20])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 17, 18, 19, 20, 21, 22, 23])
 def test_gemm_pipelined_variants(variant):
     """Every LDS-DMA pipelined bf16 tile (gemm.hip gemm3_kernel) against fp64: ragged M
     (sliver tile), a CLS-dropping row map, bias + QuickGELU + fp32 residual epilogue."""
