@@ -486,10 +486,13 @@ __global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__
   const int64_t HW = (int64_t)H * W;
   const bf16* xs = x + s * HW * C;
   const int total = (rows + 2) * WP * CPX;
-  for (int i0 = 0; i0 < total; i0 += 256 * 4) {
-    uint4 u[4];
+  // all of the band's loads in flight at once (<= 16 per thread for W <= 100): one memory
+  // round trip per workgroup instead of one per 4 loads (two workgroups per CU by LDS)
+  constexpr int NL = 16;
+  for (int i0 = 0; i0 < total; i0 += 256 * NL) {
+    uint4 u[NL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NL; ++j) {
       const int i = i0 + j * 256 + tid;
       const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
       const int yy = y0 - 1 + r, xx = xc - 1;
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__
                                                                    : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NL; ++j) {
       const int i = i0 + j * 256 + tid;
       if (i >= total) continue;
       const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
