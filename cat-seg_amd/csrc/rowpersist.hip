@@ -360,6 +360,14 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
   __shared__ __attribute__((aligned(16))) bf16 sX[BM64 * LDX64];
   __shared__ __attribute__((aligned(16))) float st[BM64 * SLD];
   __shared__ float ssc[K64], ssh[K64];
+  // bias / gamma / beta in LDS once, and the next tile's rows + GroupNorm statistics
+  // prefetched right after this tile's rows reach LDS: no global load is issued behind the
+  // previous tile's stores (vmcnt retires in order)
+  __shared__ __attribute__((aligned(16))) float sPar[NOUT + 2 * K64];
+  for (int i = threadIdx.x; i < NOUT + 2 * K64; i += NT4)
+    sPar[i] = i < NOUT ? e.bias[i] : i < NOUT + K64 ? gamma[i - NOUT] : beta[i - NOUT - K64];
+  __syncthreads();
+  const float* sbias = sPar;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int wn = wave * WN;
@@ -373,22 +381,31 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
     }
   const int groups = K64 / cpg;
   const int64_t ntiles = (M + BM64 - 1) / BM64;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t m0 = tile * BM64;
-    const int64_t s = m0 / HW;
-    uint4 u[2];
+  uint4 u[2];
+  float pm = 0.f, pr = 0.f;
+  auto fetch = [&](int64_t t) {
+    const int64_t m0 = t * BM64;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int c = threadIdx.x + k * NT4, r = c >> 3, ch = c & 7;
       u[k] = m0 + r < M ? ld16(X + (m0 + r) * K64 + ch * 8) : make_uint4(0, 0, 0, 0);
     }
     if (threadIdx.x < K64) {
-      const int c = threadIdx.x;
-      const float sc = rstd[s * groups + c / cpg] * gamma[c];
-      ssc[c] = sc;
-      ssh[c] = beta[c] - mean[s * groups + c / cpg] * sc;
+      const int64_t gi = (m0 / HW) * groups + threadIdx.x / cpg;
+      pm = mean[gi];
+      pr = rstd[gi];
     }
-    __syncthreads();
+  };
+  if (blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t m0 = tile * BM64;
+    if (threadIdx.x < K64) {
+      const int c = threadIdx.x;
+      const float sc = pr * sPar[NOUT + c];
+      ssc[c] = sc;
+      ssh[c] = sPar[NOUT + K64 + c] - pm * sc;
+    }
+    __syncthreads();                  // ssc ready; the previous tile's MFMA / epilogue reads are done
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int c = threadIdx.x + k * NT4, r = c >> 3, ch = c & 7;
@@ -397,6 +414,7 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       for (int j = 0; j < 8; ++j) ev[j] = f2bf(fmaxf(fmaf(bf2f(ev[j]), ssc[ch * 8 + j], ssh[ch * 8 + j]), 0.f));
       st16(&sX[r * LDX64 + ch * 8], u[k]);
     }
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
     __syncthreads();
     f32x4 acc[FN][FM];
 #pragma unroll
@@ -419,6 +437,7 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       for (int j = 0; j < FM; ++j)
         *reinterpret_cast<f32x4*>(&st[(16 * j + r16) * SLD + wn + 16 * i + 4 * q]) = acc[i][j];
     __syncthreads();
+    const uint32_t hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = threadIdx.x + k * NT4, r = i / CH, c = (i % CH) * 8;
@@ -428,9 +447,8 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c]);
       *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[r * SLD + c + 4]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += e.bias[c + j];
+      for (int j = 0; j < 8; ++j) v[j] += sbias[c + j];
       // ConvTranspose scatter, 32-bit index math (m < 2^31, host-checked): kk = 2
-      const uint32_t hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
       const uint32_t mu = (uint32_t)m, mw = mu / win, x = mu - mw * win;
       const uint32_t sl = mw / hin, y = mw - sl * hin;
       const uint32_t ky = (uint32_t)c / (2 * cout), rem = (uint32_t)c - ky * 2 * cout;
@@ -438,7 +456,6 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       const int64_t orow = ((int64_t)(sl * hin + y) * 2 + ky) * (2 * win) + x * 2 + kx;
       st16(e.out + orow * cout + co, pack8(v));
     }
-    __syncthreads();
   }
 }
 
