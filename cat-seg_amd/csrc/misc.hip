@@ -163,22 +163,16 @@ DEV void split_bf16(float v, bf16& hi, bf16& lo) {
 }
 
 __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr, int64_t ts, int64_t bs,
-                                                              const int32_t* classes, int Tn, int H, int W,
-                                                              const float* w, const float* bias, bf16* out) {
+                                                              const int32_t* classes, int64_t S, int Tn, int H,
+                                                              int W, const float* w, const float* bias, bf16* out) {
   constexpr int HID = 128;
   __shared__ float sin[1024];          // (H + 6) x (W + 6) zero-padded slice (host-checked)
+  __shared__ float sbias[HID];
   const int PW = W + 6, PH = H + 6;
-  const int64_t s = blockIdx.x;
-  const int64_t b = s / Tn;
-  const int t = (int)(s % Tn);
-  const int cls = classes ? classes[s] : t;
-  const float* src = corr + (int64_t)cls * ts + b * bs;
-  for (int i = threadIdx.x; i < PH * PW; i += blockDim.x) {
-    const int y = i / PW - 3, x = i % PW - 3;
-    sin[i] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
-  }
+  const int HW = H * W;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
+  // persistent over slices: the hi/lo weight fragments are built once per workgroup
   s16x8 whi[8][2], wlo[8][2];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -193,6 +187,7 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
       whi[i][ks] = *reinterpret_cast<const s16x8*>(h);
       wlo[i][ks] = *reinterpret_cast<const s16x8*>(l);
     }
+  if (threadIdx.x < HID) sbias[threadIdx.x] = bias[threadIdx.x];
   int toff[2][8];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
@@ -201,42 +196,65 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
       const int k = 32 * ks + 8 * q + j;
       toff[ks][j] = k < 49 ? (k / 7) * PW + k % 7 : -1;
     }
-  __syncthreads();
-  const int HW = H * W;
-  const int ntiles = (HW + 15) / 16;
-  for (int tile = wave; tile < ntiles; tile += 4) {
-    const int pix = tile * 16 + r16;
-    const bool valid = pix < HW;
-    const int y = valid ? pix / W : 0, x = valid ? pix % W : 0;
-    const int base = y * PW + x;
-    s16x8 bhi[2], blo[2];
+  // the slice's HW (<= 576, host-checked) values: up to 3 per thread, prefetched a slice ahead
+  float pv[3];
+  auto fetch = [&](int64_t s) {
+    const int64_t b = s / Tn;
+    const int t = (int)(s % Tn);
+    const int cls = classes ? classes[s] : t;
+    const float* src = corr + (int64_t)cls * ts + b * bs;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16 h[8], l[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) split_bf16(toff[ks][j] >= 0 ? sin[base + toff[ks][j]] : 0.f, h[j], l[j]);
-      bhi[ks] = *reinterpret_cast<const s16x8*>(h);
-      blo[ks] = *reinterpret_cast<const s16x8*>(l);
+    for (int k = 0; k < 3; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      pv[k] = i < HW ? src[i] : 0.f;
     }
-    f32x4 acc[8];
+  };
+  if (blockIdx.x < S) fetch(blockIdx.x);
+  for (int i = threadIdx.x; i < PH * PW; i += 256) sin[i] = 0.f;   // the halo stays zero
+  for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+    __syncthreads();                   // previous slice's gathers done (and the halo zeroed)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 3; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < HW) sin[(i / W + 3) * PW + i % W + 3] = pv[k];
+    }
+    __syncthreads();
+    if (s + gridDim.x < S) fetch(s + gridDim.x);
+    const int ntiles = (HW + 15) / 16;
+    for (int tile = wave; tile < ntiles; tile += 4) {
+      const int pix = tile * 16 + r16;
+      const bool valid = pix < HW;
+      const int y = valid ? pix / W : 0, x = valid ? pix % W : 0;
+      const int base = y * PW + x;
+      s16x8 bhi[2], blo[2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        acc[i] = mfma_bf16(whi[i][ks], bhi[ks], acc[i]);
-        acc[i] = mfma_bf16(whi[i][ks], blo[ks], acc[i]);
-        acc[i] = mfma_bf16(wlo[i][ks], bhi[ks], acc[i]);
+        bf16 h[8], l[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split_bf16(toff[ks][j] >= 0 ? sin[base + toff[ks][j]] : 0.f, h[j], l[j]);
+        bhi[ks] = *reinterpret_cast<const s16x8*>(h);
+        blo[ks] = *reinterpret_cast<const s16x8*>(l);
       }
-    }
-    if (valid) {
-      bf16* o = out + (s * HW + pix) * HID;
+      f32x4 acc[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int c = 16 * i + 4 * q;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + c);
-        *reinterpret_cast<uint2*>(o + c) = make_uint2(f2bf2(acc[i][0] + bb.x, acc[i][1] + bb.y),
-                                                      f2bf2(acc[i][2] + bb.z, acc[i][3] + bb.w));
+        acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          acc[i] = mfma_bf16(whi[i][ks], bhi[ks], acc[i]);
+          acc[i] = mfma_bf16(whi[i][ks], blo[ks], acc[i]);
+          acc[i] = mfma_bf16(wlo[i][ks], bhi[ks], acc[i]);
+        }
+      }
+      if (valid) {
+        bf16* o = out + (s * HW + pix) * HID;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int c = 16 * i + 4 * q;
+          const float4 bb = *reinterpret_cast<const float4*>(sbias + c);
+          *reinterpret_cast<uint2*>(o + c) = make_uint2(f2bf2(acc[i][0] + bb.x, acc[i][1] + bb.y),
+                                                        f2bf2(acc[i][2] + bb.z, acc[i][3] + bb.w));
+        }
       }
     }
   }
@@ -535,9 +553,18 @@ extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64
   const size_t sh = ((H + 6) * (W + 6) + 49 * hidden) * sizeof(float);
   CATSEG_CHECK(sh <= 64 * 1024, "corr_embed: slice too large for LDS");
   const unsigned grid = (unsigned)(B * T);
-  if (dtype == CATSEG_BF16 && hidden == 128 && (H + 6) * (W + 6) <= 1024 && g_corr_mfma)
-    hipLaunchKernelGGL(corr_embed_mfma_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
-                       corr_b_stride, classes, T, H, W, weight, bias, (bf16*)out);
+  if (dtype == CATSEG_BF16 && hidden == 128 && (H + 6) * (W + 6) <= 1024 && H * W <= 768 && g_corr_mfma) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const unsigned pgrid = (unsigned)std::min<int64_t>(B * T, (int64_t)cus * 2);
+    hipLaunchKernelGGL(corr_embed_mfma_kernel, dim3(pgrid), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
+                       corr_b_stride, classes, B * (int64_t)T, T, H, W, weight, bias, (bf16*)out);
+  }
   else if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(corr_embed_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, corr, corr_t_stride,
                        corr_b_stride, classes, T, H, W, weight, bias, hidden, (bf16*)out);
