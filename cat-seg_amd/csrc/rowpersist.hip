@@ -276,11 +276,14 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     if (tile + DEPTH_MLP * G < ntiles) fetch(ry[d], rr2[d], tile + DEPTH_MLP * G);
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
+      // the accumulators start from the fc1 bias (no per-element add after the MFMAs)
       f32x4 acc1[2][FM];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        const float4 bv = *reinterpret_cast<const float4*>(sb1 + 64 * wave + 16 * (2 * hf + i) + 4 * q);
 #pragma unroll
-        for (int j = 0; j < FM; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FM; ++j) acc1[i][j] = f32x4{bv.x, bv.y, bv.z, bv.w};
+      }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s16x8 xf[FM];
@@ -294,18 +297,15 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int hh = 64 * wave + 16 * (2 * hf + i) + 4 * q;
-        const float4 bv = *reinterpret_cast<const float4*>(sb1 + hh);
-        const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
           float v[4];
           if constexpr (ACT == ACT_GELU) {
-            const f32x2 g0 = gelu2(f32x2{acc1[i][j][0] + bb[0], acc1[i][j][1] + bb[1]});
-            const f32x2 g1 = gelu2(f32x2{acc1[i][j][2] + bb[2], acc1[i][j][3] + bb[3]});
-            v[0] = g0.x; v[1] = g0.y; v[2] = g1.x; v[3] = g1.y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = gelu1(acc1[i][j][r]);
           } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r] + bb[r]);
+            for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r]);
           }
           store4<bf16>(&sH[(16 * j + r16) * LDH + hh], v);
         }
