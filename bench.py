@@ -40,6 +40,7 @@ from cat_seg.weights import synthesize_state_dict  # noqa: E402
 GF_PER_IMAGE = 875.7          # reference eval forward FLOPs, L/14@336, T=150
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_FP8_TFLOPS = 5000.0      # MI355X dense fp8 MFMA (block-scaled K=128 form)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -54,6 +55,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--cpu-images", type=int, default=4, help="oracle sample size for cpu_baseline (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--vit-fp8", action="store_true",
+                    help="config 5's e4m3 CLIP image-encoder GEMMs (not the headline: the headline is bf16)")
     return ap.parse_args()
 
 
@@ -78,7 +81,7 @@ def main():
     R = arch.clip_resolution
 
     sd = synthesize_state_dict(arch, seed=0)
-    eng = CatSegEngine(arch, sd, dtype=dtype, device=dev)
+    eng = CatSegEngine(arch, sd, dtype=dtype, device=dev, vit_fp8=args.vit_fp8)
     with torch.no_grad():
         text = eng.encode_text(class_tokens(T))
         eng.set_text(text)
@@ -154,7 +157,8 @@ def main():
             "metric": "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling",
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype + ("+fp8e4m3 ViT GEMMs" if args.vit_fp8 else ""),
             "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, ade150 prompt tokens)",
             "config": {"workload": f"CATSeg eval forward ViT-L/14@336, T={T} classes, bs={B}/GPU, "
                                    "POOLING [1,1], sigmoid upsampled to 336x336",
@@ -211,7 +215,8 @@ def roofline_pass(step, stream, dtype):
     traffic, tsrc = pmc_traffic(top)
     if a["flops"] > 0:
         achieved = a["flops"] / a["launches"] / avg_s / 1e12
-        peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+        peak = (PEAK_FP8_TFLOPS if top == "gemm_fp8" else
+                PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS)
         roof = {"bound": "mfma", "kernel": top, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2),

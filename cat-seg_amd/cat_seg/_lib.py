@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CATSEG_HIP_LIB", os.path.join(_HERE, "libcatseg_hip.so"))
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_QUICKGELU, ACT_SIGMOID = 0, 1, 2, 3, 4
 BIG = 1 << 62
 
@@ -123,6 +123,9 @@ class ConvArgs(C.Structure):
 # name -> (argtypes); every entry returns int
 _SIGS = {
     "catseg_gemm": [C.POINTER(GemmArgs), vp],
+    "catseg_gemm_fp8": [C.POINTER(GemmArgs), vp, vp, vp],
+    "catseg_quant_fp8_rows": [vp, i32, i64, i64, i64, vp, i64, vp, vp],
+    "catseg_set_gemm_fp8_variant": [i32],
     "catseg_rows_gemm": [vp, i64, i64, vp, vp, f32, vp, i64, C.POINTER(RowsEpi), i32, vp],
     "catseg_rows_mlp": [vp, i64, i64, vp, vp, f32, vp, vp, i64, i32, vp, C.POINTER(RowsEpi), i32, vp],
     "catseg_layernorm": [vp, i64, RowMap, i32, vp, i64, i32, vp, vp, i64, i64, f32, vp],

@@ -53,7 +53,8 @@ class CATSeg(nn.Module):
                  pixel_std: Tuple[float], clip_pixel_mean: Tuple[float], clip_pixel_std: Tuple[float],
                  train_class_json: str, test_class_json: str, sliding_window: bool, clip_finetune: str,
                  backbone_multiplier: float, clip_pretrained: str, arch: Optional[CatSegArch] = None,
-                 dtype: str = "bf16", return_all_images: bool = True, synthetic_seed: int = 0):
+                 dtype: str = "bf16", return_all_images: bool = True, synthetic_seed: int = 0,
+                 vit_fp8: bool = False):
         super().__init__()
         self.backbone = backbone
         self.sem_seg_head = sem_seg_head
@@ -74,6 +75,7 @@ class CATSeg(nn.Module):
             clip_pixel_mean=tuple(clip_pixel_mean), clip_pixel_std=tuple(clip_pixel_std))
         self.compute_dtype = _DTYPES[dtype]
         self.return_all_images = return_all_images
+        self.vit_fp8 = bool(vit_fp8)
         self._sd = synthesize_state_dict(self.arch, seed=synthetic_seed)
         self._engine: Optional[CatSegEngine] = None
 
@@ -98,6 +100,7 @@ class CATSeg(nn.Module):
             "dtype": hip.get("DTYPE", "bf16") if hip else "bf16",
             "return_all_images": bool(hip.get("RETURN_ALL_IMAGES", True)) if hip else True,
             "synthetic_seed": int(hip.get("SYNTHETIC_SEED", 0)) if hip else 0,
+            "vit_fp8": bool(hip.get("VIT_FP8", False)) if hip else False,
         }
 
     # ------------------------------------------------------------------ parameters
@@ -129,7 +132,8 @@ class CATSeg(nn.Module):
     def engine(self) -> CatSegEngine:
         if self._engine is None or self._engine.device != self.device:
             dev = self.device if self.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
-            self._engine = CatSegEngine(self.arch, self._sd, dtype=self.compute_dtype, device=dev)
+            self._engine = CatSegEngine(self.arch, self._sd, dtype=self.compute_dtype, device=dev,
+                                        vit_fp8=self.vit_fp8)
             self.sem_seg_head.predictor.attach_engine(self._engine)
         return self._engine
 

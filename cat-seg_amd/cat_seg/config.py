@@ -172,4 +172,5 @@ def add_cat_seg_config(cfg):
     cfg.MODEL.CATSEG_HIP.RETURN_ALL_IMAGES = True  # reference returns batched_inputs[0] only
     cfg.MODEL.CATSEG_HIP.BPE_VOCAB = ""          # path to CLIP's bpe_simple_vocab_16e6.txt.gz
     cfg.MODEL.CATSEG_HIP.SYNTHETIC_SEED = 0      # weights when MODEL.WEIGHTS is empty
+    cfg.MODEL.CATSEG_HIP.VIT_FP8 = False         # config 5: e4m3 CLIP image-encoder GEMMs (bf16 engine)
     return cfg

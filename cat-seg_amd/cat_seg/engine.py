@@ -50,7 +50,7 @@ class _NS(dict):
 
 class CatSegEngine:
     def __init__(self, arch: CatSegArch, state_dict: Dict[str, torch.Tensor], dtype=torch.bfloat16,
-                 device="cuda"):
+                 device="cuda", vit_fp8: bool = False):
         L.require_gpu()
         if arch.hidden_dim != 128 or arch.nheads != 4:
             raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
@@ -60,6 +60,15 @@ class CatSegEngine:
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
         self.split_guidance = True      # bf16: decoder conv guidance half once per image (A/B switch)
         self.device = torch.device(device)
+        # config 5: the CLIP image encoder's block GEMMs (q/k/v, out-proj, c_fc, c_proj) in
+        # OCP e4m3 with per-row scales (catseg_gemm_fp8); bf16 engine only
+        # vit_fp8: True = all four, or an iterable naming the ones to run in fp8
+        names = ("wqkv", "wo", "wfc", "wpr")
+        self.vit_fp8_gemms = (names if vit_fp8 is True else tuple(n for n in names if n in vit_fp8)
+                              if vit_fp8 else ())
+        self.vit_fp8 = bool(self.vit_fp8_gemms)
+        if self.vit_fp8 and dtype != torch.bfloat16:
+            raise ValueError("vit_fp8 needs the bf16 engine")
         self._text = None
         with torch.no_grad():
             self.w = self._prepare(state_dict)
@@ -71,7 +80,15 @@ class CatSegEngine:
     def _F(self, t):
         return t.detach().to(self.device, _f32).contiguous()
 
-    def _block(self, sd, p, dense=False):
+    def _Q8(self, t):
+        """nn.Linear weight [N][K] -> (e4m3 [N][K], fp32 per-row scale [N]), quantized on device."""
+        wf = self._F(t)
+        q = torch.empty(wf.shape, device=self.device, dtype=torch.float8_e4m3fn)
+        sc = torch.empty(wf.shape[0], device=self.device, dtype=_f32)
+        ops.quant_fp8_rows(wf, q, sc)
+        return q, sc
+
+    def _block(self, sd, p, dense=False, fp8=False):
         width = sd[p + "attn.q_proj_weight"].shape[0]
         b = sd[p + "attn.in_proj_bias"]
         blk = _NS(
@@ -87,6 +104,18 @@ class CatSegEngine:
         else:
             blk["wqkv"] = self._W(torch.cat([sd[p + f"attn.{x}_proj_weight"] for x in "qkv"], 0))
             blk["bqkv"] = self._F(b)
+        if fp8:
+            g = self.vit_fp8_gemms
+            if "wo" in g:
+                blk["q8_wo"] = self._Q8(sd[p + "attn.out_proj.weight"])
+            if "wfc" in g:
+                blk["q8_wfc"] = self._Q8(sd[p + "mlp.c_fc.weight"])
+            if "wpr" in g:
+                blk["q8_wpr"] = self._Q8(sd[p + "mlp.c_proj.weight"])
+            if "wqkv" in g and dense:
+                blk["q8_wv"] = self._Q8(sd[p + "attn.v_proj_weight"])
+            elif "wqkv" in g:
+                blk["q8_wqkv"] = self._Q8(torch.cat([sd[p + f"attn.{x}_proj_weight"] for x in "qkv"], 0))
         return blk
 
     @staticmethod
@@ -119,8 +148,8 @@ class CatSegEngine:
             pos = torch.cat([pos[:1], out], 0).contiguous()
         w.pos = pos
         w.ln_pre = (self._F(sd[p + "ln_pre.weight"]), self._F(sd[p + "ln_pre.bias"]))
-        w.vblocks = [self._block(sd, f"{p}transformer.resblocks.{i}.", dense=(i == a.vision_layers - 1))
-                     for i in range(a.vision_layers)]
+        w.vblocks = [self._block(sd, f"{p}transformer.resblocks.{i}.", dense=(i == a.vision_layers - 1),
+                                 fp8=self.vit_fp8) for i in range(a.vision_layers)]
         w.ln_post = (self._F(sd[p + "ln_post.weight"]), self._F(sd[p + "ln_post.bias"]))
         w.proj_t = self._W(sd[p + "proj"].t())
         # ---------------- CLIP text ----------------
@@ -212,7 +241,25 @@ class CatSegEngine:
         return qkv[0, D:2 * D].contiguous(), qkv[0, 2 * D:].contiguous()
 
     # ------------------------------------------------------------------ shared transformer block
-    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None):
+    class _Fp8Linear:
+        """Per-row e4m3 quantization of the activation rows, then catseg_gemm_fp8 (config 5)."""
+
+        def __init__(self, M, width, dev):
+            self.a8 = torch.empty(M, 4 * width, device=dev, dtype=torch.float8_e4m3fn)
+            self.sa = torch.empty(M, device=dev, dtype=_f32)
+
+        def __call__(self, a, wq, out, **kw):
+            a8 = self.a8[:, :a.shape[1]]
+            ops.quant_fp8_rows(a, a8, self.sa)
+            ops.gemm_fp8(a8, self.sa, wq[0], wq[1], out, **kw)
+            return out
+
+    def _linear(self, fp8_lin, a, blk, name, out, **kw):
+        if fp8_lin is not None and "q8_" + name in blk:
+            return fp8_lin(a, blk["q8_" + name], out, **kw)
+        return ops.gemm(a, blk[name], out, **kw)
+
+    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None, fp8=False):
         """ResidualAttentionBlock.forward over a stack (model_vpt.py:208-217, 256-266)."""
         M, width = x.shape
         dt, dev = self.dt, self.device
@@ -220,19 +267,20 @@ class CatSegEngine:
         qkv = torch.empty(M, 3 * width, device=dev, dtype=dt)
         o = torch.empty(M, width, device=dev, dtype=dt)
         u = torch.empty(M, 4 * width, device=dev, dtype=dt)
+        f8 = self._Fp8Linear(M, width, dev) if fp8 else None
         fresh = False
         for i, blk in enumerate(blocks):
             ops.layernorm(x, blk.ln1w, blk.ln1b, h)
-            ops.gemm(h, blk.wqkv, qkv, bias=blk.bqkv)
+            self._linear(f8, h, blk, "wqkv", qkv, bias=blk.bqkv)
             ops.attention(qkv[:, :width], qkv[:, width:2 * width], qkv[:, 2 * width:], o,
                           n_seq=n_seq, seq_len=seq_len, n_heads=n_heads, head_dim=width // n_heads,
                           scale=(width // n_heads) ** -0.5, causal=causal)
             x_new = torch.empty_like(x) if fresh else x
-            ops.gemm(o, blk.wo, x_new, bias=blk.bo, res=x)
+            self._linear(f8, o, blk, "wo", x_new, bias=blk.bo, res=x)
             x = x_new
             ops.layernorm(x, blk.ln2w, blk.ln2b, h)
-            ops.gemm(h, blk.wfc, u, bias=blk.bfc, act=L.ACT_QUICKGELU)
-            ops.gemm(u, blk.wpr, x, bias=blk.bpr, res=x)
+            self._linear(f8, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+            self._linear(f8, u, blk, "wpr", x, bias=blk.bpr, res=x)
             fresh = i in hooks_at
             if fresh:
                 hooks.append(x)
@@ -293,22 +341,23 @@ class CatSegEngine:
         ops.vit_embed(patches, w.cls, w.pos, *w.ln_pre, x, B=B, G2=G2, width=W)
         hooks: List[torch.Tensor] = []
         x = self._resblocks(x, w.vblocks[:-1], B, Lt, a.vision_heads, False,
-                            hooks_at=set(a.hook_layers), hooks=hooks)
+                            hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8)
         if a.vision_layers - 1 in a.hook_layers:
             raise NotImplementedError("hook on the dense block")
         # forward_dense (model_vpt.py:219-240)
         blk = w.vblocks[-1]
         M = B * Lt
+        f8 = self._Fp8Linear(M, W, dev) if self.vit_fp8 else None
         h = torch.empty(M, W, device=dev, dtype=dt)
         ops.layernorm(x, blk.ln1w, blk.ln1b, h)
         v = torch.empty(M, W, device=dev, dtype=dt)
-        ops.gemm(h, blk.wv, v, bias=blk.bv)
+        self._linear(f8, h, blk, "wv", v, bias=blk.bv)
         vo = torch.empty(M, W, device=dev, dtype=_f32)
-        ops.gemm(v, blk.wo, vo, bias=blk.bo, add=x, addmap=rowmap(d1=Lt, s1=Lt))   # + x[:1] (CLS residual)
+        self._linear(f8, v, blk, "wo", vo, bias=blk.bo, add=x, addmap=rowmap(d1=Lt, s1=Lt))   # + x[:1] (CLS residual)
         ops.layernorm(vo, blk.ln2w, blk.ln2b, h)
         u = torch.empty(M, 4 * W, device=dev, dtype=dt)
-        ops.gemm(h, blk.wfc, u, bias=blk.bfc, act=L.ACT_QUICKGELU)
-        ops.gemm(u, blk.wpr, vo, bias=blk.bpr, res=vo)
+        self._linear(f8, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+        self._linear(f8, u, blk, "wpr", vo, bias=blk.bpr, res=vo)
         ops.layernorm(vo, *w.ln_post, h)                                        # ln_post (all tokens)
         feats = torch.empty(M, a.embed_dim, device=dev, dtype=_f32)
         ops.gemm(h, w.proj_t, feats)                                           # @ proj

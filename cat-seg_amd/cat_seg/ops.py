@@ -64,6 +64,8 @@ def _dt(t: torch.Tensor) -> int:
         return L.F32
     if t.dtype == torch.bfloat16:
         return L.BF16
+    if t.dtype == torch.float8_e4m3fn:
+        return L.FP8
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
@@ -108,6 +110,46 @@ def gemm(A, W, out, *, M=None, K=None, bias=None, act=L.ACT_NONE, alpha=1.0,
     kname = "gemm_bf16" if a.dtype_a == L.BF16 else "gemm_f32"
     with _rec(kname, 2 * M * N * K, A.element_size() * (M * K + N * K) + out.element_size() * M * N):
         call("catseg_gemm", a, _stream())
+    return out
+
+
+def quant_fp8_rows(x, q, scale, *, rows=None, cols=None):
+    """Per-row e4m3 quantization (catseg_quant_fp8_rows): scale[r] = max|x[r]| / 448,
+    q[r] = e4m3(x[r] / scale[r]).  q: torch.float8_e4m3fn, scale: fp32 [rows]."""
+    rows = rows if rows is not None else x.shape[0]
+    cols = cols if cols is not None else x.shape[1]
+    with _rec("quant_fp8", 0, rows * cols * (x.element_size() + 1) + 4 * rows):
+        call("catseg_quant_fp8_rows", x.data_ptr(), _dt(x), _ld(x), rows, cols, q.data_ptr(), _ld(q),
+             scale.data_ptr(), _stream())
+    return q, scale
+
+
+def gemm_fp8(A, sa, W, sw, out, *, bias=None, act=L.ACT_NONE, alpha=1.0, add=None, addmap=None,
+             add_ncols=None, res=None, res2=None, amap=None, M=None):
+    """out = epilogue((A8[amap(m)] . W8^T) * sa[amap(m)] * sw[n]) (catseg_gemm_fp8): the config-5 ViT GEMMs.
+    A, W: torch.float8_e4m3fn rows; sa [M], sw [N] fp32 dequant scales."""
+    N, K = W.shape
+    M = M if M is not None else A.shape[0]
+    a = L.GemmArgs()
+    a.A, a.lda, a.amap = A.data_ptr(), _ld(A), amap or IDENTITY
+    a.W, a.ldw = W.data_ptr(), _ld(W)
+    a.M, a.N, a.K = M, N, K
+    a.bias = _p(bias)
+    if add is not None:
+        a.add, a.ld_add = add.data_ptr(), _ld(add)
+        a.addmap = addmap or IDENTITY
+        a.add_ncols = add_ncols if add_ncols is not None else N
+    else:
+        a.addmap = IDENTITY
+    a.act, a.alpha = act, alpha
+    if res is not None:
+        a.res, a.ld_res = res.data_ptr(), _ld(res)
+    if res2 is not None:
+        a.res2, a.ld_res2 = res2.data_ptr(), _ld(res2)
+    a.out, a.ldo = out.data_ptr(), _ld(out)
+    a.dtype_a, a.dtype_out = L.FP8, _dt(out)
+    with _rec("gemm_fp8", 2 * M * N * K, M * K + N * K + out.element_size() * M * N):
+        call("catseg_gemm_fp8", a, sa.data_ptr(), sw.data_ptr(), _stream())
     return out
 
 

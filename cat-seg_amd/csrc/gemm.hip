@@ -37,6 +37,7 @@ struct EpiArgs {
   const void* res2; int64_t ld_res2;
   void* out; int64_t ldo;
   int store_mode; int cvt_k, cvt_hin, cvt_win, cvt_cout;
+  const float* sa; const float* sw;   // fp8 path: per-row scales of A and W (dequant in the epilogue)
 };
 
 template <typename TO>
@@ -391,6 +392,14 @@ DEV void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+DEV i32x8 cat8(i32x4 a, i32x4 b) { return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+// 16x16x128 e4m3 x e4m3 MFMA, unit block scales (E8M0 127 = 2^0)
+DEV f32x4 mfma_fp8x128(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
 template <int BK>
 struct Swz {
   static constexpr int BKC = BK / 8;            // 16-byte chunks per tile row
@@ -398,7 +407,12 @@ struct Swz {
   static DEV int slot(int row, int ch) { return ch ^ ((row / RPB) % BKC); }
 };
 
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+// F8: A and W hold OCP e4m3 bytes, addressed here in 2-byte units (K, lda, ldw, BK halved),
+// so staging, swizzle and LDS-DMA are byte-identical to bf16.  One K=128 block-scaled MFMA
+// (unit scales; fp8 rate = 2x bf16) consumes two 16-byte chunks per lane; A and W fragments
+// read the same chunks, so the k order inside the instruction does not matter.  The
+// epilogue multiplies by sa[m] * sw[n] (per-row dequant scales) before bias / act / residual.
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
                                                             const bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int64_t K, int tiles_n, EpiArgs e) {
@@ -472,24 +486,49 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
     if (kt + S - 1 < ktiles) issue(kt + S - 1);
     const bf16* As = smem + (kt % S) * STAGE;
     const bf16* Ws = As + BM * BK;
+    if constexpr (F8) {
+      static_assert(BK % 64 == 0, "fp8 K-step is 128 bytes");
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int ch = ks * 4 + q;
-      s16x8 bfrag[FM], afrag[FN];
+      for (int ks = 0; ks < BK / 64; ++ks) {
+        const int ch = ks * 8 + 2 * q;
+        i32x8 bfrag[FM], afrag[FN];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int row = wm + 16 * j + r;
-        bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(row * BKC + SW::slot(row, ch)) * 8]);
+        for (int j = 0; j < FM; ++j) {
+          const int row = wm + 16 * j + r;
+          bfrag[j] = cat8(*reinterpret_cast<const i32x4*>(&As[(row * BKC + SW::slot(row, ch)) * 8]),
+                          *reinterpret_cast<const i32x4*>(&As[(row * BKC + SW::slot(row, ch + 1)) * 8]));
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int row = wn + 16 * i + r;
+          afrag[i] = cat8(*reinterpret_cast<const i32x4*>(&Ws[(row * BKC + SW::slot(row, ch)) * 8]),
+                          *reinterpret_cast<const i32x4*>(&Ws[(row * BKC + SW::slot(row, ch + 1)) * 8]));
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma_fp8x128(afrag[i], bfrag[j], acc[i][j]);
       }
+    } else {
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int row = wn + 16 * i + r;
-        afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(row * BKC + SW::slot(row, ch)) * 8]);
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        const int ch = ks * 4 + q;
+        s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int row = wm + 16 * j + r;
+          bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(row * BKC + SW::slot(row, ch)) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int row = wn + 16 * i + r;
+          afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(row * BKC + SW::slot(row, ch)) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
     }
   }
   // ---- epilogue through LDS: rounds of 64 tile rows (JR m-fragments per wave row) are
@@ -516,9 +555,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
       const int lrow = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
       const int wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
       const int64_t m = m0 + wi * WM + (h * JR + jj) * 16 + rr;
-      if (m < M)
-        epilogue8<TO>(e, m, n0 + c8, *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]),
-                      *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]));
+      if (m < M) {
+        f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]);
+        f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]);
+        if constexpr (F8) {
+          const float s = e.sa[ident ? m : rowmap(amap, m)];   // scale of the A row read for m
+          const f32x4 w0 = *reinterpret_cast<const f32x4*>(e.sw + n0 + c8);
+          const f32x4 w1 = *reinterpret_cast<const f32x4*>(e.sw + n0 + c8 + 4);
+          lo = lo * (w0 * s);
+          hi = hi * (w1 * s);
+        }
+        epilogue8<TO>(e, m, n0 + c8, lo, hi);
+      }
     }
   }
 }
@@ -708,6 +756,7 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   e.out = g->out; e.ldo = g->ldo;
   e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
   e.cvt_cout = g->cvt_cout;
+  e.sa = nullptr; e.sw = nullptr;
   return e;
 }
 
@@ -719,6 +768,19 @@ bool launch3(const CatsegGemmArgs* g, hipStream_t st) {
   const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
   hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
                      st, (const bf16*)g->A, g->lda, am, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e);
+  return true;
+}
+
+// fp8: g's K / lda / ldw are in fp8 elements (bytes); the kernel sees 2-byte units
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+bool launch3f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStream_t st) {
+  if (g->N % BN != 0 || (g->K / 2) % BK != 0) return false;
+  EpiArgs e = make_epi(g);
+  e.sa = sa; e.sw = sw;
+  RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
+  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
+  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, true>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN),
+                     0, st, (const bf16*)g->A, g->lda / 2, am, (const bf16*)g->W, g->ldw / 2, g->M, g->K / 2, tn, e);
   return true;
 }
 
@@ -837,9 +899,117 @@ void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
   }
 }
 
+int g_gemm_f8_variant = 0;   // 0 = automatic
+
+// fp8 tiles (sizes in output rows x cols; BK in 2-byte units, i.e. 2x the fp8 K depth)
+template <typename TO>
+bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStream_t st) {
+  int v = g_gemm_f8_variant;
+  if (v == 0) {
+    // same wave-quantization rule as the bf16 tiles (one round of <= 256 tiles)
+    const int64_t t224 = ((g->M + 223) / 224) * (g->N / 256);
+    const int64_t t160 = ((g->M + 159) / 160) * (g->N / 128);
+    if (g->N % 256 == 0 && g->K % 128 == 0 && t224 >= 200 && t224 <= 256) v = 20;
+    else if (g->N % 128 == 0 && g->K % 256 == 0 && t160 >= 160 && t160 <= 256) v = 15;
+    else if (g->N % 128 == 0 && g->K % 128 == 0 && t160 > 256) v = 17;
+    else if (g->N % 128 == 0 && g->K % 128 == 0) v = 19;
+    else return false;
+  }
+  switch (v) {
+    case 1: return launch3f8<TO, 256, 256, 2, 4, 2, 64>(g, sa, sw, st);
+    case 15: return launch3f8<TO, 160, 128, 2, 4, 2, 128>(g, sa, sw, st);
+    case 17: return launch3f8<TO, 160, 128, 2, 4, 2, 64>(g, sa, sw, st);
+    case 19: return launch3f8<TO, 128, 128, 2, 4, 2, 64>(g, sa, sw, st);
+    case 20: return launch3f8<TO, 224, 256, 2, 4, 2, 64>(g, sa, sw, st);
+    case 21: return launch3f8<TO, 160, 128, 2, 4, 3, 64>(g, sa, sw, st);
+    case 23: return launch3f8<TO, 160, 256, 2, 4, 3, 64>(g, sa, sw, st);
+    case 24: return launch3f8<TO, 160, 256, 2, 4, 2, 64>(g, sa, sw, st);
+    default: return false;
+  }
+}
+
+// per-row e4m3 quantization: one wave per row, amax -> scale = amax / 448,
+// q = rne_e4m3(x * (448 / amax)) (|x * inv| <= 448 by construction; clamped anyway)
+template <typename TI>
+__global__ __launch_bounds__(256) void quant_rows_kernel(const TI* __restrict__ x, int64_t ldx, int64_t rows,
+                                                         int64_t cols, uint8_t* __restrict__ q, int64_t ldq,
+                                                         float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* xr = x + row * ldx;
+  float amax = 0.f;
+  for (int64_t c = lane * 4; c < cols; c += 256) {
+    float v[4];
+    load4<TI>(xr + c, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  }
+  amax = warp_max(amax);
+  amax = fmaxf(amax, 1e-30f);
+  const float inv = 448.f / amax;
+  if (lane == 0) scale[row] = amax / 448.f;
+  uint8_t* qr = q + row * ldq;
+  for (int64_t c = lane * 4; c < cols; c += 256) {
+    float v[4];
+    load4<TI>(xr + c, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = fminf(fmaxf(v[i] * inv, -448.f), 448.f);
+    int p = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    p = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], p, true);
+    *reinterpret_cast<int*>(qr + c) = p;
+  }
+}
+
 }  // namespace
 
 extern "C" void catseg_set_gemm_variant(int v) { g_gemm_variant = v; }
+extern "C" void catseg_set_gemm_fp8_variant(int v) { g_gemm_f8_variant = v; }
+
+extern "C" int catseg_quant_fp8_rows(const void* x, int dtype, int64_t ld_x, int64_t rows, int64_t cols, void* q,
+                                     int64_t ld_q, float* scale, void* stream) {
+  CATSEG_CHECK(x && q && scale, "quant_fp8_rows: null pointer");
+  CATSEG_CHECK(rows > 0 && cols > 0, "quant_fp8_rows: empty shape");
+  CATSEG_CHECK(cols % 4 == 0 && ld_x % 4 == 0 && ld_q % 4 == 0, "quant_fp8_rows: cols / ld must be multiples of 4");
+  CATSEG_CHECK(dtype == CATSEG_BF16 || dtype == CATSEG_F32, "quant_fp8_rows: dtype must be f32 or bf16");
+  const int esz = dtype == CATSEG_BF16 ? 2 : 4;
+  CATSEG_CHECK(((uintptr_t)x % (4 * esz)) == 0 && ((uintptr_t)q % 4) == 0, "quant_fp8_rows: misaligned pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)((rows + 3) / 4);
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(quant_rows_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, ld_x, rows, cols,
+                       (uint8_t*)q, ld_q, scale);
+  else
+    hipLaunchKernelGGL(quant_rows_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, ld_x, rows, cols,
+                       (uint8_t*)q, ld_q, scale);
+  return catseg_launch_status("quant_fp8_rows");
+}
+
+extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {
+  CATSEG_CHECK(g && g->A && g->W && g->out && scale_a && scale_w, "gemm_fp8: null pointer");
+  CATSEG_CHECK(g->dtype_a == CATSEG_FP8, "gemm_fp8: dtype_a must be CATSEG_FP8");
+  CATSEG_CHECK(g->M > 0 && g->N > 0 && g->K > 0, "gemm_fp8: empty shape");
+  CATSEG_CHECK(g->K % 128 == 0 && g->lda % 16 == 0 && g->ldw % 16 == 0, "gemm_fp8: K must be a multiple of 128, lda/ldw of 16");
+  CATSEG_CHECK(g->N % 128 == 0, "gemm_fp8: N must be a multiple of 128");
+  CATSEG_CHECK(((uintptr_t)g->A % 16) == 0 && ((uintptr_t)g->W % 16) == 0 && ((uintptr_t)scale_w % 16) == 0,
+               "gemm_fp8: A/W/scale_w must be 16B aligned");
+  CATSEG_CHECK(g->store_mode == 0, "gemm_fp8: row-major store only");
+  CATSEG_CHECK(g->ldo % 8 == 0 && ((uintptr_t)g->out % 16) == 0, "gemm_fp8: out rows must be 16B aligned");
+  CATSEG_CHECK(!g->res || (g->ld_res % 8 == 0 && ((uintptr_t)g->res % 16) == 0), "gemm_fp8: res rows must be 16B aligned");
+  CATSEG_CHECK(!g->res2 || (g->ld_res2 % 8 == 0 && ((uintptr_t)g->res2 % 16) == 0), "gemm_fp8: res2 rows must be 16B aligned");
+  CATSEG_CHECK(!g->add || (g->add_ncols % 8 == 0 && g->ld_add % 8 == 0 && ((uintptr_t)g->add % 16) == 0),
+               "gemm_fp8: add rows must be 16B aligned");
+  CATSEG_CHECK(g->amap.d1 > 0 && g->amap.m1 > 0 && g->amap.d2 > 0 && g->amap.m2 > 0, "gemm_fp8: bad amap");
+  CATSEG_CHECK(!g->add || (g->addmap.d1 > 0 && g->addmap.m1 > 0 && g->addmap.d2 > 0 && g->addmap.m2 > 0),
+               "gemm_fp8: bad addmap");
+  hipStream_t st = (hipStream_t)stream;
+  bool ok;
+  if (g->dtype_out == CATSEG_BF16) ok = launch_f8<bf16>(g, scale_a, scale_w, st);
+  else if (g->dtype_out == CATSEG_F32) ok = launch_f8<float>(g, scale_a, scale_w, st);
+  else CATSEG_FAIL("gemm_fp8: dtype_out must be f32 or bf16");
+  CATSEG_CHECK(ok, "gemm_fp8: no tile fits this shape / variant");
+  return catseg_launch_status("gemm_fp8");
+}
 
 extern "C" int catseg_gemm(const CatsegGemmArgs* g, void* stream) {
   CATSEG_CHECK(g && g->A && g->W && g->out, "gemm: null pointer");

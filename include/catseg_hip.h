@@ -25,7 +25,7 @@ extern "C" {
 #endif
 
 enum { CATSEG_OK = 0, CATSEG_ERR_ARG = -1, CATSEG_ERR_HIP = -2 };
-enum { CATSEG_F32 = 0, CATSEG_BF16 = 1 };
+enum { CATSEG_F32 = 0, CATSEG_BF16 = 1, CATSEG_FP8 = 2 /* OCP e4m3fn bytes */ };
 enum { CATSEG_ACT_NONE = 0, CATSEG_ACT_RELU = 1, CATSEG_ACT_GELU = 2, CATSEG_ACT_QUICKGELU = 3,
        CATSEG_ACT_SIGMOID = 4 };
 
@@ -64,6 +64,23 @@ typedef struct {
   int dtype_a, dtype_out;
 } CatsegGemmArgs;
 int catseg_gemm(const CatsegGemmArgs* args, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * fp8 ViT GEMMs ("fp8 MFMA ViT GEMMs").  The reference runs the
+ * same nn.Linear calls (model_vpt.py:193-236) in fp32/fp16; here A and W are OCP e4m3
+ * with one fp32 dequant scale per row of each (scale_a [M], scale_w [N], 16B aligned):
+ *   out = epilogue( (A8[r,:] . W8[n,:]) * scale_a[r] * scale_w[n] ), r = amap(m)   (epilogue as catseg_gemm)
+ * dtype_a = CATSEG_FP8; K, lda, ldw in bytes (K % 128 == 0); N % 128 == 0; row-major
+ * store only; dtype_out f32 or bf16.  Block-scaled K=128 MFMA at unit block scales.
+ * ------------------------------------------------------------------------- */
+int catseg_gemm_fp8(const CatsegGemmArgs* args, const float* scale_a, const float* scale_w, void* stream);
+
+/* Per-row e4m3 quantization: scale[r] = max|x[r,:]| / 448, q[r,c] = rne_e4m3(x[r,c] / scale[r]).
+ * x: f32 or bf16 (dtype), q: bytes.  cols, ld_x, ld_q multiples of 4.  Used for the
+ * weights at load and the activations ahead of catseg_gemm_fp8. */
+int catseg_quant_fp8_rows(const void* x, int dtype, int64_t ld_x, int64_t rows, int64_t cols, void* q,
+                          int64_t ld_q, float* scale, void* stream);
+void catseg_set_gemm_fp8_variant(int variant);
 
 /* Tile selection of the bf16 GEMM: 0 = automatic (default), -1 = never the LDS-DMA
  * pipelined kernel, 1..8 = force one of its tile / stage / K-depth configurations

@@ -120,6 +120,89 @@ def test_gemm_pipelined_variants(variant):
         lib.catseg_set_gemm_variant(0)
 
 
+# ----------------------------------------------------------------------------- fp8 (config 5)
+def _quant_ref(x):
+    """Per-row e4m3 quantization as catseg_quant_fp8_rows defines it (fp32 arithmetic, RNE)."""
+    x = x.float()
+    amax = x.abs().amax(dim=1).clamp_min(1e-30)
+    inv = torch.tensor(448.0) / amax
+    q = (x * inv[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q, amax / 448.0
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 1024), (300, 4096), (5, 260)])
+def test_quant_fp8_rows_bit_exact(dt, rows, cols):
+    """catseg_quant_fp8_rows vs torch's RNE float8_e4m3fn conversion: identical bytes and scales;
+    a zero row and a row with a single huge value included."""
+    x = rnd(rows, cols, seed=70, scale=3.0)
+    x[0, : min(cols, 4)] = torch.tensor([1e4, -2.0, 0.5, 3.0])[: min(cols, 4)]
+    if rows > 2:
+        x[2] = 0.0
+    x = x.to(dt)
+    q = torch.empty(rows, cols, device=dev, dtype=torch.float8_e4m3fn)
+    sc = torch.empty(rows, device=dev, dtype=torch.float32)
+    ops.quant_fp8_rows(x.to(dev), q, sc)
+    qr, sr = _quant_ref(x)
+    assert torch.equal(sc.cpu(), sr), (sc.cpu() - sr).abs().max()
+    assert torch.equal(q.cpu().view(torch.uint8), qr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 15, 17, 19, 20, 21, 23, 24])
+def test_gemm_fp8_variants(variant):
+    """catseg_gemm_fp8 (block-scaled K=128 MFMA over e4m3 rows) against fp64 products of the
+    dequantized operands: ragged M with a CLS-dropping row map, bias + QuickGELU / fp32 residual."""
+    B, L_, K, N = 3, 401, 1024, 768
+    M = B * (L_ - 1)
+    A = rnd(B * L_, K, seed=50)
+    W = rnd(N, K, seed=51) / math.sqrt(K)
+    b = rnd(N, seed=52)
+    res = rnd(M, N, seed=53)
+    qa, sa = _quant_ref(A)
+    qw, sw = _quant_ref(W)
+    amap = rowmap(d1=L_ - 1, s1=L_, d2=1, m2=L_ - 1, s2=1, off=1)
+    ad = (qa.double() * sa.double()[:, None]).reshape(B, L_, K)[:, 1:].reshape(-1, K)
+    wd = qw.double() * sw.double()[:, None]
+    lib = L.load()
+    try:
+        lib.catseg_set_gemm_fp8_variant(variant)
+        for act, odt in ((L.ACT_QUICKGELU, torch.bfloat16), (L.ACT_NONE, torch.float32)):
+            out = torch.full((M, N), float("nan"), device=dev, dtype=odt)
+            r = res.to(dev, odt)
+            ops.gemm_fp8(qa.to(dev), sa.to(dev), qw.to(dev), sw.to(dev), out, M=M, bias=b.to(dev), act=act,
+                         res=r, amap=amap)
+            v = ad @ wd.T + b.double()
+            if act == L.ACT_QUICKGELU:
+                v = v * torch.sigmoid(1.702 * v)
+            ref = v + r.double().cpu()
+            close(out, ref, atol=1e-4 if odt == torch.float32 else 2e-2, rtol=0 if odt == torch.float32 else 1e-2,
+                  what=f"gemm_fp8 variant {variant} act {act}")
+    finally:
+        lib.catseg_set_gemm_fp8_variant(0)
+
+
+def test_gemm_fp8_vit_shapes_vs_bf16():
+    """The ViT-L/14 block shapes (M = 8 x 577) through the automatic fp8 tile choice: the
+    dequantized-operand product to fp32 accuracy, and within e4m3 error of the bf16 GEMM."""
+    M = 8 * 577
+    for N, K in ((3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096)):
+        A = rnd(M, K, seed=N + K)
+        W = rnd(N, K, seed=N + K + 1) / math.sqrt(K)
+        qa = torch.empty(M, K, device=dev, dtype=torch.float8_e4m3fn)
+        sa = torch.empty(M, device=dev)
+        qw = torch.empty(N, K, device=dev, dtype=torch.float8_e4m3fn)
+        sw = torch.empty(N, device=dev)
+        ops.quant_fp8_rows(A.to(dev, torch.bfloat16), qa, sa)
+        ops.quant_fp8_rows(W.to(dev), qw, sw)
+        out = torch.empty(M, N, device=dev)
+        ops.gemm_fp8(qa, sa, qw, sw, out)
+        ref = (qa.cpu().double() * sa.cpu().double()[:, None]) @ (qw.cpu().double() * sw.cpu().double()[:, None]).T
+        close(out, ref, atol=1e-4, what=f"gemm_fp8 {M}x{N}x{K}")
+        exact = A.to(torch.bfloat16).double() @ W.double().T
+        rel = ((out.cpu().double() - exact).norm() / exact.norm()).item()
+        assert rel < 0.05, f"fp8 vs exact relative error {rel}"
+
+
 def test_gemm_amap_cls_drop():
     B, L_, C = 2, 5, 16
     A = rnd(B * L_, C, seed=13)
