@@ -254,6 +254,20 @@ class CatSegEngine:
             ops.gemm_fp8(a8, self.sa, wq[0], wq[1], out, **kw)
             return out
 
+        def ln(self, x, g, b, wq, out, **kw):
+            """LayerNorm straight to e4m3 rows, then the GEMM (no bf16 round trip)."""
+            a8 = self.a8[:, :x.shape[1]]
+            ops.layernorm_fp8(x, g, b, a8, self.sa)
+            ops.gemm_fp8(a8, self.sa, wq[0], wq[1], out, **kw)
+            return out
+
+    def _ln_linear(self, fp8_lin, x, g, b, h, blk, name, out, **kw):
+        """LN(x) -> linear; fp8 GEMMs take the LayerNorm output as e4m3 rows directly."""
+        if fp8_lin is not None and "q8_" + name in blk:
+            return fp8_lin.ln(x, g, b, blk["q8_" + name], out, **kw)
+        ops.layernorm(x, g, b, h)
+        return self._linear(fp8_lin, h, blk, name, out, **kw)
+
     def _linear(self, fp8_lin, a, blk, name, out, **kw):
         if fp8_lin is not None and "q8_" + name in blk:
             return fp8_lin(a, blk["q8_" + name], out, **kw)
@@ -270,16 +284,14 @@ class CatSegEngine:
         f8 = self._Fp8Linear(M, width, dev) if fp8 else None
         fresh = False
         for i, blk in enumerate(blocks):
-            ops.layernorm(x, blk.ln1w, blk.ln1b, h)
-            self._linear(f8, h, blk, "wqkv", qkv, bias=blk.bqkv)
+            self._ln_linear(f8, x, blk.ln1w, blk.ln1b, h, blk, "wqkv", qkv, bias=blk.bqkv)
             ops.attention(qkv[:, :width], qkv[:, width:2 * width], qkv[:, 2 * width:], o,
                           n_seq=n_seq, seq_len=seq_len, n_heads=n_heads, head_dim=width // n_heads,
                           scale=(width // n_heads) ** -0.5, causal=causal)
             x_new = torch.empty_like(x) if fresh else x
             self._linear(f8, o, blk, "wo", x_new, bias=blk.bo, res=x)
             x = x_new
-            ops.layernorm(x, blk.ln2w, blk.ln2b, h)
-            self._linear(f8, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+            self._ln_linear(f8, x, blk.ln2w, blk.ln2b, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
             self._linear(f8, u, blk, "wpr", x, bias=blk.bpr, res=x)
             fresh = i in hooks_at
             if fresh:
@@ -349,14 +361,12 @@ class CatSegEngine:
         M = B * Lt
         f8 = self._Fp8Linear(M, W, dev) if self.vit_fp8 else None
         h = torch.empty(M, W, device=dev, dtype=dt)
-        ops.layernorm(x, blk.ln1w, blk.ln1b, h)
         v = torch.empty(M, W, device=dev, dtype=dt)
-        self._linear(f8, h, blk, "wv", v, bias=blk.bv)
+        self._ln_linear(f8, x, blk.ln1w, blk.ln1b, h, blk, "wv", v, bias=blk.bv)
         vo = torch.empty(M, W, device=dev, dtype=_f32)
         self._linear(f8, v, blk, "wo", vo, bias=blk.bo, add=x, addmap=rowmap(d1=Lt, s1=Lt))   # + x[:1] (CLS residual)
-        ops.layernorm(vo, blk.ln2w, blk.ln2b, h)
         u = torch.empty(M, 4 * W, device=dev, dtype=dt)
-        self._linear(f8, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
+        self._ln_linear(f8, vo, blk.ln2w, blk.ln2b, h, blk, "wfc", u, bias=blk.bfc, act=L.ACT_QUICKGELU)
         self._linear(f8, u, blk, "wpr", vo, bias=blk.bpr, res=vo)
         ops.layernorm(vo, *w.ln_post, h)                                        # ln_post (all tokens)
         feats = torch.empty(M, a.embed_dim, device=dev, dtype=_f32)

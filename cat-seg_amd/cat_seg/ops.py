@@ -124,6 +124,16 @@ def quant_fp8_rows(x, q, scale, *, rows=None, cols=None):
     return q, scale
 
 
+def layernorm_fp8(x, gamma, beta, q, scale, *, rows=None, inmap=None, eps=1e-5):
+    """LayerNorm straight to per-row e4m3 (catseg_layernorm_fp8)."""
+    cols = gamma.shape[0]
+    rows = rows if rows is not None else q.shape[0]
+    with _rec("layernorm_fp8", 0, rows * cols * (x.element_size() + 1) + 4 * rows):
+        call("catseg_layernorm_fp8", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), q.data_ptr(), _ld(q),
+             scale.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rows, cols, eps, _stream())
+    return q, scale
+
+
 def gemm_fp8(A, sa, W, sw, out, *, bias=None, act=L.ACT_NONE, alpha=1.0, add=None, addmap=None,
              add_ncols=None, res=None, res2=None, amap=None, M=None):
     """out = epilogue((A8[amap(m)] . W8^T) * sa[amap(m)] * sw[n]) (catseg_gemm_fp8): the config-5 ViT GEMMs.

@@ -928,62 +928,10 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
   }
 }
 
-// per-row e4m3 quantization: one wave per row, amax -> scale = amax / 448,
-// q = rne_e4m3(x * (448 / amax)) (|x * inv| <= 448 by construction; clamped anyway)
-template <typename TI>
-__global__ __launch_bounds__(256) void quant_rows_kernel(const TI* __restrict__ x, int64_t ldx, int64_t rows,
-                                                         int64_t cols, uint8_t* __restrict__ q, int64_t ldq,
-                                                         float* __restrict__ scale) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const TI* xr = x + row * ldx;
-  float amax = 0.f;
-  for (int64_t c = lane * 4; c < cols; c += 256) {
-    float v[4];
-    load4<TI>(xr + c, v);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(v[i]));
-  }
-  amax = warp_max(amax);
-  amax = fmaxf(amax, 1e-30f);
-  const float inv = 448.f / amax;
-  if (lane == 0) scale[row] = amax / 448.f;
-  uint8_t* qr = q + row * ldq;
-  for (int64_t c = lane * 4; c < cols; c += 256) {
-    float v[4];
-    load4<TI>(xr + c, v);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = fminf(fmaxf(v[i] * inv, -448.f), 448.f);
-    int p = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
-    p = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], p, true);
-    *reinterpret_cast<int*>(qr + c) = p;
-  }
-}
-
 }  // namespace
 
 extern "C" void catseg_set_gemm_variant(int v) { g_gemm_variant = v; }
 extern "C" void catseg_set_gemm_fp8_variant(int v) { g_gemm_f8_variant = v; }
-
-extern "C" int catseg_quant_fp8_rows(const void* x, int dtype, int64_t ld_x, int64_t rows, int64_t cols, void* q,
-                                     int64_t ld_q, float* scale, void* stream) {
-  CATSEG_CHECK(x && q && scale, "quant_fp8_rows: null pointer");
-  CATSEG_CHECK(rows > 0 && cols > 0, "quant_fp8_rows: empty shape");
-  CATSEG_CHECK(cols % 4 == 0 && ld_x % 4 == 0 && ld_q % 4 == 0, "quant_fp8_rows: cols / ld must be multiples of 4");
-  CATSEG_CHECK(dtype == CATSEG_BF16 || dtype == CATSEG_F32, "quant_fp8_rows: dtype must be f32 or bf16");
-  const int esz = dtype == CATSEG_BF16 ? 2 : 4;
-  CATSEG_CHECK(((uintptr_t)x % (4 * esz)) == 0 && ((uintptr_t)q % 4) == 0, "quant_fp8_rows: misaligned pointer");
-  hipStream_t st = (hipStream_t)stream;
-  const unsigned grid = (unsigned)((rows + 3) / 4);
-  if (dtype == CATSEG_BF16)
-    hipLaunchKernelGGL(quant_rows_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, ld_x, rows, cols,
-                       (uint8_t*)q, ld_q, scale);
-  else
-    hipLaunchKernelGGL(quant_rows_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, ld_x, rows, cols,
-                       (uint8_t*)q, ld_q, scale);
-  return catseg_launch_status("quant_fp8_rows");
-}
 
 extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {
   CATSEG_CHECK(g && g->A && g->W && g->out && scale_a && scale_w, "gemm_fp8: null pointer");

@@ -76,10 +76,16 @@ int catseg_gemm(const CatsegGemmArgs* args, void* stream);
 int catseg_gemm_fp8(const CatsegGemmArgs* args, const float* scale_a, const float* scale_w, void* stream);
 
 /* Per-row e4m3 quantization: scale[r] = max|x[r,:]| / 448, q[r,c] = rne_e4m3(x[r,c] / scale[r]).
- * x: f32 or bf16 (dtype), q: bytes.  cols, ld_x, ld_q multiples of 4.  Used for the
+ * x: f32 or bf16 (dtype), q: bytes.  cols <= 4096; cols, ld_x, ld_q multiples of 8.  Used for the
  * weights at load and the activations ahead of catseg_gemm_fp8. */
 int catseg_quant_fp8_rows(const void* x, int dtype, int64_t ld_x, int64_t rows, int64_t cols, void* q,
                           int64_t ld_q, float* scale, void* stream);
+/* LayerNorm straight to e4m3 rows (ln_1 / ln_2 ahead of the fp8 QKV / c_fc GEMMs,
+ * model_vpt.py:208-217): y = LN(x[inmap(r)]) in fp32 as catseg_layernorm, then quantized as
+ * catseg_quant_fp8_rows.  cols <= 4096, multiples of 8. */
+int catseg_layernorm_fp8(const void* x, int64_t ld_x, CatsegRowMap inmap, int dtype_x, void* q, int64_t ld_q,
+                         float* scale, const float* gamma, const float* beta, int64_t rows, int64_t cols, float eps,
+                         void* stream);
 void catseg_set_gemm_fp8_variant(int variant);
 
 /* Tile selection of the bf16 GEMM: 0 = automatic (default), -1 = never the LDS-DMA

@@ -131,12 +131,12 @@ def _quant_ref(x):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 1024), (300, 4096), (5, 260)])
+@pytest.mark.parametrize("rows,cols", [(1, 8), (37, 1024), (300, 4096), (5, 264)])
 def test_quant_fp8_rows_bit_exact(dt, rows, cols):
     """catseg_quant_fp8_rows vs torch's RNE float8_e4m3fn conversion: identical bytes and scales;
     a zero row and a row with a single huge value included."""
     x = rnd(rows, cols, seed=70, scale=3.0)
-    x[0, : min(cols, 4)] = torch.tensor([1e4, -2.0, 0.5, 3.0])[: min(cols, 4)]
+    x[0, :4] = torch.tensor([1e4, -2.0, 0.5, 3.0])
     if rows > 2:
         x[2] = 0.0
     x = x.to(dt)
@@ -146,6 +146,29 @@ def test_quant_fp8_rows_bit_exact(dt, rows, cols):
     qr, sr = _quant_ref(x)
     assert torch.equal(sc.cpu(), sr), (sc.cpu() - sr).abs().max()
     assert torch.equal(q.cpu().view(torch.uint8), qr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_fp8(dt):
+    """catseg_layernorm_fp8 (LN in fp32, then per-row e4m3) vs fp64 LayerNorm through a
+    CLS-dropping row map: scales to fp32 rounding, values within one e4m3 rounding step."""
+    B, L_, C = 3, 7, 1024
+    x = rnd(B * L_, C, seed=80, scale=2.0) + 0.5
+    g = rnd(C, seed=81) + 1.0
+    b = rnd(C, seed=82) * 0.1
+    M = B * (L_ - 1)
+    amap = rowmap(d1=L_ - 1, s1=L_, d2=1, m2=L_ - 1, s2=1, off=1)
+    q = torch.empty(M, C, device=dev, dtype=torch.float8_e4m3fn)
+    sc = torch.empty(M, device=dev)
+    ops.layernorm_fp8(x.to(dev, dt), g.to(dev), b.to(dev), q, sc, rows=M, inmap=amap)
+    xr = x.to(dt).double().reshape(B, L_, C)[:, 1:].reshape(-1, C)
+    ln = F.layer_norm(xr, (C,), g.double(), b.double(), eps=1e-5)
+    sref = ln.abs().amax(dim=1) / 448
+    close(sc, sref, atol=0, rtol=1e-5, what="layernorm_fp8 scale")
+    deq = q.cpu().double() * sc.cpu().double()[:, None]
+    err = (deq - ln).abs()
+    tol = ln.abs() * 2.0 ** -4 + sref[:, None] * 2.0 ** -9 * 1.01
+    assert (err <= tol).all(), (err - tol).max()
 
 
 @pytest.mark.parametrize("variant", [0, 1, 15, 17, 19, 20, 21, 23, 24])
