@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--cpu-images", type=int, default=4, help="oracle sample size for cpu_baseline (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
+                    help="3 = the headline (L/14@336, T=150, bf16); 5 = sliding-window 640², pc459 classes, "
+                         "fp8 ViT GEMMs (SURVEY §8 config 5)")
     ap.add_argument("--vit-fp8", action="store_true",
                     help="config 5's e4m3 CLIP image-encoder GEMMs (not the headline: the headline is bf16)")
     return ap.parse_args()
@@ -62,7 +65,7 @@ def parse():
 
 def class_tokens(T):
     g = np.load(os.path.join(ROOT, "tests", "golden", "class_tokens.npz"))
-    tok = g["ade150"] if T <= 150 else g["ade847"]
+    tok = g["ade150"] if T <= 150 else g["pc459"] if T <= 459 else g["ade847"]
     return torch.from_numpy(tok[:T].astype(np.int32))
 
 
@@ -77,6 +80,13 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     arch = VIT_L14_336
+    cfg5 = args.config == 5
+    if cfg5:
+        if world > 1:
+            raise SystemExit("--config 5 is a single-GPU measurement (the scaling runs use the headline config)")
+        args.vit_fp8 = True
+        if args.classes == 150:
+            args.classes = 459
     B, T = args.batch, args.classes
     R = arch.clip_resolution
 
@@ -86,15 +96,19 @@ def main():
         text = eng.encode_text(class_tokens(T))
         eng.set_text(text)
     gen = torch.Generator().manual_seed(1234 + rank)
-    pad = (R + 31) // 32 * 32
+    S = 640 if cfg5 else R          # config 5: 640² images through the sliding-window branch
+    pad = (S + 31) // 32 * 32
     raw = torch.zeros(B, 3, pad, pad)
-    raw[:, :, :R, :R] = torch.rand(B, 3, R, R, generator=gen) * 255
+    raw[:, :, :S, :S] = torch.rand(B, 3, S, S, generator=gen) * 255
     raw = raw.to(dev)
-    sizes = torch.tensor([[R, R]] * B, dtype=torch.int32, device=dev)
-    out = torch.empty(B, T, R, R, device=dev)
-    gathered = torch.empty(world * B, T, 4 * arch.grid, 4 * arch.grid, device=dev) if world > 1 else None
+    sizes = torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev)
+    out = None if cfg5 else torch.empty(B, T, R, R, device=dev)
+    gsize = eng.SLIDE_OUT if cfg5 else 4 * arch.grid
+    gathered = torch.empty(world * B, T, gsize, gsize, device=dev) if world > 1 else None
 
     def step():
+        if cfg5:      # crops + head + Fold merge -> 640² probabilities at the image size (sem_seg_postprocess)
+            return eng.forward_sliding(raw, sizes, [(S, S)] * B)[0]
         logits = eng.head_logits(raw, sizes)
         ops.postprocess(logits, out, crop=(min(logits.shape[-2], R), min(logits.shape[-1], R)))
         return logits
@@ -150,23 +164,30 @@ def main():
         roofline, kernels = roofline_pass(step, stream, dtype)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_images > 0:
-        cpu = cpu_baseline(arch, sd, text.cpu(), args.cpu_images)
+        cpu = (cpu_baseline_sliding(arch, sd, text.cpu()) if cfg5 else
+               cpu_baseline(arch, sd, text.cpu(), args.cpu_images))
     if rank == 0:
         path_tflops = GF_PER_IMAGE * value / 1e3
         line = {
-            "metric": "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling",
+            "metric": ("images/sec @ ViT-L/14 sliding-window 640² (5 crops/image), 459 classes, fp8 ViT GEMMs "
+                       "(SURVEY §8 config 5; not the headline)" if cfg5 else
+                       "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling"),
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype + ("+fp8e4m3 ViT GEMMs" if args.vit_fp8 else ""),
-            "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, ade150 prompt tokens)",
-            "config": {"workload": f"CATSeg eval forward ViT-L/14@336, T={T} classes, bs={B}/GPU, "
-                                   "POOLING [1,1], sigmoid upsampled to 336x336",
+            "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, "
+                    f"{'pc459' if cfg5 else 'ade150'} prompt tokens)",
+            "config": {"workload": (f"CATSeg eval forward, TEST.SLIDING_WINDOW: {B} images/GPU of 640², "
+                                    f"{5 * B} crops through ViT-L/14@336, T={T} (top-256 per crop), "
+                                    "Fold/avg merge to 640² probabilities" if cfg5 else
+                                    f"CATSeg eval forward ViT-L/14@336, T={T} classes, bs={B}/GPU, "
+                                    "POOLING [1,1], sigmoid upsampled to 336x336"),
                        "global_batch": world * B, "classes": T, "resolution": R,
                        "parallelism": f"batch-shard x{world} + RCCL all-gather of logits" if world > 1 else "1 GPU",
                        "hipgraph": graph is not None},
             "roofline": roofline,
-            "path_roofline": {"bound": "mfma", "achieved": round(path_tflops, 2),
+            "path_roofline": None if cfg5 else {"bound": "mfma", "achieved": round(path_tflops, 2),
                               "peak": PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS,
                               "unit": "TFLOP/s", "gf_per_image": GF_PER_IMAGE,
                               "frac": round(path_tflops / (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
@@ -231,6 +252,22 @@ def roofline_pass(step, stream, dtype):
                 "tflops": round(v["flops"] / (v["ms"] / 1e3) / 1e12, 2) if v["flops"] else None}
             for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])}
     return roof, kern
+
+
+def cpu_baseline_sliding(arch, sd, text):
+    """The oracle's sliding-window branch on one 640² image (config 5's CPU baseline)."""
+    from oracle import catseg_oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(99)
+    inp = [{"image": torch.rand(3, 640, 640, generator=gen) * 255}]
+    t0 = time.perf_counter()
+    O.catseg_forward_sliding(arch, sd, inp, text.unsqueeze(1))
+    dt = time.perf_counter() - t0
+    return {"value": round(1 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 image of the same workload (640² sliding, 5 crops, L/14@336, T={text.shape[0]}, fp32) "
+                      f"through oracle/catseg_oracle.py on {threads} host threads, {dt:.1f} s"}
 
 
 def cpu_baseline(arch, sd, text, n_images):

@@ -629,6 +629,9 @@ class CatSegEngine:
         res = self.SLIDE_OUT
         outs = []
         for n, (H, W) in enumerate(out_hw):
+            if (H, W) == (res, res):      # same-size bilinear (align_corners=False) is the identity
+                outs.append(merged[n])
+                continue
             o = torch.empty(1, merged.shape[1], H, W, device=self.device, dtype=_f32)
             ops.resize_bilinear(merged[n:n + 1], o, crop=(res, res))
             outs.append(o[0])

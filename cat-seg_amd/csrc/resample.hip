@@ -169,6 +169,91 @@ __global__ void sliding_merge_kernel(const float* __restrict__ lg, int64_t N, in
   }
 }
 
+// Banded form of the same merge: one workgroup per (image, class) plane and BY output rows.
+// The global crop's sigmoid(interp 96 -> k) values under the band (<= BY + 2 rows of k) are
+// formed once into LDS, so each output pixel blends 4 LDS values instead of re-deriving 4
+// sigmoids from the 96² plane (the k-res map is 2.8x oversampled at out_res = 640, k = 384);
+// the tile terms (1-4 per pixel, at native resolution) come straight from the L2-resident
+// planes.  Sigmoid and the Fold average use the hardware exp / reciprocal (~1e-7 relative).
+constexpr int MERGE_BY = 16, MERGE_KMAX = 512;
+
+// hardware exp / reciprocal (~1 ulp each): the merge is VALU-bound on ~3 sigmoids per pixel
+DEV float sigm_fast(float v) { return __builtin_amdgcn_rcpf(1.f + __expf(-v)); }
+DEV float up_sig_fast(const float* __restrict__ pl, int h, int w, int k, int y, int x) {
+  int y0, y1, x0, x1;
+  float ly, lx;
+  lin_src(y, h, (float)h / (float)k, y0, y1, ly);
+  lin_src(x, w, (float)w / (float)k, x0, x1, lx);
+  return sigm_fast(blend(pl[y0 * w + x0], pl[y0 * w + x1], pl[y1 * w + x0], pl[y1 * w + x1], ly, lx));
+}
+
+__global__ __launch_bounds__(256) void sliding_merge_band_kernel(const float* __restrict__ lg, int T, int h, int w,
+                                                                 int k, int stride, int nb, int out_res, int bands,
+                                                                 float* __restrict__ out) {
+  extern __shared__ float gsig[];     // (rows of the global k-res map under the band) x k
+  const int L = nb * nb + 1;
+  const int64_t nt = blockIdx.x / bands;
+  const int band = blockIdx.x % bands;
+  const int t = (int)(nt % T);
+  const int64_t n = nt / T;
+  const int Y0 = band * MERGE_BY, Y1 = min(Y0 + MERGE_BY, out_res);
+  const float sg = (float)k / (float)out_res;
+  int r_lo, r_hi, tmp;
+  float tl;
+  lin_src(Y0, k, sg, r_lo, tmp, tl);
+  lin_src(Y1 - 1, k, sg, tmp, r_hi, tl);
+  const int nr = r_hi - r_lo + 1;
+  const int64_t plane = (int64_t)h * w;
+  const float* gp = lg + ((n * L + L - 1) * T + t) * plane;
+#pragma unroll 4
+  for (int idx = threadIdx.x; idx < nr * k; idx += blockDim.x) {
+    const int r = r_lo + idx / k, x = idx % k;
+    gsig[idx] = up_sig_fast(gp, h, w, k, r, x);
+  }
+  __syncthreads();
+  // each thread owns output columns X = tid + 256 j; the column terms (global-map taps, the
+  // tile columns covering X and their 96-res taps) are derived once and reused down the band
+  float* ob = out + nt * (int64_t)out_res * out_res;
+  for (int X = threadIdx.x; X < out_res; X += blockDim.x) {
+    int gx0, gx1;
+    float glx;
+    lin_src(X, k, sg, gx0, gx1, glx);
+    int tx0[4], tx1[4], tbj[4];
+    float tlx[4];
+    int ncol = 0;
+    for (int bj = 0; bj < nb && ncol < 4; ++bj) {
+      const int xx = X - stride * bj;
+      if (xx < 0 || xx >= k) continue;
+      lin_src(xx, w, (float)w / (float)k, tx0[ncol], tx1[ncol], tlx[ncol]);
+      tbj[ncol++] = bj;
+    }
+#pragma unroll 4
+    for (int Y = Y0; Y < Y1; ++Y) {       // unrolled: several rows' tile loads in flight
+      int y0, y1;
+      float ly;
+      lin_src(Y, k, sg, y0, y1, ly);
+      const float* g0 = gsig + (y0 - r_lo) * k;
+      const float* g1 = gsig + (y1 - r_lo) * k;
+      const float glob = blend(g0[gx0], g0[gx1], g1[gx0], g1[gx1], ly, glx);
+      float sum = 0.f, cnt = 0.f;
+      for (int bi = 0; bi < nb; ++bi) {
+        const int yy = Y - stride * bi;
+        if (yy < 0 || yy >= k) continue;
+        int ty0, ty1;
+        float tly;
+        lin_src(yy, h, (float)h / (float)k, ty0, ty1, tly);
+        for (int c = 0; c < ncol; ++c) {
+          const float* pl = lg + ((n * L + bi * nb + tbj[c]) * T + t) * plane;
+          sum += sigm_fast(blend(pl[ty0 * w + tx0[c]], pl[ty0 * w + tx1[c]], pl[ty1 * w + tx0[c]],
+                                 pl[ty1 * w + tx1[c]], tly, tlx[c]));
+          cnt += 1.f;
+        }
+      }
+      ob[(int64_t)Y * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int catseg_avgpool_rows(const void* in, int64_t S, int H, int W, int C, int ph, int pw, void* out,
@@ -217,8 +302,18 @@ extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h
   // every output pixel must be covered by at least one tile (Fold count > 0)
   const int nb = (out_res - kernel) / stride + 1;
   CATSEG_CHECK(stride * (nb - 1) + kernel == out_res && stride <= kernel, "sliding_merge: tiles must cover out_res");
-  const int64_t total = N * T * (int64_t)out_res * out_res;
-  hipLaunchKernelGGL(sliding_merge_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, logits, N, T, h, w,
-                     kernel, stride, nb, out_res, out);
+  if (kernel <= MERGE_KMAX && (kernel + stride - 1) / stride <= 4) {   // <= 4 tile columns cover any X
+    const int bands = (out_res + MERGE_BY - 1) / MERGE_BY;
+    const int64_t blocks = N * T * (int64_t)bands;
+    CATSEG_CHECK(blocks < ((int64_t)1 << 31), "sliding_merge: grid too large");
+    // LDS rows: the k-res rows under MERGE_BY output rows, + 2 for the bilinear taps
+    const int rows = (int)((int64_t)(MERGE_BY - 1) * kernel / out_res) + 3;
+    hipLaunchKernelGGL(sliding_merge_band_kernel, dim3((unsigned)blocks), dim3(256), rows * kernel * sizeof(float),
+                       (hipStream_t)stream, logits, T, h, w, kernel, stride, nb, out_res, bands, out);
+  } else {
+    const int64_t total = N * T * (int64_t)out_res * out_res;
+    hipLaunchKernelGGL(sliding_merge_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, logits, N, T, h,
+                       w, kernel, stride, nb, out_res, out);
+  }
   return catseg_launch_status("sliding_merge");
 }
