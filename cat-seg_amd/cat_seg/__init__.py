@@ -11,6 +11,8 @@ from .cat_seg_model import CATSeg  # noqa: F401
 from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401
 from .modeling.transformer.cat_seg_predictor import CATSegPredictor  # noqa: F401
 from .arch import CatSegArch, VIT_B16, VIT_L14_336, TINY  # noqa: F401
+from .evaluation import SemSegEvaluator, SemSegGzeroEvaluator, VOCbEvaluator  # noqa: F401
 
 __all__ = ["add_cat_seg_config", "get_cfg", "build_model", "CATSeg", "CATSegHead", "CATSegPredictor",
-           "CatSegArch", "META_ARCH_REGISTRY", "SEM_SEG_HEADS_REGISTRY"]
+           "CatSegArch", "META_ARCH_REGISTRY", "SEM_SEG_HEADS_REGISTRY",
+           "SemSegEvaluator", "SemSegGzeroEvaluator", "VOCbEvaluator"]

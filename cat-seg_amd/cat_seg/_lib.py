@@ -127,6 +127,7 @@ _SIGS = {
     "catseg_quant_fp8_rows": [vp, i32, i64, i64, i64, vp, i64, vp, vp],
     "catseg_layernorm_fp8": [vp, i64, RowMap, i32, vp, i64, vp, vp, vp, i64, i64, f32, vp],
     "catseg_set_gemm_fp8_variant": [i32],
+    "catseg_semseg_confusion": [vp, i64, i64, i64, vp, i32, i32, i32, vp, vp, vp],
     "catseg_rows_gemm": [vp, i64, i64, vp, vp, f32, vp, i64, C.POINTER(RowsEpi), i32, vp],
     "catseg_rows_mlp": [vp, i64, i64, vp, vp, f32, vp, vp, i64, i32, vp, C.POINTER(RowsEpi), i32, vp],
     "catseg_layernorm": [vp, i64, RowMap, i32, vp, i64, i32, vp, vp, i64, i64, f32, vp],

@@ -508,3 +508,15 @@ def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=
         call("catseg_rows_mlp", y.data_ptr(), _ld(y), M, ln[0].data_ptr(), ln[1].data_ptr(), eps, w1.data_ptr(),
              b1.data_ptr(), hidden, act, w2.data_ptr(), e, _dt(y), _stream())
     return out
+
+
+def semseg_confusion(probs, gt, conf, n_invalid, *, num_classes, ignore_label=255, clamp_pred=-1):
+    """conf += bincount((N+1) * argmax(probs) + gt') on the device (catseg_semseg_confusion).
+    probs (T, H, W) fp32, gt (H, W) int32, conf ((N+1)^2,) int64, n_invalid (1,) int64."""
+    T, H, W = probs.shape
+    assert probs.is_contiguous() and gt.is_contiguous() and gt.shape == (H, W) and gt.dtype == torch.int32
+    assert conf.dtype == torch.int64 and conf.numel() == (num_classes + 1) ** 2 and n_invalid.dtype == torch.int64
+    with _rec("semseg_confusion", 0, probs.numel() * 4 + gt.numel() * 4):
+        call("catseg_semseg_confusion", probs.data_ptr(), T, H, W, gt.data_ptr(), num_classes, ignore_label,
+             clamp_pred, conf.data_ptr(), n_invalid.data_ptr(), _stream())
+    return conf

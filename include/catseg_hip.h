@@ -422,6 +422,19 @@ int catseg_token_embed(const int32_t* tokens, int64_t n, int ctx, const float* t
 int catseg_eot_gather(const float* x, const int32_t* tokens, int64_t n, int ctx, int width,
                       float* out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * catseg_semseg_confusion — the confusion-matrix update of detectron2's
+ * SemSegEvaluator.process as CAT-Seg's evaluators use it (plain_train_net.py:107-116,
+ * train_net.py:55-67): pred = argmax over T of probs [T][H][W] (first maximum wins);
+ * pred >= clamp_pred -> clamp_pred (VOC-b; clamp_pred < 0 disables); gt [H][W] int32 with
+ * ignore_label -> num_classes; conf[(num_classes+1) * pred + gt] += 1 (int64,
+ * (num_classes+1)^2, caller-zeroed, accumulated across calls).  Labels outside
+ * [0, num_classes] are not binned but counted in *n_invalid (int64).
+ * ------------------------------------------------------------------------- */
+int catseg_semseg_confusion(const float* probs, int64_t T, int64_t H, int64_t W, const int32_t* gt,
+                            int num_classes, int ignore_label, int clamp_pred, int64_t* conf,
+                            int64_t* n_invalid, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
