@@ -817,7 +817,8 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     //  * a 160x128 8-wave BK=128 tile when its tiles fit one round, one workgroup per CU
     //    (fc2: 47.9 us vs 61.9 for 128x128 [42.2]; out-proj: 19.8 vs 24.7 [18.2]);
     //  * otherwise 160x128 with 8 waves at two workgroups per CU (fc1: 54.2 us vs 71.3 [55.4]).
-    // Deeper rings (S = 3 / 4 at BK = 64, variants 21 / 22) measured slower on fc2 (53 us).
+    // Deeper rings (S = 3 / 4 at BK = 64, variants 21 / 22) measured slower on fc2 (53 us);
+    // a one-round 320x256 tile for fc1 (240 tiles) 58.4 us vs 54.5 (288x256: 102 us).
     const int64_t t224 = ((g->M + 223) / 224) * (g->N / 256);
     const int64_t t256 = ((g->M + 255) / 256) * (g->N / 256);
     const int64_t t160 = ((g->M + 159) / 160) * (g->N / 128);
