@@ -134,7 +134,7 @@ class CatSegEngine:
         p = CLIP + "visual."
         W = a.vision_width
         kc = 3 * a.vision_patch ** 2
-        kp = _round_up(kc, 32)
+        kp = _round_up(kc, 64)          # K % 64: the patch GEMM takes the pipelined MFMA kernel
         pw = torch.zeros(W, kp)
         pw[:, :kc] = sd[p + "conv1.weight"].reshape(W, kc)
         w.patch_w, w.patch_k = self._W(pw), kp

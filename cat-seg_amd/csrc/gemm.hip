@@ -96,7 +96,7 @@ DEV void store8f(bf16* p, const float v[8]) {
   st16(p, make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
 }
 
-template <typename TO>
+template <typename TO, bool SC = false>
 DEV void epilogue8(const EpiArgs& e, int64_t m, int64_t n, f32x4 lo, f32x4 hi) {
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   if (e.bias) {
@@ -127,7 +127,14 @@ DEV void epilogue8(const EpiArgs& e, int64_t m, int64_t n, f32x4 lo, f32x4 hi) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] += a[r];
   }
-  store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
+  int64_t off = m * e.ldo + n;
+  if constexpr (SC) {   // ConvTranspose2d scatter (as epilogue4); cout % 8 == 0 keeps the 8 columns together
+    const int64_t k = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
+    const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
+    const int64_t ky = n / (k * cout), kx = (n / cout) % k, co = n % cout;
+    off = ((s * hin * k + y * k + ky) * (win * k) + x * k + kx) * cout + co;
+  }
+  store8f(reinterpret_cast<TO*>(e.out) + off, v);
 }
 
 template <typename TA, typename TO, int BM, int BN>
@@ -412,7 +419,7 @@ struct Swz {
 // (unit scales; fp8 rate = 2x bf16) consumes two 16-byte chunks per lane; A and W fragments
 // read the same chunks, so the k order inside the instruction does not matter.  The
 // epilogue multiplies by sa[m] * sw[n] (per-row dequant scales) before bias / act / residual.
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false>
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
                                                             const bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int64_t K, int tiles_n, EpiArgs e) {
@@ -565,7 +572,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
           lo = lo * (w0 * s);
           hi = hi * (w1 * s);
         }
-        epilogue8<TO>(e, m, n0 + c8, lo, hi);
+        epilogue8<TO, SC>(e, m, n0 + c8, lo, hi);
       }
     }
   }
@@ -760,13 +767,13 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   return e;
 }
 
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool SC = false>
 bool launch3(const CatsegGemmArgs* g, hipStream_t st) {
   if (g->N % BN != 0 || g->K % BK != 0) return false;
   const EpiArgs e = make_epi(g);
   RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
   const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
-  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
+  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, false, SC>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
                      st, (const bf16*)g->A, g->lda, am, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e);
   return true;
 }
@@ -827,6 +834,11 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     else if (g->N % 128 == 0 && g->K % 128 == 0 && t160 >= 160 && t160 <= 256) v = 15;
     else if (g->N % 128 == 0) v = 17;
     else return false;
+  }
+  if (g->store_mode != 0) {   // ConvTranspose scatter epilogue: instantiated for the two auto tiles only
+    if (v == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, true>(g, st);
+    if (v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, true>(g, st);
+    return false;
   }
   switch (v) {
     case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
@@ -889,7 +901,7 @@ void launch2(const CatsegGemmArgs* g, hipStream_t st) {
 template <typename TA, typename TO>
 void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
   if constexpr (sizeof(TA) == 2) {
-    if (g->store_mode == 0 && try_gemm3<TO>(g, st)) return;
+    if ((g->store_mode == 0 || g->cvt_cout % 8 == 0) && try_gemm3<TO>(g, st)) return;
     const int64_t t128 = ((g->M + 127) / 128) * ((g->N + 127) / 128);
     if (g->N <= 64) launch2<TO, 128, 64>(g, st);
     else if (t128 < 512) launch2<TO, 64, 128>(g, st);     // fill 256 CUs x 2 slots

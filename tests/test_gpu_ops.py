@@ -90,6 +90,24 @@ def test_gemm_convtranspose_store(dt):
     close(got, ref, atol=1e-5 if dt == torch.float32 else 2e-2, what="convT")
 
 
+@pytest.mark.parametrize("cout,k", [(256, 2), (128, 4)])
+def test_gemm_convtranspose_store_pipelined(cout, k):
+    """The guidance upsamplers' shapes (cat_seg_model.py:81-82, ViT-L/14 hooks: 1024 -> 256 / 128
+    channels, k = 2 / 4): ConvTranspose scatter from the pipelined kernel's 8-wide epilogue."""
+    S, H, Wd, cin = 2, 24, 24, 1024
+    x = rnd(S, cin, H, Wd, seed=20)
+    w = rnd(cin, cout, k, k, seed=21) / 32
+    b = rnd(cout, seed=22)
+    ref = F.conv_transpose2d(x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double(), b.double(), stride=k)
+    A = x.permute(0, 2, 3, 1).reshape(S * H * Wd, cin)
+    Wg = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)
+    out = torch.full((S * H * k * Wd * k, cout), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.gemm(A.to(dev, torch.bfloat16).contiguous(), Wg.to(dev, torch.bfloat16).contiguous(), out,
+             bias=b.repeat(k * k).to(dev), store=(k, H, Wd, cout))
+    got = out.reshape(S, H * k, Wd * k, cout).permute(0, 3, 1, 2)
+    close(got, ref, atol=2e-2, rtol=1e-2, what=f"convT pipelined cout {cout} k {k}")
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 17, 18, 19, 20, 21, 22, 23])
 def test_gemm_pipelined_variants(variant):
     """Every LDS-DMA pipelined bf16 tile (gemm.hip gemm3_kernel) against fp64: ragged M
