@@ -96,9 +96,34 @@ DEV void store8f(bf16* p, const float v[8]) {
   st16(p, make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
 }
 
-template <typename TO, bool SC = false>
+// EPI selects a compile-time epilogue: 0 = general (every runtime option), 1 = bias (+ res),
+// 2 = bias + QuickGELU.  The lean forms drop the unused paths' code and registers, which the
+// epilogue-heavy ViT GEMMs measurably feel (a dead scatter branch alone cost QKV 2.5 us).
+template <typename TO, bool SC = false, int EPI = 0>
 DEV void epilogue8(const EpiArgs& e, int64_t m, int64_t n, f32x4 lo, f32x4 hi) {
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  if constexpr (EPI != 0) {
+    if (e.bias) {
+      float b[8];
+      load8f(e.bias + n, b);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] += b[r];
+    }
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = apply_act(v[r], ACT_QUICKGELU);
+    }
+    if constexpr (EPI == 1) {
+      if (e.res) {
+        float a[8];
+        load8f(reinterpret_cast<const TO*>(e.res) + m * e.ld_res + n, a);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += a[r];
+      }
+    }
+    store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
+    return;
+  }
   if (e.bias) {
     float b[8];
     load8f(e.bias + n, b);
@@ -419,7 +444,8 @@ struct Swz {
 // (unit scales; fp8 rate = 2x bf16) consumes two 16-byte chunks per lane; A and W fragments
 // read the same chunks, so the k order inside the instruction does not matter.  The
 // epilogue multiplies by sa[m] * sw[n] (per-row dequant scales) before bias / act / residual.
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false>
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false,
+          int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
                                                             const bf16* __restrict__ W, int64_t ldw, int64_t M,
                                                             int64_t K, int tiles_n, EpiArgs e) {
@@ -572,7 +598,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
           lo = lo * (w0 * s);
           hi = hi * (w1 * s);
         }
-        epilogue8<TO, SC>(e, m, n0 + c8, lo, hi);
+        epilogue8<TO, SC, EPI>(e, m, n0 + c8, lo, hi);
       }
     }
   }
@@ -767,13 +793,13 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   return e;
 }
 
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool SC = false>
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool SC = false, int EPI = 0>
 bool launch3(const CatsegGemmArgs* g, hipStream_t st) {
   if (g->N % BN != 0 || g->K % BK != 0) return false;
   const EpiArgs e = make_epi(g);
   RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
   const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
-  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, false, SC>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
+  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, false, SC, EPI>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN), 0,
                      st, (const bf16*)g->A, g->lda, am, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e);
   return true;
 }
@@ -840,6 +866,15 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     if (v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, true>(g, st);
     return false;
   }
+  // lean epilogues for the automatic ViT tiles
+  const bool plain = !g->add && !g->res2 && g->alpha == 1.f;
+  const int epi = plain && g->act == ACT_NONE ? 1 : plain && g->act == ACT_QUICKGELU && !g->res ? 2 : 0;
+  if (epi == 1 && v == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, false, 1>(g, st);
+  if (epi == 1 && v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, false, 1>(g, st);
+  if (epi == 1 && v == 20) return launch3<TO, 224, 256, 2, 4, 2, 64, false, 1>(g, st);
+  if (epi == 2 && v == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, false, 2>(g, st);
+  if (epi == 2 && v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, false, 2>(g, st);
+  if (epi == 2 && v == 20) return launch3<TO, 224, 256, 2, 4, 2, 64, false, 2>(g, st);
   switch (v) {
     case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
     case 2: return launch3<TO, 256, 256, 2, 4, 4, 32>(g, st);
