@@ -188,6 +188,8 @@ def load() -> C.CDLL:
             "`make -C cat-seg_amd/csrc` (or __graft_entry__.build()); the CAT-Seg HIP path has no fallback")
     lib = C.CDLL(LIB_PATH)
     for name, args in _SIGS.items():
+        if name.startswith("catseg_set_") and not hasattr(lib, name):
+            continue    # a tuning knob an older build (same-box A/B reference) lacks; compute entries must exist
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = (C.c_char_p if name == "catseg_last_error" else
