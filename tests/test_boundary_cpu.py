@@ -38,6 +38,12 @@ def test_config_base_and_overrides():
     assert cfg.TEST.SLIDING_WINDOW is False
 
 
+def test_vit_fp8_config_key_reaches_the_model():
+    assert build_model(tiny_cfg()).vit_fp8 is False
+    m = build_model(tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": "bf16", "MODEL.CATSEG_HIP.VIT_FP8": "True"}))
+    assert m.vit_fp8 is True
+
+
 def test_build_model_registry_and_state_dict_keys():
     m = build_model(tiny_cfg())
     assert isinstance(m, CATSeg)

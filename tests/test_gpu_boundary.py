@@ -67,3 +67,20 @@ def test_catseg_sliding_window_matches_golden():
     # height/width default to the 640² merge resolution (cat_seg_model.py:215-216)
     out = model([{"image": torch.from_numpy(g["image0"])}])
     assert out[0]["sem_seg"].shape[-2:] == (640, 640)
+
+
+def test_catseg_vit_fp8_config_matches_golden():
+    """MODEL.CATSEG_HIP.VIT_FP8 True (config 5's e4m3 ViT GEMMs) through build_model -> forward:
+    the engine runs catseg_gemm_fp8 and the probabilities meet SURVEY §8c's fp8 gate
+    (sigmoid mean-abs <= 1e-2) against the reference golden."""
+    g = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_pad.npz")))
+    cfg = tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": "bf16", "MODEL.CATSEG_HIP.VIT_FP8": "True"})
+    model = build_model(cfg).cuda().eval()
+    model.sem_seg_head.predictor.set_class_tokens(g["tokens"])
+    model.arch = model.arch.replace(pad_len=int(g["pad_len"]))
+    model._engine = None
+    imgs = [torch.from_numpy(g[k]) for k in sorted(k for k in g if k.startswith("image"))]
+    out = model([{"image": im} for im in imgs])
+    assert model.engine.vit_fp8 and "q8_wqkv" in model.engine.w.vblocks[0]
+    err = (out[0]["sem_seg"][:, ::8, ::8].cpu() - torch.from_numpy(g["sem_seg0_sub"])).abs()
+    assert err.mean().item() <= 1e-2 and err.max().item() < 0.1, (err.mean().item(), err.max().item())
