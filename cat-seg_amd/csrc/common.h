@@ -196,6 +196,17 @@ DEV float apply_act(float v, int act) {
 // Row map: r(m) = ((m / d1) % m1) * s1 + ((m / d2) % m2) * s2 + off.
 // Identity = {1, INT64 big, 1, 1, 1, 0, 0}.  Used to gather A rows (hook tokens
 // without CLS) and to broadcast per-image / per-class guidance terms.
+// ConvTranspose2d(k, stride k) scatter of GEMM output (m, n): m = (s, y, x) over
+// (hin, win), n = (ky, kx, co); NHWC destination [s][y*k+ky][x*k+kx][co].  32-bit index
+// math (m < 2^31 and n < 2^31, host-checked): the 64-bit div/mod form cost the decoder's
+// ConvTranspose epilogue more than its MFMAs.
+DEV int64_t convt_offset(int64_t m, int64_t n, int k, int hin, int win, int cout) {
+  const unsigned mu = (unsigned)m, nu = (unsigned)n, hw = (unsigned)(hin * win), kc = (unsigned)(k * cout);
+  const unsigned s = mu / hw, rem = mu - s * hw, y = rem / (unsigned)win, x = rem - y * (unsigned)win;
+  const unsigned ky = nu / kc, r2 = nu - ky * kc, kx = r2 / (unsigned)cout, co = r2 - kx * (unsigned)cout;
+  return (((int64_t)s * hin * k + (int64_t)y * k + ky) * ((int64_t)win * k) + (int64_t)x * k + kx) * cout + co;
+}
+
 struct RowMap {
   int64_t d1, m1, s1, d2, m2, s2, off;
 };

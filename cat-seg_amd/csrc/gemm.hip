@@ -73,10 +73,7 @@ DEV void epilogue4(const EpiArgs& e, int64_t m, int64_t n, f32x4 acc) {
   if (e.store_mode == 0) {
     off = m * e.ldo + n;
   } else {   // ConvTranspose2d(k, stride k) scatter: m = (s, y, x), n = (ky, kx, co)
-    const int64_t k = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
-    const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
-    const int64_t ky = n / (k * cout), kx = (n / cout) % k, co = n % cout;
-    off = ((s * hin * k + y * k + ky) * (win * k) + x * k + kx) * cout + co;
+    off = convt_offset(m, n, e.cvt_k, e.cvt_hin, e.cvt_win, e.cvt_cout);
   }
   store4<TO>(reinterpret_cast<TO*>(e.out) + off, v);
 }
@@ -154,10 +151,7 @@ DEV void epilogue8(const EpiArgs& e, int64_t m, int64_t n, f32x4 lo, f32x4 hi) {
   }
   int64_t off = m * e.ldo + n;
   if constexpr (SC) {   // ConvTranspose2d scatter (as epilogue4); cout % 8 == 0 keeps the 8 columns together
-    const int64_t k = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
-    const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
-    const int64_t ky = n / (k * cout), kx = (n / cout) % k, co = n % cout;
-    off = ((s * hin * k + y * k + ky) * (win * k) + x * k + kx) * cout + co;
+    off = convt_offset(m, n, e.cvt_k, e.cvt_hin, e.cvt_win, e.cvt_cout);
   }
   store8f(reinterpret_cast<TO*>(e.out) + off, v);
 }
@@ -1021,6 +1015,7 @@ extern "C" int catseg_gemm(const CatsegGemmArgs* g, void* stream) {
                "gemm: bad ConvTranspose scatter geometry");
   CATSEG_CHECK(g->store_mode == 0 || g->N == (int64_t)g->cvt_k * g->cvt_k * g->cvt_cout,
                "gemm: ConvTranspose N must be k*k*cout");
+  CATSEG_CHECK(g->store_mode == 0 || g->M < (1LL << 31), "gemm: ConvTranspose row count must fit 31 bits");
   CATSEG_CHECK(g->amap.d1 > 0 && g->amap.m1 > 0 && g->amap.d2 > 0 && g->amap.m2 > 0, "gemm: bad amap");
   CATSEG_CHECK(!g->add || (g->addmap.d1 > 0 && g->addmap.m1 > 0 && g->addmap.d2 > 0 && g->addmap.m2 > 0),
                "gemm: bad addmap");

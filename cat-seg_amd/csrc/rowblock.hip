@@ -179,10 +179,7 @@ DEV void store_rows(const float* st, int sld, int64_t m0, int64_t M, int n0, con
     if (e.store_mode == 0) {
       off = m * e.ldo + n;
     } else {
-      const int64_t k = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
-      const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
-      const int64_t ky = n / (k * cout), kx = (n / cout) % k, co = n % cout;
-      off = ((s * hin * k + y * k + ky) * (win * k) + x * k + kx) * cout + co;
+      off = convt_offset(m, n, e.cvt_k, e.cvt_hin, e.cvt_win, e.cvt_cout);
     }
     T* o = reinterpret_cast<T*>(e.out) + off;
     store4<T>(o, v);
@@ -365,6 +362,7 @@ extern "C" int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const fl
   CATSEG_CHECK(ld_x % 8 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0, "rows_gemm: alignment");
   CATSEG_CHECK(!ln_gamma || ln_beta, "rows_gemm: ln_beta missing");
   if (int rc = check_epi(epi, (int)N)) return rc;
+  CATSEG_CHECK(epi->store_mode == 0 || M < (1LL << 31), "rows_gemm: ConvTranspose row count must fit 31 bits");
   Epi e = make_epi(epi);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == CATSEG_BF16 && g_persistent &&

@@ -199,10 +199,7 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
       if (m < M) {
         int64_t off;
         if constexpr (SCATTER) {
-          const int64_t kk = e.cvt_k, hin = e.cvt_hin, win = e.cvt_win, cout = e.cvt_cout;
-          const int64_t s = m / (hin * win), y = (m / win) % hin, x = m % win;
-          const int64_t ky = c / (kk * cout), kx = (c / cout) % kk, co = c % cout;
-          off = ((s * hin * kk + y * kk + ky) * (win * kk) + x * kk + kx) * cout + co;
+          off = convt_offset(m, c, e.cvt_k, e.cvt_hin, e.cvt_win, e.cvt_cout);
         } else {
           off = m * e.ldo + c;
         }
