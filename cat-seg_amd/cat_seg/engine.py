@@ -70,6 +70,7 @@ class CatSegEngine:
         if self.vit_fp8 and dtype != torch.bfloat16:
             raise ValueError("vit_fp8 needs the bf16 engine")
         self._text = None
+        self.last_corr = self.last_topk = None
         with torch.no_grad():
             self.w = self._prepare(state_dict)
 
@@ -429,6 +430,9 @@ class CatSegEngine:
             T = a.pad_len
             classes = torch.empty(B, T, device=dev, dtype=torch.int32)
             ops.topk_classes(corr, t_stride=B * HW, b_stride=HW, B=B, T=T0, HW=HW, k=T, out=classes)
+        # the last call's cost volume [T0][B*HW] and top-k selection (B, pad_len) stay readable
+        # (device tensors, no copy): parity tests check the selection against the fp32 margins
+        self.last_corr, self.last_topk = corr, classes
         S = B * T
         R = S * HW
         X = torch.empty(R, D, device=dev, dtype=dt)

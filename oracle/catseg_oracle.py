@@ -292,18 +292,23 @@ def up_block(x: Tensor, guid: Optional[Tensor], sd, p: str) -> Tensor:
     return x
 
 
-def aggregator(arch, sd, img_feats: Tensor, text_feats: Tensor, guidance: Sequence[Tensor]) -> Tensor:
+def aggregator(arch, sd, img_feats: Tensor, text_feats: Tensor, guidance: Sequence[Tensor],
+               classes: Optional[Tensor] = None) -> Tensor:
     """Aggregator.forward (model.py:683-725).  img_feats (B,C,H,W), text (B,T,P,C),
-    guidance [res3, res4, res5]."""
+    guidance [res3, res4, res5].  `classes` (B, pad_len) int64, test use only: replaces the
+    top-k selection of model.py:694-697 by a caller-supplied one (the classes the HIP path
+    selected), so everything downstream of the selection is checked at full tolerance when
+    bf16 rounding reorders near-tied classes; None = the reference's own top-k."""
     p = AGG
     imgn = F.normalize(img_feats, dim=1)
     txtn = F.normalize(text_feats, dim=-1)
     corr = torch.einsum("bchw,btpc->bpthw", imgn, txtn)            # model.py:648-652
-    classes = None
     T0 = text_feats.shape[1]
     if arch.pad_len > 0 and T0 > arch.pad_len:                       # model.py:694-702
-        m = corr.permute(0, 2, 1, 3, 4).flatten(-3).max(dim=-1)[0]
-        classes = m.topk(arch.pad_len, dim=-1, sorted=False)[1]
+        if classes is None:
+            m = corr.permute(0, 2, 1, 3, 4).flatten(-3).max(dim=-1)[0]
+            classes = m.topk(arch.pad_len, dim=-1, sorted=False)[1]
+        classes = classes.long()
         idx = classes[..., None, None].expand(-1, -1, txtn.shape[-2], txtn.shape[-1])
         txtn = torch.gather(txtn, 1, idx)
         text_feats = txtn
@@ -357,10 +362,10 @@ def sem_seg_postprocess(result: Tensor, img_size, out_h: int, out_w: int) -> Ten
     return F.interpolate(result, size=(out_h, out_w), mode="bilinear", align_corners=False)[0]
 
 
-def head_logits(arch, sd, clip_images: Tensor, text: Tensor) -> Tensor:
+def head_logits(arch, sd, clip_images: Tensor, text: Tensor, classes: Optional[Tensor] = None) -> Tensor:
     """cat_seg_model.py:155-188 + CATSegHead/Predictor (cat_seg_head.py:2009-2010,
     cat_seg_predictor.py:151-162).  clip_images (B,3,R,R) normalized+resized,
-    text (T,1,C_o) cached embeddings.  Returns logits (B,T,96,96)."""
+    text (T,1,C_o) cached embeddings.  Returns logits (B,T,96,96).  `classes`: see aggregator."""
     feats, hooks = encode_image_dense(arch, sd, clip_images)
     B = clip_images.shape[0]
     g = arch.grid
@@ -370,7 +375,19 @@ def head_logits(arch, sd, clip_images: Tensor, text: Tensor) -> Tensor:
     res4 = F.conv_transpose2d(res4, sd["upsample1.weight"], sd["upsample1.bias"], stride=2)
     res5 = F.conv_transpose2d(res5, sd["upsample2.weight"], sd["upsample2.bias"], stride=4)
     text_b = text.unsqueeze(0).expand(B, -1, -1, -1)
-    return aggregator(arch, sd, res3, text_b, [res3, res4, res5])
+    return aggregator(arch, sd, res3, text_b, [res3, res4, res5], classes=classes)
+
+
+def class_corr_max(arch, sd, clip_images: Tensor, text: Tensor) -> Tensor:
+    """Per-image, per-class max of the fp32 cost volume over (P, H, W): the top-k key of
+    model.py:694-697 (correlation model.py:648-652).  Returns (B, T)."""
+    with torch.no_grad():
+        feats, _ = encode_image_dense(arch, sd, clip_images)
+        B, g = clip_images.shape[0], arch.grid
+        img = F.normalize(feats[:, 1:, :].reshape(B, g, g, -1).permute(0, 3, 1, 2), dim=1)
+        txt = F.normalize(text.unsqueeze(0).expand(B, -1, -1, -1), dim=-1)
+        corr = torch.einsum("bchw,btpc->bpthw", img, txt)
+        return corr.permute(0, 2, 1, 3, 4).flatten(2).max(dim=-1)[0]
 
 
 def preprocess(arch, images: List[Tensor]) -> Tuple[Tensor, List[Tuple[int, int]]]:
@@ -399,8 +416,25 @@ def catseg_forward(arch, sd, batched_inputs: List[dict], text: Tensor, all_image
         return out
 
 
-def catseg_forward_sliding(arch, sd, batched_inputs: List[dict], text: Tensor):
-    """CATSeg.forward sliding-window branch (cat_seg_model.py:156-176,204-218)."""
+def sliding_clip_images(arch, image: Tensor) -> Tensor:
+    """The 5 crops of the sliding-window branch, normalized and resized (cat_seg_model.py:158-176)."""
+    kernel, overlap, out_res = 384, 0.333, [640, 640]
+    stride = int(kernel * (1 - overlap))
+    img = image.float()
+    unfold = torch.nn.Unfold(kernel_size=kernel, stride=stride)
+    x = F.interpolate(img.unsqueeze(0), size=out_res, mode="bilinear", align_corners=False).squeeze()
+    x = unfold(x).reshape(3, kernel, kernel, -1).permute(3, 0, 1, 2)
+    glob = F.interpolate(img.unsqueeze(0), size=(kernel, kernel), mode="bilinear", align_corners=False)
+    x = torch.cat([x, glob], dim=0)
+    mean = torch.tensor(arch.clip_pixel_mean).view(-1, 1, 1)
+    std = torch.tensor(arch.clip_pixel_std).view(-1, 1, 1)
+    R = arch.clip_resolution
+    return F.interpolate((x - mean) / std, size=(R, R), mode="bilinear", align_corners=False)
+
+
+def catseg_forward_sliding(arch, sd, batched_inputs: List[dict], text: Tensor, classes: Optional[Tensor] = None):
+    """CATSeg.forward sliding-window branch (cat_seg_model.py:156-176,204-218).
+    `classes` (5, pad_len): per-crop top-k override, see aggregator."""
     kernel, overlap, out_res = 384, 0.333, [640, 640]
     stride = int(kernel * (1 - overlap))
     with torch.no_grad():
@@ -415,7 +449,7 @@ def catseg_forward_sliding(arch, sd, batched_inputs: List[dict], text: Tensor):
         std = torch.tensor(arch.clip_pixel_std).view(-1, 1, 1)
         R = arch.clip_resolution
         clip_images = F.interpolate((image - mean) / std, size=(R, R), mode="bilinear", align_corners=False)
-        outputs = head_logits(arch, sd, clip_images, text)
+        outputs = head_logits(arch, sd, clip_images, text, classes=classes)
         outputs = F.interpolate(outputs, size=kernel, mode="bilinear", align_corners=False).sigmoid()
         glob_out = F.interpolate(outputs[-1:], size=out_res, mode="bilinear", align_corners=False)
         outputs = outputs[:-1]

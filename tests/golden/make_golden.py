@@ -270,7 +270,77 @@ def sliding_case(name, arch, T, shape, seed, pad_len, height, width, sub=4):
          sem_seg_sub=out[:, ::sub, ::sub], sem_seg_sum=out.double().sum())
 
 
+def ref_corr_max(arch, clip, agg, clip_images, text):
+    """Per-image, per-class max of the fp32 cost volume over (P, H, W) — the top-k key of
+    model.py:694-697 — from the reference CLIP + Aggregator.correlation (model.py:648-652)."""
+    with torch.no_grad():
+        feats = clip.encode_image(clip_images, dense=True)
+        g = arch.grid
+        B = feats.shape[0]
+        img = feats[:, 1:, :].reshape(B, g, g, -1).permute(0, 3, 1, 2)
+        corr = agg.correlation(img, text.repeat(B, 1, 1, 1))          # (B, P, T, H, W)
+        return corr.permute(0, 2, 1, 3, 4).flatten(2).max(dim=-1)[0]   # (B, T)
+
+
+def l14_case(name, T_name, shapes, seed, sub=4):
+    """ViT-L/14@336 (the benchmarked geometry: patch 14, K=588 im2col, hooks 7/15, no pos-embed
+    resize, 1024-wide ViT) with the real class prompts of `T_name`."""
+    from cat_seg.arch import VIT_L14_336
+    arch = VIT_L14_336
+    sd = synthesize_state_dict(arch, seed=0)
+    clip, agg, up1, up2 = build_reference(arch, sd)
+    tokens = np.load(os.path.join(HERE, "class_tokens.npz"))[T_name].astype(np.int64)
+    text = ref_text(clip, tokens)
+    imgs = rand_images(seed, shapes)
+    clip_images = glue_preprocess(arch, [i.float() for i in imgs])
+    logits = ref_head(arch, clip, agg, up1, up2, clip_images, text)
+    cmax = ref_corr_max(arch, clip, agg, clip_images, text)
+    out0 = glue_post(logits[0], shapes[0], shapes[0][0], shapes[0][1])
+    kw = dict(tokens=tokens.astype(np.int32), text=text, logits=logits[:, :, ::sub, ::sub], corr_max=cmax,
+              logits_sum=logits.double().sum(), logits_abs_sum=logits.double().abs().sum(),
+              sem_seg0_sub=out0[:, ::8, ::8], pad_len=256, sub=sub)
+    for i, im in enumerate(imgs):
+        kw[f"image{i}"] = im
+    save(name, **kw)
+
+
+CLASS_LISTS = ("voc20", "voc20b", "pc59", "pc459", "ade150", "ade847", "coco")
+
+
+def class_data():
+    """Class-name token ids of the reference's class lists (datasets/*.json), made with the
+    reference tokenizer: the golden fixture, plus the package data the predictor reads
+    (cat_seg/data: class_tokens.npz, class_lists.json = sha1 of the names -> list key,
+    class_names.json = the names, for dataset metadata)."""
+    import hashlib
+    tok = tok_mod.SimpleTokenizer()
+    toks, names_all, table = {}, {}, {}
+    for ds in CLASS_LISTS:
+        names = json.load(open(f"{REF}/datasets/{ds}.json"))
+        toks[ds] = tokenize(tok, class_prompts(names)).astype(np.int32)
+        names_all[ds] = names
+        table[hashlib.sha1("\n".join(names).encode()).hexdigest()] = ds
+    save("class_tokens", **toks)
+    pkg = os.path.join(ROOT, "cat-seg_amd", "cat_seg", "data")
+    np.savez_compressed(os.path.join(pkg, "class_tokens.npz"), **toks)
+    with open(os.path.join(pkg, "class_lists.json"), "w") as f:
+        json.dump(table, f, indent=0)
+    with open(os.path.join(pkg, "class_names.json"), "w") as f:
+        json.dump(names_all, f)
+    return toks
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "classes":
+        class_data()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "l14":
+        torch.set_num_threads(8)
+        # config 3 geometry, real ade150 prompts, two images (one ragged: ImageList pad 352 -> 336)
+        l14_case("e2e_l14_ade150", "ade150", [(336, 336), (300, 336)], seed=21)
+        # config 4 class count: ade847 prompts -> top-256 + -100 scatter, one image
+        l14_case("e2e_l14_ade847", "ade847", [(336, 336)], seed=22, sub=6)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "sliding":
         torch.set_num_threads(8)
         # TEST.SLIDING_WINDOW: tiny arch, T=20 > pad_len=16 (per-crop top-k), ragged 440x360 image,
@@ -279,13 +349,7 @@ def main():
         return
     torch.manual_seed(0)
     torch.set_num_threads(8)
-    tok = tok_mod.SimpleTokenizer()
-    # class-name token ids for the reference datasets (the product takes token ids)
-    toks = {}
-    for ds in ("voc20", "ade150", "pc459", "ade847"):
-        names = json.load(open(f"{REF}/datasets/{ds}.json"))
-        toks[ds] = tokenize(tok, class_prompts(names)).astype(np.int32)
-    save("class_tokens", **toks)
+    toks = class_data()
     # 1) tiny arch, T=10 < pad_len=16 (learned padding path), two ragged images (ImageList pad)
     e2e_case("e2e_tiny_pad", TINY, 10, [(300, 352), (320, 256)], seed=1, pad_len=16)
     # 2) tiny arch, T=24 > pad_len=16 (top-k + scatter -100), pooling (2,2)

@@ -88,48 +88,14 @@ def test_engine_b16_config2_vs_oracle(dtype):
         assert err.max().item() < 5e-2 and err.mean().item() < 5e-3
 
 
-@pytest.mark.parametrize("T", [150, 847])
-def test_engine_l14_configs_3_4_vs_oracle(T):
-    """Config 3 (ViT-L/14 @336, 150 classes, bf16) and config 4's class count (847 -> top-256,
-    the class-attention tile at its maximum T' = 256) on one image against the CPU oracle;
-    bf16 gate max-abs 5e-2 / mean-abs 5e-3 on logits, untouched top-k classes exactly -100."""
-    arch = VIT_L14_336
-    sd = synthesize_state_dict(arch, seed=0)
-    gen = torch.Generator().manual_seed(11)
-    text = torch.nn.functional.normalize(torch.randn(T, arch.embed_dim, generator=gen), dim=-1)
-    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float()]
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
-    clip_images, _ = O.preprocess(arch, imgs)
-    ref = O.head_logits(arch, sd, clip_images, text.unsqueeze(1))
-    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16)
-    eng.set_text(text.cuda())
-    raw, sizes = batch_raw(imgs)
-    got = eng.head_logits(raw, sizes).cpu()
-    assert got.shape == ref.shape
-    live = ref > -99
-    if T > arch.pad_len:
-        # the selected classes agree (ties aside) and the rest are exactly -100
-        agree = (live == (got > -99)).float().mean().item()
-        assert agree > 0.99, agree
-        live = live & (got > -99)
-        assert torch.equal(got[~(ref > -99) & ~(got > -99)], ref[~(ref > -99) & ~(got > -99)])
-    err = (got[live] - ref[live]).abs()
-    print(f"L/14 T={T}: max {err.max().item():.3e} mean {err.mean().item():.3e}")
-    assert err.max().item() < 5e-2 and err.mean().item() < 5e-3, (err.max().item(), err.mean().item())
-
-
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("T", [150, 459])
-def test_engine_l14_config5_fp8_sliding_vs_oracle(T):
-    """Config 5: ViT-L/14 sliding-window 640² inference with fp8 (e4m3, per-row scales) CLIP
-    image-encoder GEMMs, against the fp32 CPU oracle's sliding branch
-    (cat_seg_model.py:156-176,204-218).  Gate: sigmoid mean-abs <= 1e-2.
-    T=150: no class truncation, the gate on every probability.  T=459 (config 5's class
-    count, top-256 per crop): random synthetic class embeddings put many classes within
-    rounding of the 256-th cost, so some classes flip membership in a crop (their map there
-    goes to sigmoid(-100) = 0 on one side); those classes (per-class mean error > 0.05) must
-    stay under 10 % of T, and the gate holds on the rest.  Measured: fp8 1.09e-2 overall,
-    30 flipped classes, 1.5e-3 on the rest; bf16 1.05e-3, 6 flipped, 2.6e-4."""
+def test_engine_l14_config5_fp8_sliding_vs_oracle():
+    """Config 5 geometry: ViT-L/14 sliding-window 640² inference with fp8 (e4m3, per-row
+    scales) CLIP image-encoder GEMMs, against the fp32 CPU oracle's sliding branch
+    (cat_seg_model.py:156-176,204-218), T=150 (no class truncation): gate
+    sigmoid mean-abs <= 1e-2 on every probability.  Config 5's real class count (pc459,
+    top-256 per crop) is test_gpu_parity_bench.py::test_l14_config5_fp8_sliding_pc459_vs_oracle."""
+    T = 150
     arch = VIT_L14_336
     sd = synthesize_state_dict(arch, seed=0)
     gen = torch.Generator().manual_seed(5)
@@ -144,15 +110,8 @@ def test_engine_l14_config5_fp8_sliding_vs_oracle(T):
     got = eng.forward_sliding(raw, sizes, [(480, 640)])[0].cpu()
     assert got.shape == ref.shape
     e = (got - ref).abs()
-    per_class = e.mean(dim=(1, 2))
-    flipped = per_class > 0.05
-    print(f"config 5 fp8 sliding T={T}: mean {e.mean().item():.3e} max {e.max().item():.3f} "
-          f"flipped classes {int(flipped.sum())} rest mean {per_class[~flipped].mean().item():.3e}")
-    if T <= arch.pad_len:
-        assert e.mean().item() <= 1e-2 and not flipped.any()
-    else:
-        assert int(flipped.sum()) <= 0.1 * T
-        assert per_class[~flipped].mean().item() <= 1e-2
+    print(f"config 5 fp8 sliding T={T}: mean {e.mean().item():.3e} max {e.max().item():.3f}")
+    assert e.mean().item() <= 1e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -1,0 +1,255 @@
+"""Parity at the configurations bench.py times, against
+(a) golden vectors made by the REFERENCE's own modules at ViT-L/14@336 (make_golden.py l14)
+and (b) the CPU oracle at the benchmarked batch sizes, with the real class prompts.
+
+Top-k (T > pad_len, model.py:694-702): with synthetic weights the encoded prompts of one
+dataset are near-parallel (mean pairwise cosine 0.93-0.95), so dozens of classes sit within
+1e-3 of the 256-th largest max-correlation.  Any rounding difference (bf16, fp8, or an fp32
+summation order) may swap such classes in or out of the selection.  The tests therefore
+  1. measure eps = max |corr_max_gpu - corr_max_ref| over all classes, and prove every class
+     whose membership differs is within 2*eps of the selection threshold (a class further
+     than that from the threshold provably keeps its membership), and
+  2. compare every logit against the oracle run with the GPU's selection
+     (oracle.aggregator(classes=...)) at the full gates: fp32 1e-3; bf16 max-abs 5e-2 /
+     mean-abs 5e-3; fp8 sigmoid mean-abs 1e-2.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cat_seg.arch import VIT_B16, VIT_L14_336
+from cat_seg.engine import CatSegEngine
+from cat_seg.weights import synthesize_state_dict
+from oracle import catseg_oracle as O
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+BF16_MAX, BF16_MEAN = 5e-2, 5e-3
+_SD = {}
+
+
+def sd_of(arch):
+    if arch.name not in _SD:
+        _SD[arch.name] = synthesize_state_dict(arch, seed=0)
+    return _SD[arch.name]
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def batch_raw(imgs, div=32):
+    H = -(-max(i.shape[1] for i in imgs) // div) * div
+    W = -(-max(i.shape[2] for i in imgs) // div) * div
+    raw = torch.zeros(len(imgs), 3, H, W)
+    for k, im in enumerate(imgs):
+        raw[k, :, : im.shape[1], : im.shape[2]] = im
+    sizes = torch.tensor([[i.shape[1], i.shape[2]] for i in imgs], dtype=torch.int32)
+    return raw.cuda(), sizes.cuda()
+
+
+def threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def gate(got, ref, dtype, what=""):
+    err = (got - ref).abs()
+    mx, mn = err.max().item(), err.mean().item()
+    print(f"{what} {dtype}: max {mx:.3e} mean {mn:.3e}")
+    if dtype == torch.float32:
+        assert mx < 1e-3, (what, mx)
+    else:
+        assert mx < BF16_MAX and mn < BF16_MEAN, (what, mx, mn)
+
+
+def check_selection(eng, ref_cmax, k):
+    """Every class whose top-k membership differs from the reference's is within 2*eps of the
+    threshold, eps = max |corr_max_gpu - corr_max_ref|.  Returns (eps, flipped count)."""
+    corr = eng.last_corr                              # [T0][B*HW] fp32
+    sel = eng.last_topk.long().cpu()                  # (B, k)
+    B, T0 = ref_cmax.shape
+    gmax = corr.view(T0, B, -1).amax(-1).t().cpu()
+    eps = (gmax - ref_cmax).abs().max().item()
+    flipped = 0
+    for b in range(B):
+        s = torch.sort(ref_cmax[b], descending=True)[0]
+        s_in, s_out = s[k - 1].item(), s[k].item()
+        ref_set = set(torch.topk(ref_cmax[b], k)[1].tolist())
+        gpu_set = set(sel[b].tolist())
+        assert len(gpu_set) == k
+        for c in ref_set - gpu_set:
+            assert ref_cmax[b, c].item() - s_out <= 2 * eps + 1e-7, (b, c, ref_cmax[b, c].item(), s_out, eps)
+        for c in gpu_set - ref_set:
+            assert s_in - ref_cmax[b, c].item() <= 2 * eps + 1e-7, (b, c, ref_cmax[b, c].item(), s_in, eps)
+        flipped += len(ref_set - gpu_set)
+    print(f"top-{k}: eps {eps:.3e}, {flipped} classes swapped over {B} images")
+    return eps, flipped
+
+
+# ---------------------------------------------------------------- reference goldens at L/14
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_l14_ade150_reference_golden(dtype):
+    """ViT-L/14@336 (patch 14, K=588 im2col, hooks 7/15, no pos-embed resize), real ade150
+    prompts, two images (one ragged: ImageList pad 352 -> resize 336), vs the reference modules."""
+    g = load("e2e_l14_ade150")
+    arch = VIT_L14_336
+    eng = CatSegEngine(arch, sd_of(arch), dtype=dtype)
+    text = eng.encode_text(torch.from_numpy(g["tokens"]))          # the HIP text encoder
+    gate_t = 1e-4 if dtype == torch.float32 else 2e-2
+    t_err = (text.cpu() - torch.from_numpy(g["text"][:, 0])).abs().max().item()
+    assert t_err < gate_t, t_err
+    eng.set_text(torch.from_numpy(g["text"]).cuda())
+    imgs = [torch.from_numpy(g[k]).float() for k in ("image0", "image1")]
+    raw, sizes = batch_raw(imgs)
+    sub = int(g["sub"])
+    got = eng.head_logits(raw, sizes)[:, :, ::sub, ::sub].cpu()
+    gate(got, torch.from_numpy(g["logits"]), dtype, "L/14 ade150 golden")
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_l14_ade847_reference_golden(dtype):
+    """Config 4's class count with the real ade847 prompts: top-256 of 847 + -100 scatter,
+    vs the reference modules; selection differences justified by the fp32 margins, then every
+    logit vs the oracle on the GPU's selection."""
+    g = load("e2e_l14_ade847")
+    arch = VIT_L14_336
+    sd = sd_of(arch)
+    eng = CatSegEngine(arch, sd, dtype=dtype)
+    text = torch.from_numpy(g["text"])
+    eng.set_text(text.cuda())
+    img = torch.from_numpy(g["image0"]).float()
+    raw, sizes = batch_raw([img])
+    got = eng.head_logits(raw, sizes).cpu()
+    eps, flipped = check_selection(eng, torch.from_numpy(g["corr_max"]), arch.pad_len)
+    assert eps < (2e-5 if dtype == torch.float32 else 5e-3), eps
+    sub = int(g["sub"])
+    ref = torch.from_numpy(g["logits"])
+    gs = got[:, :, ::sub, ::sub]
+    if flipped == 0:        # same selection as the reference: the golden itself is the check
+        assert torch.equal(gs[ref < -99], ref[ref < -99])
+        gate(gs, ref, dtype, "L/14 ade847 golden")
+    threads()
+    clip_images, _ = O.preprocess(arch, [img])
+    forced = O.head_logits(arch, sd, clip_images, text, classes=eng.last_topk.long().cpu())
+    assert torch.equal(got[forced < -99], forced[forced < -99])
+    live = forced > -99
+    gate(got[live], forced[live], dtype, "L/14 ade847 vs oracle (GPU selection)")
+
+
+# ---------------------------------------------------------------- the benchmarked batches
+@pytest.mark.timeout(900)
+def test_l14_config3_bs8_vs_oracle():
+    """Config 3 exactly as bench.py runs it: ViT-L/14@336, ade150 prompts, bs=8, bf16."""
+    g = load("e2e_l14_ade150")
+    arch = VIT_L14_336
+    sd = sd_of(arch)
+    gen = torch.Generator().manual_seed(31)
+    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float() for _ in range(8)]
+    text = torch.from_numpy(g["text"])
+    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    threads()
+    clip_images, _ = O.preprocess(arch, imgs)
+    ref = torch.cat([O.head_logits(arch, sd, clip_images[i:i + 2], text) for i in range(0, 8, 2)])
+    gate(got, ref, torch.bfloat16, "config 3 bs=8")
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_b16_config2_bs4_vs_oracle(dtype):
+    """Config 2: ViT-B/16@384 (bicubic pos-embed resize), ade150 prompts, bs=4; fp32 gate 1e-3."""
+    arch = VIT_B16
+    sd = sd_of(arch)
+    tokens = torch.from_numpy(np.load(os.path.join(GOLDEN, "class_tokens.npz"))["ade150"]).long()
+    threads()
+    with torch.no_grad():
+        text = O.text_embeds(arch, sd, tokens)                          # (150, 1, 512)
+    gen = torch.Generator().manual_seed(32)
+    imgs = [torch.randint(0, 256, (3, 384, 384), generator=gen).float() for _ in range(4)]
+    eng = CatSegEngine(arch, sd, dtype=dtype)
+    t_gpu = eng.encode_text(tokens.int()).cpu()
+    assert (t_gpu - text[:, 0]).abs().max().item() < (1e-4 if dtype == torch.float32 else 2e-2)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    clip_images, _ = O.preprocess(arch, imgs)
+    with torch.no_grad():
+        ref = O.head_logits(arch, sd, clip_images, text)
+    gate(got, ref, dtype, "config 2 bs=4")
+
+
+@pytest.mark.timeout(900)
+def test_l14_config4_bs4_ade847_vs_oracle():
+    """Config 4 per-GPU shard: ViT-L/14@336, ade847 prompts (top-256), 4 images, bf16."""
+    g = load("e2e_l14_ade847")
+    arch = VIT_L14_336
+    sd = sd_of(arch)
+    text = torch.from_numpy(g["text"])
+    gen = torch.Generator().manual_seed(33)
+    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float() for _ in range(4)]
+    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    threads()
+    clip_images, _ = O.preprocess(arch, imgs)
+    cmax = O.class_corr_max(arch, sd, clip_images, text)
+    check_selection(eng, cmax, arch.pad_len)
+    with torch.no_grad():
+        forced = O.head_logits(arch, sd, clip_images, text, classes=eng.last_topk.long().cpu())
+    assert torch.equal(got[forced < -99], forced[forced < -99])
+    live = forced > -99
+    gate(got[live], forced[live], torch.bfloat16, "config 4 bs=4")
+
+
+@pytest.mark.timeout(900)
+def test_l14_config5_fp8_sliding_pc459_vs_oracle():
+    """Config 5: sliding-window 640² (5 crops), real pc459 prompts (top-256 per crop), fp8 ViT
+    GEMMs.  Selection differences justified per crop from the fp32 margins; every probability
+    vs the oracle's sliding branch on the GPU's per-crop selection, gate sigmoid mean-abs 1e-2."""
+    arch = VIT_L14_336
+    sd = sd_of(arch)
+    tokens = torch.from_numpy(np.load(os.path.join(GOLDEN, "class_tokens.npz"))["pc459"]).long()
+    threads()
+    with torch.no_grad():
+        text = O.text_embeds(arch, sd, tokens)
+    gen = torch.Generator().manual_seed(34)
+    img = torch.randint(0, 256, (3, 480, 640), generator=gen).float()
+    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16, vit_fp8=True)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw([img])
+    got = eng.forward_sliding(raw, sizes, [(480, 640)])[0].cpu()
+    crops = O.sliding_clip_images(arch, img)
+    check_selection(eng, O.class_corr_max(arch, sd, crops, text), arch.pad_len)
+    ref = O.catseg_forward_sliding(arch, sd, [{"image": img, "height": 480, "width": 640}], text,
+                                   classes=eng.last_topk.long().cpu())[0]["sem_seg"]
+    e = (got - ref).abs()
+    print(f"config 5 fp8 pc459: sigmoid mean {e.mean().item():.3e} max {e.max().item():.3e}")
+    assert e.mean().item() <= 1e-2
+
+
+# ---------------------------------------------------------------- batch invariance
+@pytest.mark.parametrize("T_name,big,small", [("ade150", 8, 1), ("ade847", 32, 4)])
+def test_batch_invariance(T_name, big, small):
+    """Image i's logits must not depend on its batch-mates (the multi-GPU gate: the gathered
+    logits of N ranks equal the 1-GPU logits bit for bit): logits of a batch of
+    `big` images equal, bit for bit, those of the same images run in batches of `small`."""
+    g = load("e2e_l14_" + T_name)
+    arch = VIT_L14_336
+    eng = CatSegEngine(arch, sd_of(arch), dtype=torch.bfloat16)
+    eng.set_text(torch.from_numpy(g["text"]).cuda())
+    gen = torch.Generator().manual_seed(35)
+    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float() for _ in range(big)]
+    raw, sizes = batch_raw(imgs)
+    whole = eng.head_logits(raw, sizes).clone()
+    for i in range(0, big, small):
+        part = eng.head_logits(raw[i:i + small].contiguous(), sizes[i:i + small].contiguous())
+        d = (part - whole[i:i + small]).abs().max().item()
+        assert torch.equal(part, whole[i:i + small]), (i, d)

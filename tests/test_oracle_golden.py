@@ -62,3 +62,27 @@ def test_oracle_sliding_matches_reference_golden():
     assert out.shape == (g["text"].shape[0], int(g["height"]), int(g["width"]))
     np.testing.assert_allclose(out[:, ::sub, ::sub].numpy(), g["sem_seg_sub"], atol=1e-5, rtol=0)
     assert abs(out.double().sum().item() - float(g["sem_seg_sum"])) < 1e-2
+
+
+@pytest.mark.parametrize("name", ["e2e_l14_ade150", "e2e_l14_ade847"])
+def test_oracle_matches_reference_golden_l14(name):
+    """ViT-L/14@336 (the benchmarked geometry) with real class prompts: the oracle's logits, the
+    top-k key (per-class max correlation) and, for ade847, the top-256 selection itself."""
+    from cat_seg.arch import VIT_L14_336
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = load(name)
+    arch = VIT_L14_336
+    sd = synthesize_state_dict(arch, seed=0)
+    text = torch.from_numpy(g["text"])
+    if name == "e2e_l14_ade150":      # text encoder at L/14 width (the ade847 one is the same code)
+        t = O.text_embeds(arch, sd, torch.from_numpy(g["tokens"]).long())
+        np.testing.assert_allclose(t.numpy(), g["text"], atol=2e-6, rtol=0)
+    imgs = [torch.from_numpy(g[k]).float() for k in sorted(k for k in g if k.startswith("image"))]
+    clip_images, _ = O.preprocess(arch, imgs)
+    with torch.no_grad():
+        cmax = O.class_corr_max(arch, sd, clip_images, text)
+        logits = O.head_logits(arch, sd, clip_images, text)
+    np.testing.assert_allclose(cmax.numpy(), g["corr_max"], atol=2e-6, rtol=0)
+    sub = int(g["sub"])
+    np.testing.assert_allclose(logits[:, :, ::sub, ::sub].numpy(), g["logits"], atol=2e-5, rtol=0)
+    assert abs(logits.double().sum().item() - float(g["logits_sum"])) < 2e-2
