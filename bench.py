@@ -69,15 +69,42 @@ def class_tokens(T):
     return torch.from_numpy(tok[:T].astype(np.int32))
 
 
+def _spawned_rank(local, args_list, world, port):
+    """One rank of a self-launched N-GPU run (python bench.py --gpus N without torchrun)."""
+    os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + args_list
+    main()
+
+
+def launch_ranks(n):
+    """--gpus N with no WORLD_SIZE in the environment: start N rank processes (spawned
+    interpreters, one per GPU) before this process touches the GPU, and exit with their status
+    (detectron2 `launch` for the reference, train_net.py:314-324)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_spawned_rank, args=(sys.argv[1:], n, port), nprocs=n, join=True, start_method="spawn")
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: the ranks must match the GPUs asked for")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"RCCL group has {dist.get_world_size()} ranks, expected {args.gpus}")
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     arch = VIT_L14_336
     cfg5 = args.config == 5
@@ -145,7 +172,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            run()
+            lg_last = run()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -158,6 +185,15 @@ def main():
     images = world * B * args.steps
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    # the all-gather is a pure copy: every rank's slice of the gathered logits must equal its
+    # own logits bit for bit (the multi-GPU parity gate of BASELINE.md), checked after timing
+    gather_ok = None
+    if world > 1:
+        local_lg = g_logits if graph is not None else lg_last
+        mine = gathered[rank * B:(rank + 1) * B]
+        flag = torch.tensor([1 if torch.equal(mine, local_lg) else 0], device=dev, dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather_ok = bool(flag.item())
 
     roofline, kernels = None, None
     if rank == 0 and not args.no_roofline:
@@ -174,7 +210,8 @@ def main():
                        "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling"),
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
+            "scaling": "weak", "vs_baseline": None, "ranks": world,
+            "gather_bit_identical": gather_ok,
             "dtype": args.dtype + ("+fp8e4m3 ViT GEMMs" if args.vit_fp8 else ""),
             "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, "
                     f"{'pc459' if cfg5 else 'ade150'} prompt tokens)",
@@ -254,38 +291,60 @@ def roofline_pass(step, stream, dtype):
     return roof, kern
 
 
-def cpu_baseline_sliding(arch, sd, text):
-    """The oracle's sliding-window branch on one 640² image (config 5's CPU baseline)."""
+def host_cores() -> int:
+    """Cores this process may use: the affinity mask, capped by OMP_NUM_THREADS when the host
+    sets it (the GPU box gives each job a 16-thread share of a larger machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def _timed_runs(fn, runs):
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return ts
+
+
+def cpu_baseline_sliding(arch, sd, text, runs=3):
+    """The oracle's sliding-window branch on one 640² image (config 5's CPU baseline):
+    1 warm-up, median of `runs` timed runs."""
     from oracle import catseg_oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    cores = host_cores()
+    torch.set_num_threads(cores)
     gen = torch.Generator().manual_seed(99)
     inp = [{"image": torch.rand(3, 640, 640, generator=gen) * 255}]
-    t0 = time.perf_counter()
-    O.catseg_forward_sliding(arch, sd, inp, text.unsqueeze(1))
-    dt = time.perf_counter() - t0
-    return {"value": round(1 / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+    O.catseg_forward_sliding(arch, sd, inp, text.unsqueeze(1))        # warm-up
+    ts = _timed_runs(lambda: O.catseg_forward_sliding(arch, sd, inp, text.unsqueeze(1)), runs)
+    med = float(np.median(ts))
+    return {"value": round(1 / med, 4), "unit": "images/s", "cores": cores, "kind": "port", "runs": runs,
+            "spread": [round(min(ts), 2), round(max(ts), 2)],
             "sample": f"1 image of the same workload (640² sliding, 5 crops, L/14@336, T={text.shape[0]}, fp32) "
-                      f"through oracle/catseg_oracle.py on {threads} host threads, {dt:.1f} s"}
+                      f"through oracle/catseg_oracle.py on {cores} host threads: 1 warm-up, median of {runs} runs "
+                      f"({med:.1f} s)"}
 
 
-def cpu_baseline(arch, sd, text, n_images):
-    """The oracle (CPU fp32 restatement of the reference path) on a bounded sample."""
+def cpu_baseline(arch, sd, text, n_images, runs=3):
+    """The oracle (CPU fp32 restatement of the reference path) on a bounded sample of the same
+    workload: a batch of `n_images`, 1 warm-up, the median of `runs` timed runs."""
     from oracle import catseg_oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    cores = host_cores()
+    torch.set_num_threads(cores)
     gen = torch.Generator().manual_seed(99)
     R = arch.clip_resolution
     inputs = [{"image": torch.rand(3, R, R, generator=gen) * 255} for _ in range(n_images)]
     O.catseg_forward(arch, sd, inputs[:1], text.unsqueeze(1))     # warm-up
-    t0 = time.perf_counter()
-    O.catseg_forward(arch, sd, inputs, text.unsqueeze(1), all_images=True)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_images / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n_images} images of the same workload (L/14@336, T={text.shape[0]}, fp32, one batch) "
-                      f"through oracle/catseg_oracle.py on {threads} host threads, {dt:.1f} s"}
+    ts = _timed_runs(lambda: O.catseg_forward(arch, sd, inputs, text.unsqueeze(1), all_images=True), runs)
+    med = float(np.median(ts))
+    return {"value": round(n_images / med, 4), "unit": "images/s", "cores": cores, "kind": "port", "runs": runs,
+            "spread": [round(n_images / max(ts), 4), round(n_images / min(ts), 4)],
+            "sample": f"batches of {n_images} images of the same workload (L/14@336, T={text.shape[0]}, fp32) through "
+                      f"oracle/catseg_oracle.py on {cores} host threads: 1 warm-up, median of {runs} timed runs "
+                      f"({med:.1f} s per batch)"}
 
 
 if __name__ == "__main__":

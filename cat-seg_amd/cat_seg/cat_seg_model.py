@@ -21,19 +21,22 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 from torch import nn
+from torch.nn.modules.module import _IncompatibleKeys
 
 from . import ops
 from .arch import CatSegArch, arch_from_cfg
 from .engine import CatSegEngine
 from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401  (registers the head)
 from .registry import META_ARCH_REGISTRY, build_sem_seg_head, configurable
-from .weights import synthesize_state_dict
+from .weights import CLIP as CLIP_PREFIX, synthesize_state_dict
 
 _DTYPES = {"bf16": torch.bfloat16, "f32": torch.float32, "fp32": torch.float32}
 
 
 def convert_openai_clip_keys(sd: Dict[str, torch.Tensor], prefix: str = "") -> Dict[str, torch.Tensor]:
-    """OpenAI CLIP `attn.in_proj_weight` -> q/k/v_proj_weight split (model_vpt.py:520-528)."""
+    """OpenAI CLIP `attn.in_proj_weight` -> q/k/v_proj_weight split (model_vpt.py:520-528), the
+    metadata entries input_resolution / context_length / vocab_size dropped (:511-512), every
+    key prefixed with `prefix`."""
     out = {}
     for k, v in sd.items():
         if k.endswith("attn.in_proj_weight"):
@@ -78,6 +81,7 @@ class CATSeg(nn.Module):
         self.vit_fp8 = bool(vit_fp8)
         self._sd = synthesize_state_dict(self.arch, seed=synthetic_seed)
         self._engine: Optional[CatSegEngine] = None
+        self.input_format = "RGB"          # read by SemanticSegmentorWithTTA / DefaultPredictor
 
     @classmethod
     def from_config(cls, cfg):
@@ -111,11 +115,18 @@ class CATSeg(nn.Module):
     def state_dict(self, *args, **kwargs):        # reference checkpoint keys
         return dict(self._sd)
 
-    def load_state_dict(self, state_dict, strict: bool = True):
+    def load_state_dict(self, state_dict, strict: bool = True, **_):
+        """Reference checkpoint keys (detectron2 `{"model": sd}` accepted, OpenAI `in_proj_weight`
+        split).  Returns torch's `_IncompatibleKeys(missing_keys, unexpected_keys)` (lists), which
+        fvcore's Checkpointer._load_model reads and edits (DetectionCheckpointer drops
+        pixel_mean / pixel_std from missing_keys)."""
         sd = state_dict.get("model", state_dict)
         sd = {k: (v if torch.is_tensor(v) else torch.as_tensor(v)) for k, v in sd.items()}
         if any(k.endswith("attn.in_proj_weight") for k in sd):
-            sd = convert_openai_clip_keys(sd)
+            # an OpenAI CLIP state dict (clip.load -> build_model, model_vpt.py:515-531) has no
+            # module prefix: its keys belong under sem_seg_head.predictor.clip_model.
+            prefix = "" if any(k.startswith(CLIP_PREFIX) for k in sd) else CLIP_PREFIX
+            sd = convert_openai_clip_keys(sd, prefix)
         missing = [k for k in self._sd if k not in sd]
         unexpected = [k for k in sd if k not in self._sd]
         if strict and (missing or unexpected):
@@ -126,31 +137,45 @@ class CATSeg(nn.Module):
                     raise ValueError(f"{k}: shape {tuple(sd[k].shape)} != {tuple(self._sd[k].shape)}")
                 self._sd[k] = sd[k].float().cpu()
         self._engine = None
-        return missing, unexpected
+        return _IncompatibleKeys(list(missing), list(unexpected))
+
+    def _engine_device(self) -> torch.device:
+        """The CUDA device the engine runs on: the module's device when it is on the GPU,
+        else the current CUDA device (the HIP path has no CPU fallback)."""
+        d = self.device
+        if d.type == "cuda":
+            return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
+        return torch.device("cuda", torch.cuda.current_device())
 
     @property
     def engine(self) -> CatSegEngine:
-        if self._engine is None or self._engine.device != self.device:
-            dev = self.device if self.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+        """Built once per resolved device (weights converted / uploaded once), rebuilt only when
+        the model moves to another GPU or new weights are loaded."""
+        dev = self._engine_device()
+        if self._engine is None or self._engine.device != dev:
             self._engine = CatSegEngine(self.arch, self._sd, dtype=self.compute_dtype, device=dev,
                                         vit_fp8=self.vit_fp8)
             self.sem_seg_head.predictor.attach_engine(self._engine)
         return self._engine
 
     # ------------------------------------------------------------------ forward
-    def _batch(self, images: List[torch.Tensor]):
+    def _batch(self, eng: CatSegEngine, images: List[torch.Tensor]):
         """Stage the images into one zero-padded fp32 canvas on the device (ImageList.from_tensors
-        geometry: batch max, rounded up to size_divisibility)."""
+        geometry: batch max, rounded up to size_divisibility).  Host images go through one pinned
+        canvas and one H2D copy; images already on the device are copied in place there."""
         d = max(self.size_divisibility, 1)
         H = max(int(i.shape[-2]) for i in images)
         W = max(int(i.shape[-1]) for i in images)
         H, W = -(-H // d) * d, -(-W // d) * d
-        raw = torch.zeros(len(images), 3, H, W, dtype=torch.float32, pin_memory=True)
+        dev = eng.device
+        on_dev = all(i.is_cuda for i in images)
+        raw = torch.zeros(len(images), 3, H, W, dtype=torch.float32, device=dev if on_dev else "cpu",
+                          pin_memory=not on_dev)
         for k, im in enumerate(images):
             raw[k, :, : im.shape[-2], : im.shape[-1]].copy_(im)
-        sizes = torch.tensor([[int(i.shape[-2]), int(i.shape[-1])] for i in images], dtype=torch.int32)
-        dev = self.engine.device
-        return raw.to(dev, non_blocking=True), sizes.to(dev), sizes.tolist()
+        sizes = [[int(i.shape[-2]), int(i.shape[-1])] for i in images]
+        sizes_dev = torch.tensor(sizes, dtype=torch.int32).to(dev, non_blocking=True)
+        return (raw if on_dev else raw.to(dev, non_blocking=True)), sizes_dev, sizes
 
     def forward(self, batched_inputs: List[dict]):
         if self.training:
@@ -160,7 +185,7 @@ class CATSeg(nn.Module):
         with torch.no_grad():
             eng = self.engine
             self.sem_seg_head.predictor.get_text_embeds()
-            raw, sizes_dev, sizes = self._batch([x["image"] for x in batched_inputs])
+            raw, sizes_dev, sizes = self._batch(eng, [x["image"] for x in batched_inputs])
             logits = eng.head_logits(raw, sizes_dev)
             n = len(batched_inputs) if self.return_all_images else 1
             results = []
@@ -183,7 +208,7 @@ class CATSeg(nn.Module):
             self.sem_seg_head.predictor.get_text_embeds()
             n = len(batched_inputs) if self.return_all_images else 1
             inputs = batched_inputs[:n]
-            raw, sizes_dev, _ = self._batch([x["image"] for x in inputs])
+            raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in inputs])
             res = eng.SLIDE_OUT
             out_hw = [(int(x.get("height", res)), int(x.get("width", res))) for x in inputs]
             return [{"sem_seg": o} for o in eng.forward_sliding(raw, sizes_dev, out_hw)]

@@ -22,6 +22,17 @@ except Exception:  # noqa: BLE001
     HAVE_D2 = False
 
 
+def _decode(v):
+    """yacs `_decode_cfg_value`: strings that are Python literals ("(384, 384)", "[1,1]", "True")
+    become those values; anything else stays as given."""
+    if isinstance(v, str):
+        try:
+            return ast.literal_eval(v)
+        except (ValueError, SyntaxError):
+            return v
+    return v
+
+
 class CfgNode(dict):
     """Minimal yacs.CfgNode: nested dict with attribute access."""
 
@@ -66,6 +77,7 @@ class CfgNode(dict):
                     self[k] = node
                 node._merge(v)
             else:
+                v = _decode(v)
                 self[k] = tuple(v) if isinstance(self.get(k), tuple) and isinstance(v, list) else v
 
     def merge_from_file(self, path: str):
@@ -83,11 +95,7 @@ class CfgNode(dict):
             parts = k.split(".")
             for p in parts[:-1]:
                 node = node[p]
-            try:
-                v = ast.literal_eval(v) if isinstance(v, str) else v
-            except (ValueError, SyntaxError):
-                pass
-            node[parts[-1]] = v
+            node[parts[-1]] = _decode(v)
 
 
 def get_cfg():
@@ -99,11 +107,20 @@ def get_cfg():
                   "PIXEL_MEAN": [103.530, 116.280, 123.675], "PIXEL_STD": [1.0, 1.0, 1.0],
                   "SEM_SEG_HEAD": {"NAME": "CATSegHead", "IGNORE_VALUE": 255, "NUM_CLASSES": 54,
                                    "IN_FEATURES": ["res2", "res3", "res4", "res5"]}},
-        "INPUT": {"MIN_SIZE_TEST": 640, "MAX_SIZE_TEST": 2560, "FORMAT": "RGB", "CROP": {"ENABLED": False}},
+        # detectron2 v0.6 defaults (config/defaults.py) of the keys the data / eval path reads;
+        # MIN/MAX_SIZE_TEST are the CAT-Seg configs' values (configs/config.yaml:52-53)
+        "INPUT": {"MIN_SIZE_TRAIN": (800,), "MIN_SIZE_TRAIN_SAMPLING": "choice", "MAX_SIZE_TRAIN": 1333,
+                  "MIN_SIZE_TEST": 640, "MAX_SIZE_TEST": 2560, "FORMAT": "RGB",
+                  "CROP": {"ENABLED": False, "TYPE": "relative_range", "SIZE": [0.9, 0.9]}},
         "DATASETS": {"TRAIN": (), "TEST": ()},
-        "SOLVER": {"IMS_PER_BATCH": 16, "BASE_LR": 0.001},
-        "TEST": {"EVAL_PERIOD": 0, "AUG": {"ENABLED": False}},
+        "SOLVER": {"IMS_PER_BATCH": 16, "BASE_LR": 0.001, "WEIGHT_DECAY": 0.0001, "WEIGHT_DECAY_NORM": 0.0,
+                   "MOMENTUM": 0.9, "MAX_ITER": 40000,
+                   "CLIP_GRADIENTS": {"ENABLED": False, "CLIP_TYPE": "value", "CLIP_VALUE": 1.0, "NORM_TYPE": 2.0}},
+        "TEST": {"EVAL_PERIOD": 0, "EXPECTED_RESULTS": [],
+                 "AUG": {"ENABLED": False, "MIN_SIZES": (400, 500, 600, 700, 800, 900, 1000, 1100, 1200),
+                         "MAX_SIZE": 4000, "FLIP": True}},
         "DATALOADER": {"NUM_WORKERS": 4},
+        "OUTPUT_DIR": "./output",
         "VERSION": 2,
     })
 

@@ -596,13 +596,15 @@ class CatSegEngine:
         return logits
 
     # ------------------------------------------------------------------ full eval forward
-    def forward(self, raw: torch.Tensor, sizes: torch.Tensor, out_hw) -> torch.Tensor:
-        """Sigmoid probabilities upsampled to out_hw for every image (cat_seg_model.py:220-229)."""
+    def forward(self, raw: torch.Tensor, sizes: torch.Tensor, out_hw, image_hw) -> torch.Tensor:
+        """Sigmoid probabilities upsampled to out_hw for every image (cat_seg_model.py:220-229).
+        image_hw: the host-side (h, w) of the valid image region, which sem_seg_postprocess crops
+        to (one size for the whole batch; CATSeg.forward handles ragged batches per image)."""
         logits = self.head_logits(raw, sizes)
         B, T0, h, w = logits.shape
         H, W = out_hw
         out = torch.empty(B, T0, H, W, device=self.device, dtype=_f32)
-        ih, iw = [int(v) for v in sizes[0].tolist()] if sizes.is_cpu else (h, w)
+        ih, iw = (int(v) for v in image_hw)
         ops.postprocess(logits, out, crop=(min(h, ih), min(w, iw)))
         return out
 

@@ -28,11 +28,23 @@ from . import ops
 
 
 def _metadata(dataset_name):
-    try:
-        from detectron2.data import MetadataCatalog
-    except ImportError:
-        return None
+    """MetadataCatalog entry (detectron2's when importable, else cat_seg.data's stand-in, where
+    the reference's dataset names are registered on import); None without a name."""
+    from .data.catalog import MetadataCatalog
     return MetadataCatalog.get(dataset_name) if dataset_name else None
+
+
+def _catalog_gt_loader(dataset_name):
+    """detectron2 SemSegEvaluator's ground truth: the label file registered for the input's
+    "file_name" (input_file_to_gt_file), read as stored (8-bit PNG or 16-bit TIFF)."""
+    from PIL import Image
+    from .data.catalog import DatasetCatalog
+    table = {d["file_name"]: d["sem_seg_file_name"] for d in DatasetCatalog.get(dataset_name)}
+
+    def load(inp):
+        with Image.open(table[inp["file_name"]]) as im:
+            return np.array(im, dtype=np.int64)
+    return load
 
 
 def reduce_confusion(conf: torch.Tensor) -> torch.Tensor:
@@ -89,12 +101,18 @@ class SemSegEvaluator:
                  class_names: Optional[Sequence[str]] = None, ignore_label: Optional[int] = None,
                  gt_loader: Optional[Callable] = None, device=None):
         meta = _metadata(dataset_name)
-        self._class_names = list(class_names if class_names is not None else meta.stuff_classes)
+        if class_names is None:
+            class_names = meta.get("stuff_classes") if meta is not None else None
+            if class_names is None:
+                raise ValueError(f"SemSegEvaluator: no class names (dataset {dataset_name!r} has no 'stuff_classes' "
+                                 "metadata and class_names= was not given)")
+        self._class_names = list(class_names)
         self._num_classes = len(self._class_names)
         self._ignore_label = ignore_label if ignore_label is not None else (
-            meta.ignore_label if meta is not None else 255)
+            meta.get("ignore_label", 255) if meta is not None else 255)
         self._distributed = distributed
         self._output_dir = output_dir
+        self._dataset_name = dataset_name
         self._gt_loader = gt_loader
         self._device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.reset()
@@ -107,13 +125,19 @@ class SemSegEvaluator:
     def _gt(self, inp) -> torch.Tensor:
         gt = inp.get("sem_seg_gt")
         if gt is None:
+            if self._gt_loader is None and self._dataset_name and "file_name" in inp:
+                self._gt_loader = _catalog_gt_loader(self._dataset_name)
             if self._gt_loader is None:
-                raise KeyError("input has no 'sem_seg_gt' and no gt_loader was given")
+                raise KeyError("input has no 'sem_seg_gt' and no gt_loader / registered dataset was given")
             gt = self._gt_loader(inp)
         gt = torch.as_tensor(np.asarray(gt) if not torch.is_tensor(gt) else gt)
         return gt.to(self._device, torch.int32).contiguous()
 
     def process(self, inputs, outputs):
+        with torch.cuda.device(self._device):      # the kernel runs on this device's current stream
+            self._process(inputs, outputs)
+
+    def _process(self, inputs, outputs):
         for inp, out in zip(inputs, outputs):
             probs = out["sem_seg"] if isinstance(out, dict) else out
             probs = probs.to(self._device, torch.float32).contiguous()
@@ -154,7 +178,7 @@ class SemSegGzeroEvaluator(SemSegEvaluator):
         super().__init__(*args, **kw)
         if val_extra_classes is None:
             meta = _metadata(args[0] if args else kw.get("dataset_name"))
-            val_extra_classes = meta.val_extra_classes if meta is not None else ()
+            val_extra_classes = meta.get("val_extra_classes", ()) if meta is not None else ()
         self._val_extra_classes = list(val_extra_classes)
 
     def _metrics(self, conf):

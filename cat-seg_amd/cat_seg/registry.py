@@ -60,8 +60,14 @@ except Exception:  # noqa: BLE001
 
 
 def build_model(cfg):
-    """detectron2.modeling.build_model: META_ARCH_REGISTRY[cfg.MODEL.META_ARCHITECTURE](cfg)."""
+    """detectron2.modeling.build_model: META_ARCH_REGISTRY[cfg.MODEL.META_ARCHITECTURE](cfg), moved
+    to cfg.MODEL.DEVICE.  A "cuda" device is only bound when CUDA is present (the CPU-only
+    tests build models without a GPU; the HIP engine itself always needs one)."""
+    import torch
     model = META_ARCH_REGISTRY.get(cfg.MODEL.META_ARCHITECTURE)(cfg)
+    dev = torch.device(getattr(cfg.MODEL, "DEVICE", "cuda") or "cuda")
+    if dev.type != "cuda" or torch.cuda.is_available():
+        model.to(dev)
     return model
 
 

@@ -282,10 +282,12 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
 
 // split-K factor for the im2col kernel: grids far below the CU count (the per-image guidance
 // projections: 36-144 tiles over K = 9 x 256..768) split K so >= ~512 workgroups run;
-// never with GroupNorm statistics (partials are per output tile).
+// never with GroupNorm statistics (partials are per output tile).  Sized on ONE slice
+// (S = 1), never on the batch: the K partition, hence every output bit, must not depend on
+// how many images share the launch (batch invariance, the multi-GPU bit-identity gate).
 int conv_ksplit(const CatsegConvArgs* a) {
   if (a->stats) return 1;
-  const int64_t M = a->S * (int64_t)a->H * a->W;
+  const int64_t M = (int64_t)a->H * a->W;
   const int64_t tiles = ((M + BM - 1) / BM) * ((a->c_out + 127) / 128);
   const int64_t ktiles = (9LL * (a->c1 + a->c2) + BK - 1) / BK;
   int ks = 1;
