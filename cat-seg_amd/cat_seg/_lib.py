@@ -80,6 +80,7 @@ class ClassAttnArgs(C.Structure):
         ("y", vp), ("ld_y", i64),
         ("B", i64), ("T", i32), ("HW", i32), ("n_heads", i32), ("head_dim", i32),
         ("dtype", i32),
+        ("tgk_t", vp), ("ld_tgk_t", i64), ("tgk_t_bstride", i64),
     ]
 
 
@@ -146,6 +147,7 @@ _SIGS = {
     "catseg_corr_embed": [vp, i64, i64, vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, vp],
     "catseg_topk_classes": [vp, i64, i64, i64, i32, i32, i32, vp, vp],
     "catseg_gather_rows": [vp, i64, vp, i64, i64, vp, i64, i32, vp],
+    "catseg_transpose_rows": [vp, i64, i64, i64, i64, i64, vp, i64, i32, vp],
     "catseg_convert": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, vp],
     "catseg_fill_f32": [vp, i64, f32, vp],
     "catseg_preprocess_im2col": [vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, i64, i32, vp],
@@ -167,6 +169,7 @@ _SIGS = {
     "catseg_set_gemm_variant": [i32],
     "catseg_set_attn_variant": [i32],
     "catseg_set_ring_variant": [i32],
+    "catseg_set_classattn_variant": [i32],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
     "catseg_abi_version": [],
     "catseg_last_error": [],

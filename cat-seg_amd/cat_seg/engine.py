@@ -329,12 +329,14 @@ class CatSegEngine:
         ops.l2normalize(t, txn)                           # correlation's F.normalize (model.py:650)
         tg = torch.empty(T, D, device=dev, dtype=dt)       # text_guidance_projection (model.py:712-715)
         ops.gemm(txn, self.w.tg_w, tg, bias=self.w.tg_b, act=L.ACT_RELU)
-        tgqk = []
+        tgqk, tgkt = [], []
         for lay in self.w.layers:
             o = torch.empty(T, 2 * D, device=dev, dtype=dt)
             ops.gemm(tg, lay.ca.wqk_t, o)
             tgqk.append(o)
-        self._text = _NS(T=T, txn=txn, tgqk=tgqk, src=text)
+            if dt == torch.bfloat16 and T <= self.arch.pad_len:   # the fused class attention's k half, transposed
+                tgkt.append(ops.class_attention_kt(o, T))
+        self._text = _NS(T=T, txn=txn, tgqk=tgqk, tgkt=tgkt or None, src=text)
 
     # ------------------------------------------------------------------ image encoder
     def encode_image(self, raw: torch.Tensor, sizes: torch.Tensor):
@@ -454,16 +456,18 @@ class CatSegEngine:
         HWc = (H_ // ph) * (W_ // pw)          # pixels per class-attention slice
         # ---- text guidance terms per class (gathered per image after top-k) ----
         if classes is not None:
-            tgqk = []
+            tgqk, tgkt = [], []
             idx = classes.reshape(-1).contiguous()
             for t in tx.tgqk:
                 o = torch.empty(S, 2 * D, device=dev, dtype=dt)
                 ops.gather_rows(t, idx, o)
                 tgqk.append(o)
+                if dt == torch.bfloat16:
+                    tgkt.append(ops.class_attention_kt(o, T, B))
             tmap = rowmap(d1=HWc)
             tg_bstride = T
         else:
-            tgqk = tx.tgqk
+            tgqk, tgkt = tx.tgqk, tx.tgkt
             tmap = rowmap(d1=HWc, m1=T)
             tg_bstride = 0
         # ---- aggregation layers (model.py:717-718) ----
@@ -512,7 +516,8 @@ class CatSegEngine:
                 if fused_class:
                     ops.class_attention(X, (ca.n1w, ca.n1b), ca.wqkv, ca.bqkv, tgqk[l], Y, B=B, T=T, HW=HW,
                                         n_heads=a.nheads, head_dim=D // a.nheads, tg_bstride=tg_bstride,
-                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"),
+                                        tgk_t=tgkt[l] if tgkt else None)
                 else:
                     ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
                                   add_ncols=2 * D)
@@ -528,7 +533,8 @@ class CatSegEngine:
                 if fused_class:
                     ops.class_attention(Xp, (ca.n1w, ca.n1b), ca.wqkv, ca.bqkv, tgqk[l], Yp, B=B, T=T, HW=HWc,
                                         n_heads=a.nheads, head_dim=D // a.nheads, tg_bstride=tg_bstride,
-                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                                        n_pad=n_pad, k_pad=ca.get("kpad"), v_pad=ca.get("vpad"),
+                                        tgk_t=tgkt[l] if tgkt else None)
                 else:
                     qkvp = qkv[:Rp]
                     ops.rows_gemm(Xp, ca.wqkv, qkvp, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,

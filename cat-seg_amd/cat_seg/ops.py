@@ -224,9 +224,12 @@ def swin_window_attention(x, ln, w_qkv, b_qkv, gqk, gmap, out, *, S, img_hw, win
 
 
 def class_attention(x, ln, w_qkv, b_qkv, tg, y, *, B, T, HW, n_heads, head_dim, tg_bstride=0, n_pad=0,
-                    k_pad=None, v_pad=None, eps=1e-5, attn_eps=1e-6):
+                    k_pad=None, v_pad=None, eps=1e-5, attn_eps=1e-6, tgk_t=None):
     """Fused norm1 + q/k/v (+ text-guidance half) + linear class attention + residual
-    (catseg_class_attention): y = x + LinearAttention(...)."""
+    (catseg_class_attention): y = x + LinearAttention(...).  tgk_t: the transposed k half of tg
+    (class_attention_kt), made here when not given."""
+    if tgk_t is None:
+        tgk_t = class_attention_kt(tg if tg_bstride == 0 else tg[:B * T], T, 1 if tg_bstride == 0 else B)
     a = L.ClassAttnArgs()
     a.x, a.ld_x = x.data_ptr(), _ld(x)
     a.ln_g, a.ln_b, a.eps = ln[0].data_ptr(), ln[1].data_ptr(), eps
@@ -235,6 +238,8 @@ def class_attention(x, ln, w_qkv, b_qkv, tg, y, *, B, T, HW, n_heads, head_dim, 
     a.n_pad, a.k_pad, a.v_pad, a.attn_eps = n_pad, _p(k_pad), _p(v_pad), attn_eps
     a.y, a.ld_y = y.data_ptr(), _ld(y)
     a.B, a.T, a.HW, a.n_heads, a.head_dim, a.dtype = B, T, HW, n_heads, head_dim, _dt(x)
+    a.tgk_t, a.ld_tgk_t = tgk_t.data_ptr(), tgk_t.shape[-1]
+    a.tgk_t_bstride = tgk_t.shape[-2] * tgk_t.shape[-1] if tgk_t.shape[0] > 1 else 0
     R = B * T * HW
     C = n_heads * head_dim
     flops = 2 * R * C * 3 * C + 4 * R * n_heads * head_dim * head_dim
@@ -358,6 +363,23 @@ def corr_embed(corr, *, t_stride, b_stride, B, T, H, W, weight, bias, out, class
 def topk_classes(corr, *, t_stride, b_stride, B, T, HW, k, out):
     call("catseg_topk_classes", corr.data_ptr(), t_stride, b_stride, B, T, HW, k, out.data_ptr(), _stream())
     return out
+
+
+def transpose_rows(x, out, *, rows, batch=1, in_bstride=0):
+    """out[b][c][r] = x[b*in_bstride + r][c] (r < rows), zero for rows <= r < out.shape[-1]
+    (catseg_transpose_rows); x (., cols) with any row stride, out (batch, cols, ld) contiguous."""
+    cols = out.shape[-2]
+    call("catseg_transpose_rows", x.data_ptr(), _ld(x), rows, cols, batch, in_bstride, out.data_ptr(),
+         out.shape[-1], _dt(x), _stream())
+    return out
+
+
+def class_attention_kt(tg, T, batch=1):
+    """The k half of the class-attention text guidance transposed per image: (batch, 128, Tp),
+    Tp = T rounded up to 16, zero past T (catseg_class_attention's tgk_t)."""
+    Tp = (T + 15) // 16 * 16
+    out = torch.empty(batch, tg.shape[1] // 2, Tp, device=tg.device, dtype=tg.dtype)
+    return transpose_rows(tg[:, tg.shape[1] // 2:], out, rows=T, batch=batch, in_bstride=T if batch > 1 else 0)
 
 
 def gather_rows(x, idx, out):

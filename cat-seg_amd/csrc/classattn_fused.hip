@@ -290,6 +290,8 @@ __global__ __launch_bounds__(NT, 2) void classattn_kernel(ClsP a) {
 
 }  // namespace
 
+int classattn2_launch(const CatsegClassAttnArgs* a, hipStream_t st);   // classattn2.hip (default kernel)
+
 extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->x && a->w_qkv && a->b_qkv && a->ln_g && a->ln_b && a->tg && a->y,
                "class_attention: null pointer");
@@ -310,6 +312,9 @@ extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream
   p.k_pad = a->k_pad; p.v_pad = a->v_pad; p.n_pad = a->n_pad; p.attn_eps = a->attn_eps;
   p.y = (bf16*)a->y; p.ld_y = a->ld_y;
   p.B = a->B; p.T = a->T; p.HW = a->HW;
+  const int rc2 = classattn2_launch(a, (hipStream_t)stream);
+  if (rc2 == 0) return catseg_launch_status("class_attention");
+  if (rc2 < 0) return rc2;
   static int cus = 0;
   if (!cus) {
     int dev = 0;

@@ -595,6 +595,30 @@ extern "C" int catseg_gather_rows(const void* in, int64_t ld_in, const int32_t* 
   return catseg_launch_status("gather_rows");
 }
 
+// out[b][c][r] = in[b * in_bstride + r][c] (r < rows), 0 for rows <= r < ld_out
+template <typename E>
+__global__ void transpose_rows_kernel(const E* in, int64_t ld_in, int64_t rows, int64_t cols, int64_t in_bstride,
+                                      E* out, int64_t ld_out, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i % ld_out, bc = i / ld_out, c = bc % cols, b = bc / cols;
+    out[i] = r < rows ? in[(b * in_bstride + r) * ld_in + c] : (E)0;
+  }
+}
+
+extern "C" int catseg_transpose_rows(const void* in, int64_t ld_in, int64_t rows, int64_t cols, int64_t batch,
+                                     int64_t in_bstride, void* out, int64_t ld_out, int dtype, void* stream) {
+  CATSEG_CHECK(in && out && rows > 0 && cols > 0 && batch > 0 && ld_out >= rows && ld_in >= cols,
+               "transpose_rows: bad args");
+  const int64_t total = batch * cols * ld_out;
+  if (dtype == CATSEG_BF16)
+    hipLaunchKernelGGL(transpose_rows_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)in, ld_in, rows, cols, in_bstride, (bf16*)out, ld_out, total);
+  else
+    hipLaunchKernelGGL(transpose_rows_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)in, ld_in, rows, cols, in_bstride, (float*)out, ld_out, total);
+  return catseg_launch_status("transpose_rows");
+}
+
 extern "C" int catseg_fill_f32(float* out, int64_t n, float value, void* stream) {
   CATSEG_CHECK(out && n > 0, "fill: bad args");
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, value);

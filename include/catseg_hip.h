@@ -291,6 +291,11 @@ void catseg_set_corr_mfma(int enable);
 int catseg_topk_classes(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
                         int64_t B, int T, int HW, int k, int32_t* classes, void* stream);
 
+/* catseg_transpose_rows — out[b][c][r] = in[b*in_bstride + r][c] for r < rows, 0 for
+ * rows <= r < ld_out (the transposed text-guidance k half of catseg_class_attention). */
+int catseg_transpose_rows(const void* in, int64_t ld_in, int64_t rows, int64_t cols, int64_t batch,
+                          int64_t in_bstride, void* out, int64_t ld_out, int dtype, void* stream);
+
 /* catseg_gather_rows — out[r] = in[idx[r]] for fp32/bf16 rows (text guidance gather
  * of model.py:697-698). */
 int catseg_gather_rows(const void* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols,
@@ -380,8 +385,16 @@ typedef struct {
   void* y; int64_t ld_y;
   int64_t B; int T; int HW; int n_heads; int head_dim;
   int dtype;
+  /* the k half of tg transposed, [128][ld_tgk_t] per image (catseg_transpose_rows), image b
+   * at element offset b*tgk_t_bstride (0 = shared); ld_tgk_t >= round_up(T, 16), zero past T.
+   * Required by the default kernel (variant 0); null selects variant 1. */
+  const void* tgk_t; int64_t ld_tgk_t; int64_t tgk_t_bstride;
 } CatsegClassAttnArgs;
 int catseg_class_attention(const CatsegClassAttnArgs* args, void* stream);
+/* kernel choice for catseg_class_attention (A/B and tests): 0 = register-resident form, one
+ * pixel per 4-wave workgroup (classattn2.hip, default, T <= 256); 1 = the chunked two-pass form
+ * (classattn_fused.hip). */
+void catseg_set_classattn_variant(int variant);
 
 /* ---------------------------------------------------------------------------
  * Class-attention pooling (POOLING_SIZES != [1,1]; ClassTransformerLayer,

@@ -6,7 +6,9 @@ Each DIR is a rocprofv3 -d output directory (one counter pass).  Prints, per ker
 counter averaged per dispatch, plus derived ratios when their inputs are present:
   wait%/inst%/active% = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES,
   valu/mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA, bank% = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE,
-  fetchMB = 2 x FETCH_SIZE (gfx950 tallies 128-B streaming requests at 64 B), writeMB = WRITE_SIZE.
+  fetchMB = 2 x FETCH_SIZE (gfx950 tallies 128-B streaming requests at 64 B), writeMB = WRITE_SIZE,
+  clk = GRBM_GUI_ACTIVE / 8 (sum over the XCDs) / duration, each counter averaged over the
+  dispatches of the passes that collected it (GRBM_GUI_ACTIVE is in every pass).
 """
 import collections
 import csv
@@ -22,14 +24,15 @@ if "--top" in sys.argv:
 kern = collections.OrderedDict()
 for d in args:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        seen = set()
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
-            k = kern.setdefault(name, {"disp": set(), "dur": {}, "ctr": collections.defaultdict(float)})
+            k = kern.setdefault(name, {"disp": collections.defaultdict(set), "dur": {},
+                                       "ctr": collections.defaultdict(lambda: collections.defaultdict(float))})
             key = (f, row["Dispatch_Id"])
-            k["disp"].add(key)
+            k["disp"][f].add(key)
             k["dur"][key] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-3
-            k["ctr"][row["Counter_Name"]] += float(row["Counter_Value"])
+            # one row per counter instance (XCD / SE): summed, as rocprofv3 reports them
+            k["ctr"][f][row["Counter_Name"]] += float(row["Counter_Value"])
 
 
 def short(n):
@@ -39,12 +42,16 @@ def short(n):
 
 rows = []
 for name, k in kern.items():
-    nd = len(k["disp"])
-    # counters are summed over every pass's dispatches: average per dispatch of the pass
-    # that collected them (each pass saw the same dispatch sequence)
-    passes = len({key[0] for key in k["disp"]})
-    per = nd / max(passes, 1)
-    avg = {c: v / per for c, v in k["ctr"].items()}
+    passes = len(k["disp"])
+    per = sum(len(v) for v in k["disp"].values()) / max(passes, 1)     # dispatches per pass
+    # a counter collected in several passes (GRBM_GUI_ACTIVE rides along in each) is averaged
+    # over the dispatches of exactly the passes that collected it, never summed across them
+    tot_c, n_c = collections.defaultdict(float), collections.defaultdict(int)
+    for f, cs in k["ctr"].items():
+        for cn, v in cs.items():
+            tot_c[cn] += v
+            n_c[cn] += len(k["disp"][f])
+    avg = {cn: tot_c[cn] / n_c[cn] for cn in tot_c}
     rows.append((sum(k["dur"].values()) / max(passes, 1), name, per, avg))
 rows.sort(key=lambda r: -r[0])
 for tot, name, per, c in rows[:top]:
@@ -66,7 +73,10 @@ for tot, name, per, c in rows[:top]:
     if "WRITE_SIZE" in c:
         d.append(f"write {c['WRITE_SIZE'] / 1024:8.1f} MB")
     if c.get("GRBM_GUI_ACTIVE"):
-        d.append(f"clk {c['GRBM_GUI_ACTIVE'] / 8 / (tot / per) / 1e3:4.2f} GHz")
+        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall (MI355X_MICROARCH.md "DVFS give-back");
+        # it reads high on dispatches shorter than ~0.3 ms: marked "~" there
+        us = tot / per
+        d.append(f"clk {'~' if us < 300 else ''}{c['GRBM_GUI_ACTIVE'] / 8 / us / 1e3:4.2f} GHz")
     print(line)
     if d:
         print("      " + "  ".join(d))
