@@ -92,6 +92,9 @@ void catseg_set_gemm_fp8_variant(int variant);
  * pipelined kernel, 1..8 = force one of its tile / stage / K-depth configurations
  * (gemm.hip try_gemm3) where the shape allows.  For A/B tests and tuning; process-wide. */
 void catseg_set_gemm_variant(int variant);
+/* tile order of the pipelined bf16/fp8 GEMM: 0 = row-major, G > 0 = grouped (G m-tiles swept
+ * across all n-tiles, so an XCD's contiguous tile range is a 2-D block of the output) */
+void catseg_set_gemm_group(int group_m);
 
 /* ---------------------------------------------------------------------------
  * Row-block kernels over the 128-channel cost-embedding rows (K = 128).

@@ -12,6 +12,7 @@ from cat_seg import ops
 from cat_seg import _lib as L
 
 variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").split(",")]
+# variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (catseg_set_gemm_group)
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True)}
@@ -33,8 +34,11 @@ for name, (N, K, act, has_res) in shapes.items():
         ref = ref + R.float()
     def run():
         ops.gemm(A, W, out, bias=bias, act=act, res=R)
+    def setv(v):
+        lib.catseg_set_gemm_variant(0 if v >= 1000 else v)
+        lib.catseg_set_gemm_group(v - 1000 if v >= 1000 else 0)
     for v in variants:
-        lib.catseg_set_gemm_variant(v)
+        setv(v)
         out.zero_()
         run(); torch.cuda.synchronize()
         err = (out.float() - ref).abs().max().item()
@@ -42,7 +46,7 @@ for name, (N, K, act, has_res) in shapes.items():
     flops = 2 * M * N * K
     for rnd in range(7):
         for v in variants:
-            lib.catseg_set_gemm_variant(v)
+            setv(v)
             run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -68,3 +72,4 @@ for name, (N, K, act, has_res) in shapes.items():
         print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  "
               f"max_err {res[(name, v)]['err']:.3e}", flush=True)
 lib.catseg_set_gemm_variant(0)
+lib.catseg_set_gemm_group(0)
