@@ -137,6 +137,9 @@ _SIGS = {
     "catseg_linear_attention": [C.POINTER(LinAttnArgs), vp],
     "catseg_conv3x3": [C.POINTER(ConvArgs), vp],
     "catseg_conv3x3_partial": [vp, i64, i32, i32, i32, vp, i32, vp, i32, vp],
+    "catseg_upconv3x3": [C.POINTER(ConvArgs), vp],
+    "catseg_upconv3x3_stats_tile": [],
+    "catseg_upconv_addend": [vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, vp],
     "catseg_conv_tile_rows": [],
     "catseg_conv3x3_stats_tile": [C.POINTER(ConvArgs)],
     "catseg_conv3x3_workspace": [C.POINTER(ConvArgs)],

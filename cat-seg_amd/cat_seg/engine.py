@@ -59,6 +59,7 @@ class CatSegEngine:
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
         self.split_guidance = True      # bf16: decoder conv guidance half once per image (A/B switch)
+        self.fold_upconv = True         # bf16: second Up block's ConvTranspose folded into its conv (A/B switch)
         self.device = torch.device(device)
         # config 5: the CLIP image encoder's block GEMMs (q/k/v, out-proj, c_fc, c_proj) in
         # OCP e4m3 with per-row scales (catseg_gemm_fp8); bf16 engine only
@@ -127,6 +128,29 @@ class CatSegEngine:
     def _convt_w(w, b):  # ConvTranspose2d (ci, co, k, k) -> GEMM W [(ky, kx, co)][ci], bias per n
         ci, co, k, _ = w.shape
         return w.permute(2, 3, 1, 0).reshape(k * k * co, ci), b.repeat(k * k)
+
+    @staticmethod
+    def _upconv_weights(wt, bt, wc):
+        """Composite weights of ConvTranspose2d(k=2, s=2) followed by a 3x3 / pad-1 conv (the x half
+        of Up's first conv, model.py:546-555) as catseg_upconv3x3 reads them.  wt (ci, m, 2, 2),
+        bt (m,), wc (co, m, 3, 3).  The conv tap (dy, dx) at output pixel (2y + a, 2x + b) reads
+        ConvTranspose output (2y + a + dy, 2x + b + dx) = source pixel (y + (a+dy)//2, x + (b+dx)//2)
+        through kernel entry ((a+dy)%2, (b+dx)%2); summed per source tap in float64.
+        Returns the bf16-ready fp32 [4*co][9*ci] (row block 2a+b = parity (a, b)) and the fp32
+        tap bias [9][co] = wc[:, :, tap] . bt (the ConvTranspose bias through each conv tap)."""
+        ci, m = wt.shape[:2]
+        co = wc.shape[0]
+        wt64, wc64 = wt.double(), wc.double()
+        comp = torch.zeros(4, co, 3, 3, ci, dtype=torch.float64)
+        for a_ in (0, 1):
+            for b_ in (0, 1):
+                for dy in (-1, 0, 1):
+                    for dx in (-1, 0, 1):
+                        sy, sx = (a_ + dy) // 2, (b_ + dx) // 2
+                        py, px = (a_ + dy) % 2, (b_ + dx) % 2
+                        comp[2 * a_ + b_, :, sy + 1, sx + 1, :] += wc64[:, :, dy + 1, dx + 1] @ wt64[:, :, py, px].t()
+        tap_b = torch.einsum("omyx,m->yxo", wc64, bt.double()).reshape(9, co)
+        return comp.reshape(4 * co, 9 * ci).float(), tap_b.float()
 
     def _prepare(self, sd):
         a = self.arch
@@ -213,7 +237,9 @@ class CatSegEngine:
             ww, bb = self._convt_w(sd[q + "up.weight"], sd[q + "up.bias"])
             cu = sd[q + "up.weight"].shape[1]
             c0 = sd[q + "conv.double_conv.0.weight"]
+            upc_w, upc_tb = self._upconv_weights(sd[q + "up.weight"], sd[q + "up.bias"], c0[:, :cu])
             w.dec.append(_NS(
+                upc_w=self._W(upc_w), upc_tb=self._F(upc_tb),
                 up_w=self._W(ww), up_b=self._F(bb), up_c=cu,
                 c0=self._W(self._conv_w(c0)),
                 # [x | g] split of the first conv (model.py:551-554): the guidance half runs
@@ -550,39 +576,55 @@ class CatSegEngine:
         for i, dec in enumerate(w.dec):
             cu = dec.up_c
             Ho = Hc * 2
-            up = torch.empty(S * Ho * Ho, cu, device=dev, dtype=dt)
-            if src_gn is not None and dt == torch.bfloat16 and tuple(dec.up_w.shape) == (192, 64):
-                # GroupNorm+ReLU of the previous DoubleConv fused into this ConvTranspose
-                ops.convt64_gn(src, dec.up_w, up, HW=Hc * Hc, gn=src_gn, bias=dec.up_b, store=(2, Hc, Hc, cu))
-            else:
-                if src_gn is not None:
-                    z = torch.empty_like(src)
-                    m_, r_, g_, b_, cpg_ = src_gn
-                    ops.groupnorm_relu(src, z, S=S, HW=Hc * Hc, C=src.shape[1], cpg=cpg_, mean=m_, rstd=r_,
-                                       gamma=g_, beta=b_)
-                    src = z
-                if src.shape[1] == 128 and dec.up_w.shape[0] % 128 == 0:
-                    ops.rows_gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
-                else:
-                    ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
             cout = dec.c0.shape[0]
             groups = cout // 16
-            c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
-            gd = GD[i]
-            if self.split_guidance and dt == torch.bfloat16 and (cu, Ho) in ((96, 48), (48, 96)) and cout in (64, 32):
-                gpart = torch.empty(B * Ho * Ho, cout, device=dev, dtype=_f32)
-                ops.conv3x3_partial(gd, dec.c0_g, gpart, B=B, H=Ho, W=Ho)
-                kw = dict(S=S, H=Ho, W=Ho, c1=cu, addend=gpart, addend_div=T)
-                wc0 = dec.c0_x
+            if (self.fold_upconv and self.split_guidance and dt == torch.bfloat16 and src_gn is not None
+                    and src.shape[1] == 64 and cout == 32 and 48 <= Hc <= 50 and (Hc * Hc) % 128 == 0):
+                # ConvTranspose + conv over [up | guidance] as one 4-parity conv over the
+                # GroupNorm+ReLU'd source (catseg_upconv3x3); guidance half + ConvT bias as addend
+                gpart = torch.empty(B * Hc * Hc, 4 * cout, device=dev, dtype=_f32)
+                ops.upconv_addend(GD[i], dec.c0_g, dec.upc_tb, gpart, B=B, H2=Ho, W2=Ho)
+                tile = ops.upconv3x3_stats_tile()
+                ntl = 4 * Hc * Hc // tile
+                st = torch.empty(S * ntl * groups * 2, device=dev, dtype=_f32)
+                c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
+                ops.upconv3x3(src, dec.upc_w, c1, S=S, H=Hc, W=Hc, c1=src.shape[1], gn=src_gn, stats=st,
+                              addend=gpart, addend_div=T)
+                m1 = torch.empty(S * groups, device=dev, dtype=_f32)
+                r1 = torch.empty_like(m1)
+                ops.groupnorm_stats(st, S, ntl, groups, tile * 16, m1, r1)
             else:
-                kw = dict(S=S, H=Ho, W=Ho, c1=cu, src2=gd, c2=gd.shape[1], src2_div=T)
-                wc0 = dec.c0
-            tile = ops.conv3x3_stats_tile(up, wc0, **kw)
-            st = torch.empty(S * (Ho * Ho // tile) * groups * 2, device=dev, dtype=_f32)
-            ops.conv3x3(up, wc0, c1, stats=st, **kw)
-            m1 = torch.empty(S * groups, device=dev, dtype=_f32)
-            r1 = torch.empty_like(m1)
-            ops.groupnorm_stats(st, S, Ho * Ho // tile, groups, tile * 16, m1, r1)
+                up = torch.empty(S * Ho * Ho, cu, device=dev, dtype=dt)
+                if src_gn is not None and dt == torch.bfloat16 and tuple(dec.up_w.shape) == (192, 64):
+                    # GroupNorm+ReLU of the previous DoubleConv fused into this ConvTranspose
+                    ops.convt64_gn(src, dec.up_w, up, HW=Hc * Hc, gn=src_gn, bias=dec.up_b, store=(2, Hc, Hc, cu))
+                else:
+                    if src_gn is not None:
+                        z = torch.empty_like(src)
+                        m_, r_, g_, b_, cpg_ = src_gn
+                        ops.groupnorm_relu(src, z, S=S, HW=Hc * Hc, C=src.shape[1], cpg=cpg_, mean=m_, rstd=r_,
+                                           gamma=g_, beta=b_)
+                        src = z
+                    if src.shape[1] == 128 and dec.up_w.shape[0] % 128 == 0:
+                        ops.rows_gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+                    else:
+                        ops.gemm(src, dec.up_w, up, bias=dec.up_b, store=(2, Hc, Hc, cu))
+                c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
+                gd = GD[i]
+                if self.split_guidance and dt == torch.bfloat16 and (cu, Ho) in ((96, 48), (48, 96)) and cout in (64, 32):
+                    gpart = torch.empty(B * Ho * Ho, cout, device=dev, dtype=_f32)
+                    ops.conv3x3_partial(gd, dec.c0_g, gpart, B=B, H=Ho, W=Ho)
+                    kw = dict(S=S, H=Ho, W=Ho, c1=cu, addend=gpart, addend_div=T)
+                    wc0 = dec.c0_x
+                else:
+                    kw = dict(S=S, H=Ho, W=Ho, c1=cu, src2=gd, c2=gd.shape[1], src2_div=T)
+                    wc0 = dec.c0
+                tile = ops.conv3x3_stats_tile(up, wc0, **kw)
+                st = torch.empty(S * (Ho * Ho // tile) * groups * 2, device=dev, dtype=_f32)
+                ops.conv3x3(up, wc0, c1, stats=st, **kw)
+                m1 = torch.empty(S * groups, device=dev, dtype=_f32)
+                r1 = torch.empty_like(m1)
+                ops.groupnorm_stats(st, S, Ho * Ho // tile, groups, tile * 16, m1, r1)
             c2 = torch.empty_like(c1)
             kw2 = dict(S=S, H=Ho, W=Ho, c1=cout, gn=(m1, r1, *dec.g0, 16))
             tile = ops.conv3x3_stats_tile(c1, dec.c3, **kw2)

@@ -327,6 +327,37 @@ def conv3x3_partial(g, weight, out, *, B, H, W):
     return out
 
 
+def upconv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, gn=None, stats=None, stats_cpg=16,
+              addend=None, addend_div=1):
+    """ConvTranspose2d(k=2, s=2) + conv3x3 folded into one 4-parity conv over the ConvTranspose
+    input (catseg_upconv3x3): src1 [S][H][W][c1] -> out [S][2H][2W][c_out/4] with the composite
+    weight [4 * cout][9 * c1] (CatSegEngine._upconv_weights) and the parity-layout addend
+    (upconv_addend).  `stats` receives [S][4 * H*W / upconv3x3_stats_tile()][cout/16][2]."""
+    a = _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, 0, None, 0, 0, 0, 1, None, L.ACT_NONE, gn,
+                   stats, stats_cpg, addend, addend_div)
+    # executed MFMA work: 4 of the 9 taps per output parity
+    with _rec("upconv3x3", 2 * S * H * W * weight.shape[0] * 4 * c1):
+        call("catseg_upconv3x3", a, _stream())
+    return out
+
+
+def upconv3x3_stats_tile() -> int:
+    return L.load().catseg_upconv3x3_stats_tile()
+
+
+def upconv_addend(g, weight, tap_bias, out, *, B, H2, W2):
+    """catseg_upconv_addend: the guidance half of the Up conv on the 2H x 2W grid (fp32 weight
+    [cout][9 * cin]) + the ConvTranspose bias through the in-image taps (tap_bias [9][cout]), in
+    the parity layout [B][H2/2 * W2/2][4 * cout] of upconv3x3's addend."""
+    cout, k = weight.shape
+    cin = k // 9
+    assert g.shape[-1] == cin and out.dtype == torch.float32 and weight.dtype == torch.float32
+    with _rec("conv3x3_partial", 2 * B * H2 * W2 * cout * k):
+        call("catseg_upconv_addend", g.data_ptr(), B, H2, W2, cin, weight.data_ptr(), _p(tap_bias), cout,
+             out.data_ptr(), _dt(g), _stream())
+    return out
+
+
 def conv_tile_rows() -> int:
     return L.load().catseg_conv_tile_rows()
 

@@ -57,7 +57,11 @@ struct RingGeom {
 // for the 96-channel variant whose 108 weight VGPRs leave no room at 2)
 // NR: ring rows = rows a chunk can span + 2 halo rows (CH = 128: 4 + 2 at W >= 48, 3 + 2 at
 // W >= 64; CH = 64: 3 + 2 at W >= 48)
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD>
+// UP: the 4-parity form of ConvTranspose2d(k=2, s=2) followed by this conv (catseg_upconv3x3):
+// the source grid is the ConvTranspose INPUT, wave wco computes output parity
+// (a, b) = (wco >> 1, wco & 1) with its 2x2 of the 9 taps (rows a, a+1; columns b, b+1), and
+// channel block wco of COUT lands at pixel (2y + a, 2x + b) of the 2H x 2W output map.
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false>
 __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   constexpr int CPX = C / 8;
   constexpr int PS = RingGeom<C>::PS;
@@ -90,18 +94,23 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   // The trailing 16 channels of two taps share one K=32 step: lanes q < 2 carry tap 2p's
   // channels KC*32 + 8q.., lanes q >= 2 tap 2p+1's (zero weights past tap 8) -- the k order
   // inside an MFMA step is free as long as A and B agree.
-  s16x8 wf[9][KC > 0 ? KC : 1][FN];
+  static_assert(!UP || (WPX == 1 && WCO == 4 && !KT), "UP: one output parity per wave, C % 32 == 0");
+  constexpr int NTAP = UP ? 4 : 9;
+  const int pa = UP ? (wco >> 1) : 0, pb = UP ? (wco & 1) : 0;     // UP: this wave's output parity
+  s16x8 wf[NTAP][KC > 0 ? KC : 1][FN];
   s16x8 wt[NTP > 0 ? NTP : 1][FN];
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int n = wco * COW + 16 * i + r16;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int t = 0; t < NTAP; ++t) {
+      const int tap = UP ? (pa + t / 2) * 3 + pb + t % 2 : t;
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         uint4 u = ld16(p.w + ((int64_t)n * 9 + tap) * C + kc * 32 + 8 * q);
-        wf[tap][kc][i] = *reinterpret_cast<s16x8*>(&u);
+        wf[t][kc][i] = *reinterpret_cast<s16x8*>(&u);
       }
+    }
 #pragma unroll
     for (int tp = 0; tp < NTP; ++tp) {
       const int tap = 2 * tp + (q >> 1);
@@ -223,13 +232,35 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (UP) {
+      // taps (pa + sy, pb + sx): ring row y + pa + sy - 1, column x + pb + sx - 1
+      int rbu[2][FM];
+#pragma unroll
+      for (int sy = 0; sy < 2; ++sy)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) rbu[sy][j] = (((prow[j] + pa + sy) % NR) * WP + pcol[j] + pb) * PS;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          s16x8 xf[FM];
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            xf[j] = *reinterpret_cast<const s16x8*>(ring + rbu[t / 2][j] + 8 * q + (t % 2) * PS + kc * 32);
+#pragma unroll
+          for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wf[t][kc][i], xf[j], acc[i][j]);
+        }
+      }
+    }
     int rb[3][FM];                            // pixel (row y+dy-1, column x-1) of each tile row
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int j = 0; j < FM; ++j) rb[dy][j] = (((prow[j] + dy) % NR) * WP + pcol[j]) * PS;
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
+    for (int dy = 0; dy < (UP ? 0 : 3); ++dy) {
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int tap = dy * 3 + dx;
@@ -241,7 +272,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
           for (int i = 0; i < FN; ++i)
 #pragma unroll
-            for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wf[tap][kc][i], xf[j], acc[i][j]);
+            for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(wf[UP ? 0 : tap][kc][i], xf[j], acc[i][j]);
         }
       }
     }
@@ -301,14 +332,28 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         }
       }
     }
-    bf16* ob = p.out + ((int64_t)s * HW + p0 + wpx * PXW) * COUT + wco * COW;
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
+    if constexpr (UP) {
+      // parity (pa, pb) of source pixel (y, x) -> pixel (2y + pa, 2x + pb) of the 2H x 2W map, COW channels
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        store4<bf16>(ob + (int64_t)(16 * j + r16) * COUT + 16 * i + 4 * q, v);
+        const int pp = p0 + 16 * j + r16, yy = pp / W, xx = pp - yy * W;
+        bf16* ob = p.out + ((int64_t)s * 4 * HW + (2 * yy + pa) * (2 * W) + 2 * xx + pb) * COW;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          store4<bf16>(ob + 16 * i + 4 * q, v);
+        }
       }
+    } else {
+      bf16* ob = p.out + ((int64_t)s * HW + p0 + wpx * PXW) * COUT + wco * COW;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          store4<bf16>(ob + (int64_t)(16 * j + r16) * COUT + 16 * i + 4 * q, v);
+        }
+    }
 
     // ---- rotate the ring: prefetched rows into the slots the next chunk no longer needs ----
     __syncthreads();
@@ -328,7 +373,7 @@ size_t ring_lds(int W, int NR) { return (size_t)NR * (W + 2) * RingGeom<C>::PS *
 // NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
 // <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
 // adds <= 2 rows (104).
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD>
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false>
 int launch_ring_t(const RingP& p0, hipStream_t st) {
   RingP p = p0;
   const int nchunks = p.H * p.W / CH;
@@ -344,11 +389,11 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   const size_t sh = ring_lds<C>(p.W, NR);
   static size_t configured = 0;
   if (sh > configured) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD>), dim3((unsigned)(p.S * bands)), dim3(NT), sh, st, p);
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>), dim3((unsigned)(p.S * bands)), dim3(NT), sh, st, p);
   return 0;
 }
 
@@ -391,6 +436,66 @@ __global__ __launch_bounds__(256) void conv_partial_kernel(const T* __restrict__
       }
     }
     *reinterpret_cast<float4*>(out + pixg * cout + cg * 4) = make_float4(a0, a1, a2, a3);
+  }
+}
+
+// bf16 guidance with CIN % 8 == 0 channels: the same sum, the pixel's channels of a tap read
+// as 16-byte vectors (the scalar 2-byte loads above issue one VMEM instruction per FMA group
+// and bound the kernel at ~10 TF/s); weights stay fp32 in LDS, summation order tap-major as above
+// PAR (catseg_upconv_addend): also + tap_bias[tap][co] for every in-image tap, and the output in
+// the parity layout of catseg_upconv3x3's addend: [b][(y/2)*(W/2) + x/2][((y%2)*2 + x%2)*cout + co]
+template <int CIN, bool PAR = false>
+__global__ __launch_bounds__(256) void conv_partial_vec_kernel(const bf16* __restrict__ g, int64_t B, int H, int W,
+                                                              const float* __restrict__ w, int cout, float* out,
+                                                              const float* __restrict__ tap_bias = nullptr) {
+  extern __shared__ float sw[];        // [9][CIN][cout] (+ PAR: [9][cout] tap bias)
+  for (int i = threadIdx.x; i < 9 * CIN * cout; i += blockDim.x) {
+    const int co = i % cout, ci = (i / cout) % CIN, tap = i / (cout * CIN);
+    sw[i] = w[((int64_t)co * 9 + tap) * CIN + ci];
+  }
+  float* stb = sw + 9 * CIN * cout;
+  if constexpr (PAR)
+    for (int i = threadIdx.x; i < 9 * cout; i += blockDim.x) stb[i] = tap_bias ? tap_bias[i] : 0.f;
+  __syncthreads();
+  const int groups = cout / 4;
+  const int64_t total = B * H * W * groups;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(idx % groups);
+    const int64_t pixg = idx / groups;
+    const int64_t b = pixg / (H * W);
+    const int pix = (int)(pixg % (H * W));
+    const int y = pix / W, x = pix % W;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+      if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+      const bf16* src = g + ((b * H + yy) * W + xx) * CIN;
+      uint4 u[CIN / 8];
+#pragma unroll
+      for (int v = 0; v < CIN / 8; ++v) u[v] = ld16(src + 8 * v);
+      const bf16* e = reinterpret_cast<const bf16*>(u);
+      const float* wt = sw + tap * CIN * cout + cg * 4;
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci) {
+        const float v = bf2f(e[ci]);
+        const float4 ww = *reinterpret_cast<const float4*>(wt + ci * cout);
+        a0 += v * ww.x; a1 += v * ww.y; a2 += v * ww.z; a3 += v * ww.w;
+      }
+    }
+    if constexpr (PAR) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+        const float4 tb = *reinterpret_cast<const float4*>(stb + tap * cout + cg * 4);
+        a0 += tb.x; a1 += tb.y; a2 += tb.z; a3 += tb.w;
+      }
+      const int64_t o = ((b * (H / 2) + y / 2) * (W / 2) + x / 2) * 4 * cout + ((y & 1) * 2 + (x & 1)) * cout + cg * 4;
+      *reinterpret_cast<float4*>(out + o) = make_float4(a0, a1, a2, a3);
+    } else {
+      *reinterpret_cast<float4*>(out + pixg * cout + cg * 4) = make_float4(a0, a1, a2, a3);
+    }
   }
 }
 
@@ -472,7 +577,26 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
   }
   const int64_t total = B * H * W * (cout / 4);
   const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
-  if (dtype == CATSEG_BF16)
+  const bool vec = dtype == CATSEG_BF16 && ((uintptr_t)g % 16) == 0 && (cin == 16 || cin == 32);
+  if (vec) {
+    // grid-stride over the pixels with ~2 workgroups per CU: the [9][cin][cout] weight image
+    // (up to 73 KB, a strided gather) is staged once per workgroup, not once per 256 pixels
+    const unsigned vgrid = (unsigned)std::min<int64_t>((total + 255) / 256, 512);
+    static bool vconfigured = false;
+    if (!vconfigured) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_vec_kernel<16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_vec_kernel<32>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      vconfigured = true;
+    }
+    if (cin == 16)
+      hipLaunchKernelGGL(conv_partial_vec_kernel<16>, dim3(vgrid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B,
+                         H, W, weight, cout, out);
+    else
+      hipLaunchKernelGGL(conv_partial_vec_kernel<32>, dim3(vgrid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B,
+                         H, W, weight, cout, out);
+  } else if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(conv_partial_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B, H,
                        W, cin, weight, cout, out);
   else
@@ -482,3 +606,69 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
 }
 
 extern "C" void catseg_set_ring_variant(int v) { g_ring_variant = v; }
+
+// ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
+// The conv over the ConvTranspose output y (2H x 2W, no nonlinearity between them) equals, per
+// output parity (a, b), a 2x2-tap conv over the ConvTranspose INPUT with composite weights
+// W_c(a,b)[co][tap][ci] = sum over the conv taps that land on source tap `tap` of
+// W_conv[co][.][m] W_convT[ci][m][py][px] (built by the caller), plus the ConvTranspose bias
+// pushed through the conv taps that fall inside the image (the addend, catseg_upconv_addend).
+// The 2H x 2W ConvTranspose output is never materialised.
+extern "C" int catseg_upconv_addend(const void* g, int64_t B, int H2, int W2, int cin, const float* weight,
+                                    const float* tap_bias, int cout, float* out, int dtype, void* stream) {
+  CATSEG_CHECK(g && weight && out && B > 0 && H2 > 0 && W2 > 0 && H2 % 2 == 0 && W2 % 2 == 0, "upconv_addend: bad args");
+  CATSEG_CHECK(dtype == CATSEG_BF16 && (cin == 16 || cin == 32) && ((uintptr_t)g % 16) == 0,
+               "upconv_addend: bf16 guidance with 16 or 32 channels, 16B aligned");
+  CATSEG_CHECK(cout % 4 == 0 && (size_t)(9 * cin * cout + 9 * cout) * 4 <= 128 * 1024 && ((uintptr_t)out % 16) == 0 &&
+                   (!tap_bias || ((uintptr_t)tap_bias % 16) == 0),
+               "upconv_addend: cout % 4, weights <= 128 KB, 16B aligned out / tap_bias");
+  const size_t sh = (size_t)(9 * cin * cout + 9 * cout) * 4;
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_vec_kernel<16, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_vec_kernel<32, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    configured = true;
+  }
+  const int64_t total = B * H2 * W2 * (cout / 4);
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 512);
+  if (cin == 16)
+    hipLaunchKernelGGL((conv_partial_vec_kernel<16, true>), dim3(grid), dim3(256), sh, (hipStream_t)stream,
+                       (const bf16*)g, B, H2, W2, weight, cout, out, tap_bias);
+  else
+    hipLaunchKernelGGL((conv_partial_vec_kernel<32, true>), dim3(grid), dim3(256), sh, (hipStream_t)stream,
+                       (const bf16*)g, B, H2, W2, weight, cout, out, tap_bias);
+  return catseg_launch_status("upconv_addend");
+}
+
+// Pixels per GroupNorm partial of catseg_upconv3x3 on the SOURCE grid; its stats hold
+// [S][4 * H*W / tile][c_out/4/16][2] (parity-major partials).
+extern "C" int catseg_upconv3x3_stats_tile(void) { return 64; }
+
+extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->src1 && a->weight && a->out, "upconv3x3: null pointer");
+  CATSEG_CHECK(a->dtype == CATSEG_BF16 && a->c2 == 0 && !a->src2, "upconv3x3: bf16, one source");
+  CATSEG_CHECK(a->c1 == 64 && a->c_out == 128 && a->W >= 48 && a->W <= 50 && ((int64_t)a->H * a->W) % 128 == 0,
+               "upconv3x3: instantiated for 64 source channels -> 4 x 32 outputs on a 48..50-wide source grid");
+  CATSEG_CHECK(a->s1_offset == 0 && a->s1_slice_stride % 8 == 0, "upconv3x3: src stride alignment");
+  CATSEG_CHECK(!a->stats || a->stats_cpg == 16, "upconv3x3: GN stats in 16-channel groups");
+  CATSEG_CHECK(!a->gn_mean || (a->gn_rstd && a->gn_gamma && a->gn_beta && a->gn_cpg > 0 && a->c1 % a->gn_cpg == 0),
+               "upconv3x3: bad GroupNorm prologue");
+  CATSEG_CHECK(!a->addend || (((uintptr_t)a->addend % 16) == 0 && a->addend_slice_stride % 4 == 0),
+               "upconv3x3: addend alignment");
+  RingP p;
+  p.s1 = (const bf16*)a->src1; p.s1_ss = a->s1_slice_stride; p.c1 = a->c1;
+  p.s2 = nullptr; p.s2_ss = 0; p.c2 = 0; p.s2_div = 1;
+  p.S = a->S; p.H = a->H; p.W = a->W;
+  p.w = (const bf16*)a->weight; p.bias = a->bias; p.act = a->act;
+  p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
+  p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
+  p.out = (bf16*)a->out; p.stats = a->stats;
+  hipStream_t st = (hipStream_t)stream;
+  // 64-pixel chunks (a 48-wide chunk spans <= 3 rows: 5-row ring, <= 2 new rows = 104 positions):
+  // 128-pixel chunks spilled ~100 VGPRs with the addend
+  if (p.add) launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true>(p, st);
+  else launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true>(p, st);
+  return catseg_launch_status("upconv3x3");
+}

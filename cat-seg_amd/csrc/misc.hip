@@ -31,18 +31,24 @@ __global__ void rownorm_kernel(const TI* __restrict__ in, int64_t ld_in, RowMap 
   if (row >= rows) return;
   const TI* x = in + rowmap(inmap, row) * ld_in;
   float v[MAXV][4];
-  float s = 0.f;
-  int nv = 0;
+  float4 gv[LN ? MAXV : 1], bv[LN ? MAXV : 1];
+  // the row and (LayerNorm) gamma / beta are all requested before the first reduction, so the
+  // affine parameters do not add a dependent global-load round trip after it
 #pragma unroll
   for (int it = 0; it < MAXV; ++it) {
     const int c = (it * 64 + lane) * 4;
     if (c < cols) {
       load4<TI>(x + c, v[it]);
-      s += v[it][0] + v[it][1] + v[it][2] + v[it][3];
-      nv = it + 1;
+      if constexpr (LN) {
+        gv[it] = *reinterpret_cast<const float4*>(gamma + c);
+        bv[it] = *reinterpret_cast<const float4*>(beta + c);
+      }
     }
   }
-  (void)nv;
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXV; ++it)
+    if ((it * 64 + lane) * 4 < cols) s += v[it][0] + v[it][1] + v[it][2] + v[it][3];
   if (LN) {
     const float mean = warp_sum(s) / cols;
     float q = 0.f;
@@ -63,7 +69,7 @@ __global__ void rownorm_kernel(const TI* __restrict__ in, int64_t ld_in, RowMap 
       if (c < cols) {
         float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = v[it][r] * rstd * gamma[c + r] + beta[c + r];
+        for (int r = 0; r < 4; ++r) o[r] = v[it][r] * rstd * (&gv[it].x)[r] + (&bv[it].x)[r];
         store4<TO>(out + row * ld_out + c, o);
       }
     }
@@ -97,6 +103,7 @@ int rownorm(const void* in, int64_t ld_in, CatsegRowMap m, int dti, void* out, i
   CATSEG_CHECK(cols % 4 == 0 && cols <= 64 * 4 * MAXV, "rownorm: cols must be a multiple of 4 and <= 2048");
   CATSEG_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, "rownorm: strides must be multiples of 4");
   CATSEG_CHECK(!LN || (gamma && beta), "layernorm: gamma/beta missing");
+  CATSEG_CHECK(!LN || ((uintptr_t)gamma % 16 == 0 && (uintptr_t)beta % 16 == 0), "layernorm: gamma/beta must be 16B aligned");
   CATSEG_CHECK(m.d1 > 0 && m.m1 > 0 && m.d2 > 0 && m.m2 > 0, "rownorm: bad row map");
   RowMap rm{m.d1, m.m1, m.s1, m.d2, m.m2, m.s2, m.off};
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);

@@ -243,6 +243,26 @@ int catseg_conv3x3(const CatsegConvArgs* args, void* stream);
  * per-class conv over x as its `addend`.  g: NHWC [B][H][W][cin]; weight fp32 [cout][9][cin]. */
 int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, int cin, const float* weight, int cout,
                            float* out, int dtype, void* stream);
+/* catseg_upconv3x3 — ConvTranspose2d(k=2, s=2) followed by the 3x3 / pad-1 conv of
+ * DoubleConv, with the ConvTranspose output never materialised (Up.forward, model.py:546-555:
+ * up -> concat guidance -> conv).  Per output parity (a, b) the pair is a 2x2-tap conv over the
+ * ConvTranspose INPUT; args as catseg_conv3x3 with
+ *   src1 = the ConvTranspose input [S][H][W][c1] (optional GroupNorm+ReLU prologue as there),
+ *   weight = composite bf16 [4 * cout][3][3][c1], row block p = 2a + b holding parity (a, b)'s
+ *            taps (rows a..a+1, columns b..b+1; the other taps unused),
+ *   c_out = 4 * cout, addend = fp32 [S / addend_div][H*W][4 * cout] (catseg_upconv_addend: the
+ *            guidance half of the conv and the ConvTranspose bias through the in-image taps),
+ *   out = bf16 [S][2H][2W][cout], stats = GroupNorm partials of the 2H x 2W map:
+ *            [S][4 * H*W / catseg_upconv3x3_stats_tile()][cout / 16][2].
+ * Instantiated for c1 = 64, cout = 32, 48 <= W <= 50 (the second Up block of CAT-Seg). */
+int catseg_upconv3x3(const CatsegConvArgs* args, void* stream);
+int catseg_upconv3x3_stats_tile(void);
+/* catseg_upconv_addend — catseg_conv3x3_partial on the 2H x 2W guidance grid plus, per pixel,
+ * tap_bias[tap][co] (the ConvTranspose bias through conv tap `tap`, fp32 [9][cout], may be NULL)
+ * summed over the taps inside the image, written in catseg_upconv3x3's parity addend layout
+ * out[b][(y/2)*(W2/2) + x/2][((y%2)*2 + x%2)*cout + co].  bf16 g with 16 or 32 channels. */
+int catseg_upconv_addend(const void* g, int64_t B, int H2, int W2, int cin, const float* weight,
+                         const float* tap_bias, int cout, float* out, int dtype, void* stream);
 /* Rows per conv tile of the im2col / LDS-tile kernels (128). */
 int catseg_conv_tile_rows(void);
 /* Pixels per GroupNorm partial ("tile") of the kernel catseg_conv3x3 picks for `args`:

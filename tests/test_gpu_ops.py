@@ -850,3 +850,58 @@ def test_swin_window_attention_fused_vs_unfused(shift):
         o = torch.roll(o, shifts=(shift, shift), dims=(1, 2))
     e2 = (out.float().cpu().reshape(S, 24, 24, D) - o).abs()
     assert e2.max().item() < 5e-2 and e2.mean().item() < 5e-3, (e2.max().item(), e2.mean().item())
+
+
+@pytest.mark.parametrize("gn_src", [True, False])
+def test_upconv3x3_folded_convtranspose(gn_src):
+    """catseg_upconv3x3 + catseg_upconv_addend (the second Up block, model.py:546-555):
+    ConvTranspose2d(64 -> 48, k=2, s=2) of relu(GN(z)), concat the per-image guidance (16 ch,
+    repeated over T), conv3x3 (64 -> 32, no bias) == one 4-parity composite conv over z plus
+    the addend; vs the unfused composition in fp64 (bf16 operands), GroupNorm partials too."""
+    from cat_seg.engine import CatSegEngine
+    B, T, H, ci, m, cg, co = 2, 3, 48, 64, 48, 16, 32
+    S = B * T
+    z = rnd(S, ci, H, H, seed=81)
+    wt = rnd(ci, m, 2, 2, seed=82) / 8
+    bt = rnd(m, seed=83)
+    wc = rnd(co, m + cg, 3, 3, seed=84) / 16
+    g = rnd(B, cg, 2 * H, 2 * H, seed=85)
+    dt = torch.bfloat16
+    if gn_src:
+        mean = rnd(S * 4, seed=86) * 0.1
+        rstd = 1 + rnd(S * 4, seed=87).abs()
+        gam, bet = 1 + rnd(ci, seed=88) * 0.2, rnd(ci, seed=89) * 0.1
+        zb = z.to(dt).double().reshape(S, 4, 16, H, H)
+        zz = torch.relu(((zb - mean.double().reshape(S, 4, 1, 1, 1)) * rstd.double().reshape(S, 4, 1, 1, 1)
+                         ).reshape(S, ci, H, H) * gam.double().reshape(1, ci, 1, 1) + bet.double().reshape(1, ci, 1, 1))
+        # the kernel applies GN+ReLU in fp32 and rounds to bf16 before the MFMA
+        zz = zz.float().to(dt).double()
+    else:
+        zz = z.to(dt).double()
+    up = F.conv_transpose2d(zz, wt.double(), bt.double(), stride=2)
+    xin = torch.cat([up, g.to(dt).double().repeat_interleave(T, 0)], 1)
+    ref = F.conv2d(xin, wc.double(), padding=1)                              # (S, co, 2H, 2H)
+    comp, tap_b = CatSegEngine._upconv_weights(wt, bt, wc[:, :m])
+    wg = wc[:, m:].to(dt).float().permute(0, 2, 3, 1).reshape(co, -1).contiguous().to(dev)
+    part = torch.empty(B * H * H, 4 * co, device=dev)
+    ops.upconv_addend(g.permute(0, 2, 3, 1).contiguous().to(dev, dt), wg, tap_b.to(dev), part, B=B, H2=2 * H, W2=2 * H)
+    out = torch.empty(S * 4 * H * H, co, device=dev, dtype=dt)
+    tile = ops.upconv3x3_stats_tile()
+    ntl = 4 * H * H // tile
+    st = torch.empty(S * ntl * (co // 16) * 2, device=dev)
+    gn = None
+    if gn_src:
+        gn = (mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16)
+    ops.upconv3x3(z.permute(0, 2, 3, 1).contiguous().to(dev, dt), comp.to(dev, dt), out, S=S, H=H, W=H, c1=ci, gn=gn,
+                  stats=st, addend=part, addend_div=T)
+    got = out.reshape(S, 2 * H, 2 * H, co).permute(0, 3, 1, 2).double().cpu()
+    # bf16 composite weights vs the exact composition: a few bf16 roundings of an O(1) sum
+    err = (got - ref).abs()
+    assert err.max().item() <= 2e-2 + 2 ** -7 * ref.abs().max().item(), err.max().item()
+    assert err.mean().item() <= 2e-3, err.mean().item()
+    mean1 = torch.empty(S * (co // 16), device=dev)
+    rstd1 = torch.empty_like(mean1)
+    ops.groupnorm_stats(st, S, ntl, co // 16, tile * 16, mean1, rstd1)
+    gref = got.reshape(S, co // 16, -1)
+    close(mean1, gref.mean(-1).reshape(-1), atol=1e-4, what="gn mean")
+    close(rstd1, (1 / torch.sqrt(gref.var(-1, unbiased=False) + 1e-5)).reshape(-1), atol=0, rtol=2e-3, what="gn rstd")

@@ -15,12 +15,17 @@ variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").spli
 # variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (catseg_set_gemm_group)
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
-          "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True)}
+          "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True),
+          "sq4k": (4096, 4096, L.ACT_NONE, False)}
+# MG_SHAPES=qkv,fc1,sq4k selects shapes (sq4k: M = N = K = 4096, the guide's reference size)
+sel = os.environ.get("MG_SHAPES", "qkv,proj,fc1,fc2").split(",")
+shapes = {k: v for k, v in shapes.items() if k in sel}
 dev = "cuda"
 torch.manual_seed(0)
 lib = L.load()
 res = {}
 for name, (N, K, act, has_res) in shapes.items():
+    M = 4096 if name == "sq4k" else 8 * 577
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
     W = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
     bias = torch.rand(N, device=dev) - 0.5
