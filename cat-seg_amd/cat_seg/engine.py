@@ -59,7 +59,7 @@ class CatSegEngine:
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
         self.split_guidance = True      # bf16: decoder conv guidance half once per image (A/B switch)
-        self.fold_upconv = True         # bf16: second Up block's ConvTranspose folded into its conv (A/B switch)
+        self.fold_upconv = True         # bf16: the Up blocks' ConvTranspose folded into their first conv (A/B switch)
         self.device = torch.device(device)
         # config 5: the CLIP image encoder's block GEMMs (q/k/v, out-proj, c_fc, c_proj) in
         # OCP e4m3 with per-row scales (catseg_gemm_fp8); bf16 engine only
@@ -578,8 +578,11 @@ class CatSegEngine:
             Ho = Hc * 2
             cout = dec.c0.shape[0]
             groups = cout // 16
-            if (self.fold_upconv and self.split_guidance and dt == torch.bfloat16 and src_gn is not None
-                    and src.shape[1] == 64 and cout == 32 and 48 <= Hc <= 50 and (Hc * Hc) % 128 == 0):
+            fold = (self.fold_upconv and self.split_guidance and dt == torch.bfloat16 and (Hc * Hc) % 64 == 0 and
+                    GD[i].shape[1] in (16, 32) and
+                    ((src_gn is not None and src.shape[1] == 64 and cout == 32 and 48 <= Hc <= 50) or
+                     (src_gn is None and src.shape[1] == 128 and cout == 64 and Hc == 24)))
+            if fold:
                 # ConvTranspose + conv over [up | guidance] as one 4-parity conv over the
                 # GroupNorm+ReLU'd source (catseg_upconv3x3); guidance half + ConvT bias as addend
                 gpart = torch.empty(B * Hc * Hc, 4 * cout, device=dev, dtype=_f32)

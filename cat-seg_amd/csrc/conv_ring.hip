@@ -43,6 +43,7 @@ struct RingP {
   const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
   const float* add; int64_t add_ss; int64_t add_div;
   bf16* out; float* stats;
+  int up_split;   // UP: output channels of a parity split over this many workgroups (1 or 2)
 };
 
 template <int C>
@@ -82,8 +83,14 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int wpx = wave % WPX, wco = wave / WPX;
-  const int64_t s = blockIdx.x / p.bands;
+  // UP with up_split > 1: workgroup `half` computes channel block half of every parity
+  // (COW of the CO = COW * up_split channels per parity); the source ring is read per block
+  const int nsplit = UP ? p.up_split : 1;
+  const int64_t s = blockIdx.x / (p.bands * nsplit);
   const int band = blockIdx.x % p.bands;
+  const int half = UP ? (int)((blockIdx.x / p.bands) % nsplit) : 0;
+  const int CO = COW * nsplit;                          // UP: channels per parity in the output map
+  const int ch0 = wco * CO + half * COW;                // first weight row / addend channel of this wave
   const int HW = H * W;
   const int nchunks = HW / CH;
   const int c_begin = band * p.chunks_per_band;
@@ -101,7 +108,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   s16x8 wt[NTP > 0 ? NTP : 1][FN];
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
-    const int n = wco * COW + 16 * i + r16;
+    const int n = ch0 + 16 * i + r16;
 #pragma unroll
     for (int t = 0; t < NTAP; ++t) {
       const int tap = UP ? (pa + t / 2) * 3 + pb + t % 2 : t;
@@ -131,7 +138,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[wco * COW + 16 * i + 4 * q + r] : 0.f;
+    for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[ch0 + 16 * i + 4 * q + r] : 0.f;
   const bf16* s1base = p.s1 + s * p.s1_ss;
   const bf16* s2base = p.s2 ? p.s2 + (s / p.s2_div) * p.s2_ss : nullptr;
 
@@ -189,14 +196,17 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     const int p0 = c * CH;
     // the per-image addend of this chunk (L2-resident) first, so that waiting for it does
     // not also wait for the row prefetch issued after it (vmcnt retires in issue order)
+    // LATE_ADD (the 512-register UP variant): the addend is read in the epilogue instead, so its
+    // 4 x FN x FM registers are not live across the MFMAs
+    constexpr bool LATE_ADD = UP && C >= 128 && OCC > 1;
+    const float* addb = ADD ? p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT * nsplit + ch0 : nullptr;
     float4 ad[FN][FM];
-    if constexpr (ADD) {
-      const float* addb = p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT + wco * COW;
+    if constexpr (ADD && !LATE_ADD) {
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j)
-          ad[i][j] = *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT + 16 * i + 4 * q);
+          ad[i][j] = *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT * nsplit + 16 * i + 4 * q);
     }
     // ---- prefetch the rows the next chunk adds: unconditional loads from clamped addresses
     // (zero-selected at the ring write), so the code is straight-line and every wait is an
@@ -299,7 +309,11 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         float adv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (ADD) { adv[0] = ad[i][j].x; adv[1] = ad[i][j].y; adv[2] = ad[i][j].z; adv[3] = ad[i][j].w; }
+        if constexpr (ADD) {
+          const float4 av = LATE_ADD ? *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT * nsplit + 16 * i + 4 * q)
+                                     : ad[i][j];
+          adv[0] = av.x; adv[1] = av.y; adv[2] = av.z; adv[3] = av.w;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] += adv[r] + bv[i][r];
         if (p.act != ACT_NONE)
@@ -325,8 +339,8 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
           for (int r = 0; r < 4; ++r) { const float d = acc[i][j][r] - gm; m2 += d * d; }
         m2 = wave_sum(m2);
         if (lane == 0) {
-          const int grp = (wco * COW) / 16 + i;
-          float* o = p.stats + (((int64_t)s * ntiles + tile) * (COUT / 16) + grp) * 2;
+          const int grp = ch0 / 16 + i;
+          float* o = p.stats + (((int64_t)s * ntiles + tile) * (COUT * nsplit / 16) + grp) * 2;
           o[0] = gm;
           o[1] = m2;
         }
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int pp = p0 + 16 * j + r16, yy = pp / W, xx = pp - yy * W;
-        bf16* ob = p.out + ((int64_t)s * 4 * HW + (2 * yy + pa) * (2 * W) + 2 * xx + pb) * COW;
+        bf16* ob = p.out + ((int64_t)s * 4 * HW + (2 * yy + pa) * (2 * W) + 2 * xx + pb) * CO + half * COW;
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
           const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
@@ -393,7 +407,13 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>), dim3((unsigned)(p.S * bands)), dim3(NT), sh, st, p);
+  const int nsplit = UP ? p.up_split : 1;
+  if (nsplit < 1 || nsplit > 2 || (COUT / WCO) % 16 != 0) {
+    catseg_set_error("conv ring: bad channel split %d", nsplit);
+    return -1;
+  }
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>), dim3((unsigned)(p.S * bands * nsplit)),
+                     dim3(NT), sh, st, p);
   return 0;
 }
 
@@ -542,6 +562,7 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
   p.s1 = (const bf16*)a->src1; p.s1_ss = a->s1_slice_stride; p.c1 = a->c1;
   p.s2 = (const bf16*)a->src2; p.s2_ss = a->s2_slice_stride; p.c2 = a->c2; p.s2_div = a->src2_div > 0 ? a->src2_div : 1;
   p.S = a->S; p.H = a->H; p.W = a->W;
+  p.up_split = 1;
   p.w = (const bf16*)a->weight; p.bias = a->bias; p.act = a->act;
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
@@ -649,8 +670,11 @@ extern "C" int catseg_upconv3x3_stats_tile(void) { return 64; }
 extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a && a->src1 && a->weight && a->out, "upconv3x3: null pointer");
   CATSEG_CHECK(a->dtype == CATSEG_BF16 && a->c2 == 0 && !a->src2, "upconv3x3: bf16, one source");
-  CATSEG_CHECK(a->c1 == 64 && a->c_out == 128 && a->W >= 48 && a->W <= 50 && ((int64_t)a->H * a->W) % 128 == 0,
-               "upconv3x3: instantiated for 64 source channels -> 4 x 32 outputs on a 48..50-wide source grid");
+  const bool up2 = a->c1 == 64 && a->c_out == 128 && a->W >= 48 && a->W <= 50;
+  const bool up1 = a->c1 == 128 && a->c_out == 256 && a->W == 24;
+  CATSEG_CHECK((up1 || up2) && ((int64_t)a->H * a->W) % 64 == 0,
+               "upconv3x3: instantiated for 64 source channels -> 4 x 32 outputs on a 48..50-wide source grid "
+               "and 128 -> 4 x 64 on a 24-wide one (H*W % 64 == 0)");
   CATSEG_CHECK(a->s1_offset == 0 && a->s1_slice_stride % 8 == 0, "upconv3x3: src stride alignment");
   CATSEG_CHECK(!a->stats || a->stats_cpg == 16, "upconv3x3: GN stats in 16-channel groups");
   CATSEG_CHECK(!a->gn_mean || (a->gn_rstd && a->gn_gamma && a->gn_beta && a->gn_cpg > 0 && a->c1 % a->gn_cpg == 0),
@@ -665,10 +689,22 @@ extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
   p.out = (bf16*)a->out; p.stats = a->stats;
+  p.up_split = 1;
   hipStream_t st = (hipStream_t)stream;
   // 64-pixel chunks (a 48-wide chunk spans <= 3 rows: 5-row ring, <= 2 new rows = 104 positions):
   // 128-pixel chunks spilled ~100 VGPRs with the addend
-  if (p.add) launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true>(p, st);
-  else launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true>(p, st);
+  int rc;
+  if (up2) {
+    if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true>(p, st);
+    else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true>(p, st);
+  } else {
+    // first Up block (24-wide source, 128 channels): a parity's 64 outputs x 4 taps x 4 k-steps would
+    // be 256 weight VGPRs per wave, so two workgroups split them (32 each, the source ring read by
+    // both); a 64-pixel chunk spans <= 4 rows (6-row ring) and adds <= 3 (78 positions)
+    p.up_split = 2;
+    if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true>(p, st);
+    else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true>(p, st);
+  }
+  if (rc != 0) return rc;
   return catseg_launch_status("upconv3x3");
 }

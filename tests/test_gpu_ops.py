@@ -852,14 +852,16 @@ def test_swin_window_attention_fused_vs_unfused(shift):
     assert e2.max().item() < 5e-2 and e2.mean().item() < 5e-3, (e2.max().item(), e2.mean().item())
 
 
-@pytest.mark.parametrize("gn_src", [True, False])
-def test_upconv3x3_folded_convtranspose(gn_src):
-    """catseg_upconv3x3 + catseg_upconv_addend (the second Up block, model.py:546-555):
-    ConvTranspose2d(64 -> 48, k=2, s=2) of relu(GN(z)), concat the per-image guidance (16 ch,
-    repeated over T), conv3x3 (64 -> 32, no bias) == one 4-parity composite conv over z plus
-    the addend; vs the unfused composition in fp64 (bf16 operands), GroupNorm partials too."""
+@pytest.mark.parametrize("ci,m,cg,co,H,gn_src", [(64, 48, 16, 32, 48, True), (64, 48, 16, 32, 48, False),
+                                                   (128, 96, 32, 64, 24, False)])
+def test_upconv3x3_folded_convtranspose(ci, m, cg, co, H, gn_src):
+    """catseg_upconv3x3 + catseg_upconv_addend (Up blocks, model.py:546-555):
+    ConvTranspose2d(ci -> m, k=2, s=2) of z (relu(GN(z)) in the second block), concat the
+    per-image guidance (cg ch, repeated over T), conv3x3 (m + cg -> co, no bias) == one 4-parity
+    composite conv over z plus the addend; vs the unfused composition in fp64 (bf16 operands),
+    GroupNorm partials too.  Shapes of the second (48 -> 96) and first (24 -> 48) block."""
     from cat_seg.engine import CatSegEngine
-    B, T, H, ci, m, cg, co = 2, 3, 48, 64, 48, 16, 32
+    B, T = 2, 3
     S = B * T
     z = rnd(S, ci, H, H, seed=81)
     wt = rnd(ci, m, 2, 2, seed=82) / 8
@@ -868,11 +870,11 @@ def test_upconv3x3_folded_convtranspose(gn_src):
     g = rnd(B, cg, 2 * H, 2 * H, seed=85)
     dt = torch.bfloat16
     if gn_src:
-        mean = rnd(S * 4, seed=86) * 0.1
-        rstd = 1 + rnd(S * 4, seed=87).abs()
+        mean = rnd(S * (ci // 16), seed=86) * 0.1
+        rstd = 1 + rnd(S * (ci // 16), seed=87).abs()
         gam, bet = 1 + rnd(ci, seed=88) * 0.2, rnd(ci, seed=89) * 0.1
-        zb = z.to(dt).double().reshape(S, 4, 16, H, H)
-        zz = torch.relu(((zb - mean.double().reshape(S, 4, 1, 1, 1)) * rstd.double().reshape(S, 4, 1, 1, 1)
+        zb = z.to(dt).double().reshape(S, ci // 16, 16, H, H)
+        zz = torch.relu(((zb - mean.double().reshape(S, -1, 1, 1, 1)) * rstd.double().reshape(S, -1, 1, 1, 1)
                          ).reshape(S, ci, H, H) * gam.double().reshape(1, ci, 1, 1) + bet.double().reshape(1, ci, 1, 1))
         # the kernel applies GN+ReLU in fp32 and rounds to bf16 before the MFMA
         zz = zz.float().to(dt).double()
