@@ -580,7 +580,7 @@ class CatSegEngine:
             groups = cout // 16
             fold = (self.fold_upconv and self.split_guidance and dt == torch.bfloat16 and (Hc * Hc) % 64 == 0 and
                     GD[i].shape[1] in (16, 32) and
-                    ((src_gn is not None and src.shape[1] == 64 and cout == 32 and 48 <= Hc <= 50) or
+                    ((src_gn is not None and src.shape[1] == 64 and cout == 32 and Hc == 48) or
                      (src_gn is None and src.shape[1] == 128 and cout == 64 and Hc == 24)))
             if fold:
                 # ConvTranspose + conv over [up | guidance] as one 4-parity conv over the

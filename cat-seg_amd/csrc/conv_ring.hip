@@ -43,7 +43,7 @@ struct RingP {
   const float* gmean; const float* grstd; const float* ggamma; const float* gbeta; int gcpg;
   const float* add; int64_t add_ss; int64_t add_div;
   bf16* out; float* stats;
-  int up_split;   // UP: output channels of a parity split over this many workgroups (1 or 2)
+  int up_split;   // UP: output channels of a parity split over this many workgroups (1, 2 or 4)
 };
 
 template <int C>
@@ -62,7 +62,9 @@ struct RingGeom {
 // the source grid is the ConvTranspose INPUT, wave wco computes output parity
 // (a, b) = (wco >> 1, wco & 1) with its 2x2 of the 9 taps (rows a, a+1; columns b, b+1), and
 // channel block wco of COUT lands at pixel (2y + a, 2x + b) of the 2H x 2W output map.
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false>
+// WFIX > 0: the map width as a compile-time constant (UP variants; the per-pixel row / column
+// divisions become multiplies), 0 = p.W
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0>
 __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   constexpr int CPX = C / 8;
   constexpr int PS = RingGeom<C>::PS;
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   static_assert(WPX * WCO == 4 && FM >= 1 && FN >= 1, "wave grid");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* ring = reinterpret_cast<bf16*>(smem);
-  const int W = p.W, WP = W + 2, H = p.H;
+  const int W = WFIX > 0 ? WFIX : p.W, WP = W + 2, H = p.H;
   const int ring_elems = NR * WP * PS;
   float* gsc = reinterpret_cast<float*>(smem + (size_t)ring_elems * 2);   // [C]
   float* gsh = gsc + C;                                                    // [C]
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     // not also wait for the row prefetch issued after it (vmcnt retires in issue order)
     // LATE_ADD (the 512-register UP variant): the addend is read in the epilogue instead, so its
     // 4 x FN x FM registers are not live across the MFMAs
-    constexpr bool LATE_ADD = UP && C >= 128 && OCC > 1;
+    constexpr bool LATE_ADD = UP && ((C >= 128 && OCC > 1) || CH >= 128);
     const float* addb = ADD ? p.add + (s / p.add_div) * p.add_ss + (int64_t)(p0 + wpx * PXW) * COUT * nsplit + ch0 : nullptr;
     float4 ad[FN][FM];
     if constexpr (ADD && !LATE_ADD) {
@@ -387,7 +389,7 @@ size_t ring_lds(int W, int NR) { return (size_t)NR * (W + 2) * RingGeom<C>::PS *
 // NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
 // <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
 // adds <= 2 rows (104).
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false>
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0>
 int launch_ring_t(const RingP& p0, hipStream_t st) {
   RingP p = p0;
   const int nchunks = p.H * p.W / CH;
@@ -403,22 +405,28 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   const size_t sh = ring_lds<C>(p.W, NR);
   static size_t configured = 0;
   if (sh > configured) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
   const int nsplit = UP ? p.up_split : 1;
-  if (nsplit < 1 || nsplit > 2 || (COUT / WCO) % 16 != 0) {
-    catseg_set_error("conv ring: bad channel split %d", nsplit);
+  if (nsplit < 1 || nsplit > 4 || (COUT / WCO) % 16 != 0 || ((int64_t)p.H * p.W) % CH != 0 || (WFIX > 0 && p.W != WFIX)) {
+    catseg_set_error("conv ring: bad channel split %d or H*W %% %d != 0", nsplit, CH);
     return -1;
   }
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP>), dim3((unsigned)(p.S * bands * nsplit)),
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>), dim3((unsigned)(p.S * bands * nsplit)),
                      dim3(NT), sh, st, p);
   return 0;
 }
 
+// the CAT-Seg decoder widths (48, 96) get a compile-time width; others run with p.W
 template <int C, int COUT, int WPX, int WCO, int NPOS, int CH = 128, int OCC = 2, int NR = 6>
 int launch_ring(const RingP& p0, hipStream_t st) {
+  constexpr int WF = NPOS > 160 ? 96 : 48;      // the width class a variant is sized for
+  if (p0.W == WF) {
+    if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true, false, WF>(p0, st);
+    return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false, false, WF>(p0, st);
+  }
   if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true>(p0, st);
   return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false>(p0, st);
 }
@@ -670,10 +678,10 @@ extern "C" int catseg_upconv3x3_stats_tile(void) { return 64; }
 extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   CATSEG_CHECK(a && a->src1 && a->weight && a->out, "upconv3x3: null pointer");
   CATSEG_CHECK(a->dtype == CATSEG_BF16 && a->c2 == 0 && !a->src2, "upconv3x3: bf16, one source");
-  const bool up2 = a->c1 == 64 && a->c_out == 128 && a->W >= 48 && a->W <= 50;
+  const bool up2 = a->c1 == 64 && a->c_out == 128 && a->W == 48;
   const bool up1 = a->c1 == 128 && a->c_out == 256 && a->W == 24;
   CATSEG_CHECK((up1 || up2) && ((int64_t)a->H * a->W) % 64 == 0,
-               "upconv3x3: instantiated for 64 source channels -> 4 x 32 outputs on a 48..50-wide source grid "
+               "upconv3x3: instantiated for 64 source channels -> 4 x 32 outputs on a 48-wide source grid "
                "and 128 -> 4 x 64 on a 24-wide one (H*W % 64 == 0)");
   CATSEG_CHECK(a->s1_offset == 0 && a->s1_slice_stride % 8 == 0, "upconv3x3: src stride alignment");
   CATSEG_CHECK(!a->stats || a->stats_cpg == 16, "upconv3x3: GN stats in 16-channel groups");
@@ -693,17 +701,34 @@ extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // 64-pixel chunks (a 48-wide chunk spans <= 3 rows: 5-row ring, <= 2 new rows = 104 positions):
   // 128-pixel chunks spilled ~100 VGPRs with the addend
+  // tiling variants for A/B (catseg_set_ring_variant 11..14; 0 = default)
   int rc;
+  const int v = g_ring_variant;
   if (up2) {
-    if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true>(p, st);
-    else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true>(p, st);
+    if (v == 11) {       // 128-pixel chunks (<= 4 rows: 6-row ring, <= 3 new rows), one 512-register workgroup per CU
+      if (p.add) rc = launch_ring_t<64, 128, 1, 4, 156, 128, 1, 6, true, true, 48>(p, st);
+      else rc = launch_ring_t<64, 128, 1, 4, 156, 128, 1, 6, false, true, 48>(p, st);
+    } else {
+      if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true, 48>(p, st);
+      else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true, 48>(p, st);
+    }
   } else {
     // first Up block (24-wide source, 128 channels): a parity's 64 outputs x 4 taps x 4 k-steps would
     // be 256 weight VGPRs per wave, so two workgroups split them (32 each, the source ring read by
     // both); a 64-pixel chunk spans <= 4 rows (6-row ring) and adds <= 3 (78 positions)
-    p.up_split = 2;
-    if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true>(p, st);
-    else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true>(p, st);
+    if (v == 13) {       // 96-pixel chunks (4 whole rows at W = 24: 7-row ring, <= 4 new rows = 104 positions)
+      p.up_split = 2;
+      if (p.add) rc = launch_ring_t<128, 128, 1, 4, 104, 96, 1, 7, true, true, 24>(p, st);
+      else rc = launch_ring_t<128, 128, 1, 4, 104, 96, 1, 7, false, true, 24>(p, st);
+    } else if (v == 14) {  // four workgroups of 16 channels per parity, two workgroups per CU
+      p.up_split = 4;
+      if (p.add) rc = launch_ring_t<128, 64, 1, 4, 78, 64, 2, 6, true, true, 24>(p, st);
+      else rc = launch_ring_t<128, 64, 1, 4, 78, 64, 2, 6, false, true, 24>(p, st);
+    } else {
+      p.up_split = 2;
+      if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true, 24>(p, st);
+      else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true, 24>(p, st);
+    }
   }
   if (rc != 0) return rc;
   return catseg_launch_status("upconv3x3");

@@ -1,0 +1,50 @@
+"""Time catseg_upconv3x3 tiling variants (catseg_set_ring_variant) at the L/14@336 bs=8 T=150 decoder shapes
+(S = 1200 slices): Up1 = 24x24x128 -> 48x48x64, Up2 = relu(GN(48x48x64)) -> 96x96x32, addend included.
+usage: python tools/micro_upconv.py [variants, default 0]"""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
+import torch
+from cat_seg import ops
+from cat_seg import _lib as L
+
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0").split(",")]
+lib = L.load()
+dev, dt = "cuda", torch.bfloat16
+B, T = 8, 150
+S = B * T
+torch.manual_seed(0)
+for name, H, ci, co, gn in (("up1", 24, 128, 64, False), ("up2", 48, 64, 32, True)):
+    src = (torch.rand(S * H * H, ci, device=dev) - 0.5).to(dt)
+    w = ((torch.rand(4 * co, 9 * ci, device=dev) - 0.5) / 16).to(dt)
+    add = torch.rand(B * H * H, 4 * co, device=dev)
+    out = torch.empty(S * 4 * H * H, co, device=dev, dtype=dt)
+    tile = ops.upconv3x3_stats_tile()
+    st = torch.empty(S * (4 * H * H // tile) * (co // 16) * 2, device=dev)
+    g = None
+    if gn:
+        g = (torch.rand(S * ci // 16, device=dev) * 0.1, 1 + torch.rand(S * ci // 16, device=dev),
+             torch.rand(ci, device=dev), torch.rand(ci, device=dev) * 0.1, 16)
+    ref = None
+    res = {}
+    for v in variants:
+        lib.catseg_set_ring_variant(v)
+        ops.upconv3x3(src, w, out, S=S, H=H, W=H, c1=ci, gn=g, stats=st, addend=add, addend_div=T)
+        torch.cuda.synchronize()
+        o = out.float().clone()
+        if ref is None:
+            ref = o
+        res[v] = {"same": bool(torch.equal(o, ref)), "t": []}
+    for r in range(7):
+        for v in variants:
+            lib.catseg_set_ring_variant(v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                ops.upconv3x3(src, w, out, S=S, H=H, W=H, c1=ci, gn=g, stats=st, addend=add, addend_div=T)
+            e1.record(); torch.cuda.synchronize()
+            res[v]["t"].append(e0.elapsed_time(e1) / 5)
+    for v in variants:
+        t = sorted(res[v]["t"])[3]
+        print(f"{name} variant {v:2d}: {t * 1e3:7.1f} us  bit-identical to first: {res[v]['same']}", flush=True)
+lib.catseg_set_ring_variant(0)
