@@ -146,6 +146,9 @@ void catseg_set_conv_lds(int mode);
  * alternative wave splits of the 48- / 32-channel wide-map variants; 3 / 4 = half / double
  * band length. */
 void catseg_set_ring_variant(int variant);
+/* Swin window kernel: 0 = pipelined (head h+1's projection beside head h's attention, one
+ * barrier per head; default), 1 = two barriers per head (A/B reference). */
+void catseg_set_swin_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */
