@@ -905,8 +905,6 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     case 21: return launch3<TO, 160, 128, 2, 4, 3, 64>(g, st);
     case 22: return launch3<TO, 160, 128, 2, 4, 4, 64>(g, st);
     case 23: return launch3<TO, 224, 256, 2, 4, 4, 32>(g, st);
-    case 24: return launch3<TO, 160, 128, 2, 2, 2, 128>(g, st);    // 4 waves of 80 x 64, one workgroup per CU
-    case 25: return launch3<TO, 160, 128, 2, 2, 3, 64>(g, st);     // 4 waves of 80 x 64, 3-stage BK 64
     default: return false;
   }
 }
