@@ -59,6 +59,7 @@ class CatSegEngine:
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
         self.split_guidance = True      # bf16: decoder conv guidance half once per image (A/B switch)
+        self.fused_swin_mlp = True      # bf16: Swin output proj + residual + Mlp(norm2) in one kernel (A/B switch)
         self.fold_upconv = True         # bf16: the Up blocks' ConvTranspose folded into their first conv (A/B switch)
         self.device = torch.device(device)
         # config 5: the CLIP image encoder's block GEMMs (q/k/v, out-proj, c_fc, c_proj) in
@@ -534,9 +535,14 @@ class CatSegEngine:
                     ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, n_seq=S * nwin,
                                   seq_len=ws * ws, n_heads=a.nheads, head_dim=D // a.nheads,
                                   scale=(D // a.nheads) ** -0.5, mode=1, img_hw=(H_, W_), window=ws, shift=shift)
-                ops.rows_gemm(o, blk.wproj, X, bias=blk.bproj, res=X)          # x = shortcut + proj(attn)
-                ops.rows_mlp(X, blk.wfc1, blk.bfc1, blk.wfc2, X, ln=(blk.n2w, blk.n2b), b2=blk.bfc2,
-                             act=L.ACT_GELU, res=X)                              # x = x + Mlp(norm2(x))
+                if self.fused_swin_mlp and dt == torch.bfloat16 and D == 128 and blk.wfc1.shape[0] == 512:
+                    # x = shortcut + proj(attn); x = x + Mlp(norm2(x)) in one pass (x1 on chip)
+                    ops.swin_proj_mlp(o, X, blk.wproj, blk.bproj, blk.wfc1, blk.bfc1, blk.wfc2, blk.bfc2, X,
+                                      ln=(blk.n2w, blk.n2b))
+                else:
+                    ops.rows_gemm(o, blk.wproj, X, bias=blk.bproj, res=X)      # x = shortcut + proj(attn)
+                    ops.rows_mlp(X, blk.wfc1, blk.bfc1, blk.wfc2, X, ln=(blk.n2w, blk.n2b), b2=blk.bfc2,
+                                 act=L.ACT_GELU, res=X)                          # x = x + Mlp(norm2(x))
             ca = lay.ca
             if not pooled:
                 if fused_class:

@@ -563,6 +563,19 @@ def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=
     return out
 
 
+def swin_proj_mlp(attn, x, w_proj, b_proj, w1, b1, w2, b2, out, *, ln, eps=1e-5):
+    """out = x1 + GELU(LN(x1) . w1^T + b1) . w2^T + b2, x1 = x + attn . w_proj^T + b_proj (bf16 rows of
+    128; the Swin block after its window attention, catseg_swin_proj_mlp).  out may be x."""
+    M, C_ = x.shape
+    hidden = w1.shape[0]
+    flops = 2 * M * C_ * C_ + 4 * M * hidden * C_
+    with _rec("swin_proj_mlp", flops, x.element_size() * M * 3 * C_):
+        call("catseg_swin_proj_mlp", attn.data_ptr(), _ld(attn), x.data_ptr(), _ld(x), M, w_proj.data_ptr(),
+             b_proj.data_ptr(), ln[0].data_ptr(), ln[1].data_ptr(), eps, w1.data_ptr(), b1.data_ptr(), hidden,
+             w2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), _stream())
+    return out
+
+
 def semseg_confusion(probs, gt, conf, n_invalid, *, num_classes, ignore_label=255, clamp_pred=-1):
     """conf += bincount((N+1) * argmax(probs) + gt') on the device (catseg_semseg_confusion).
     probs (T, H, W) fp32, gt (H, W) int32, conf ((N+1)^2,) int64, n_invalid (1,) int64."""

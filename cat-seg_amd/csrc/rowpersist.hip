@@ -219,24 +219,44 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
 // SQ_LDS_BANK_CONFLICT: slot r16 + q collides once per group)
 constexpr int HID = 512, LDH = HID + 16;
 
-template <int ACT, bool RES2>
+// PROJ (catseg_swin_proj_mlp): the Swin block's output projection + residual runs first, per
+// tile: x1 = bf16(x + attn . Wp^T + bp) (model.py:112 proj, :222 shortcut), then the MLP above
+// on x1 (Y = the attention rows, res2 slot = the x rows); x1 never reaches HBM, and the
+// arithmetic (MFMA order, bias then residual, one bf16 rounding) is the separate
+// pgemm_kernel<128, false, true> + pmlp_kernel pair's, bit for bit.
+template <int ACT, bool RES2, bool PROJ = false>
 __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
                                                      const float* ln_g, const float* ln_b, float eps,
                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
-                                                     const bf16* __restrict__ W2, PEpi e) {
+                                                     const bf16* __restrict__ W2, PEpi e,
+                                                     const bf16* __restrict__ Xr = nullptr, int64_t ldxr = 0,
+                                                     const bf16* __restrict__ Wp = nullptr,
+                                                     const float* __restrict__ bp = nullptr) {
+  static_assert(!(PROJ && RES2), "PROJ carries the x rows in the res2 slot");
   constexpr int FM = BM / 16, SLD = KD + 4;
+  constexpr int NPAR = 2 * KD + HID + KD + (PROJ ? KD : 0);
   __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
   __shared__ __attribute__((aligned(16))) bf16 sH[BM * LDH];
   __shared__ __attribute__((aligned(16))) float st[BM * SLD];
-  // gamma / beta / b1 / b2 in LDS (see pgemm_kernel: no global loads behind the prefetch)
-  __shared__ __attribute__((aligned(16))) float sPar[2 * KD + HID + KD];
-  for (int i = threadIdx.x; i < 3 * KD + HID; i += NT)
-    sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD] : e.bias[i - 2 * KD - HID];
+  // gamma / beta / b1 / b2 (/ bp) in LDS (see pgemm_kernel: no global loads behind the prefetch)
+  __shared__ __attribute__((aligned(16))) float sPar[NPAR];
+  for (int i = threadIdx.x; i < NPAR; i += NT)
+    sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
+            : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
   __syncthreads();
   const float* sb1 = sPar + 2 * KD;
   const float* sb2 = sPar + 2 * KD + HID;
+  const float* sbp = sPar + 3 * KD + HID;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
+  s16x8 wpf[PROJ ? 4 : 1];           // PROJ: Wp rows 16*wave .. +15 (this wave's proj columns)
+  if constexpr (PROJ) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 u = ld16(Wp + (int64_t)(16 * wave + r16) * KD + ks * 32 + 8 * q);
+      wpf[ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  }
   s16x8 w1f[4][4], w2f[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -257,6 +277,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   auto fetch = [&](uint4& y, uint4& r2, int64_t t) {
     y = fetch_chunk(Y, ldy, t * BM, M);
     if constexpr (RES2) r2 = fetch_chunk(e.res2, e.ld_res2, t * BM, M);
+    if constexpr (PROJ) r2 = fetch_chunk(Xr, ldxr, t * BM, M);
   };
 #pragma unroll
   for (int d = 0; d < DEPTH_MLP; ++d)
@@ -267,8 +288,34 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     const int64_t tile = base + d * G;
     if (tile >= ntiles) break;
     const int64_t m0 = tile * BM;
-    const uint4 y_raw = ry[d], r2_cur = rr2[d];     // residuals of this tile stay in registers
-    put_chunk(ry[d], sPar, sPar + KD, eps, sX);
+    uint4 y_raw = ry[d];                            // residuals of this tile stay in registers
+    const uint4 r2_cur = rr2[d];
+    if constexpr (PROJ) {
+      put_chunk(ry[d], nullptr, nullptr, eps, sX);  // the attention rows, as they are
+      __syncthreads();
+      f32x4 ap[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) ap[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          ap[j] = mfma_bf16(wpf[ks], *reinterpret_cast<const s16x8*>(&sX[cslot<BM>(ks * 4 + q, 16 * j + r16)]), ap[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        *reinterpret_cast<f32x4*>(&st[(16 * j + r16) * SLD + 16 * wave + 4 * q]) = ap[j];
+      __syncthreads();
+      float v[8];
+      *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec]);
+      *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&st[er * SLD + ec + 4]);
+      const float4 p0 = *reinterpret_cast<const float4*>(sbp + ec), p1 = *reinterpret_cast<const float4*>(sbp + ec + 4);
+      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+      add8(v, r2_cur);
+      y_raw = pack8(v);                             // x1 = bf16(attn . Wp^T + bp + x)
+    }
+    put_chunk(y_raw, sPar, sPar + KD, eps, sX);
     __syncthreads();
     if (tile + DEPTH_MLP * G < ntiles) fetch(ry[d], rr2[d], tile + DEPTH_MLP * G);
 #pragma unroll
@@ -543,4 +590,23 @@ int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const flo
                        (const bf16*)w2, e);
   else return 1;
   return 0;
+}
+
+extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const void* x, int64_t ld_x, int64_t M,
+                                    const void* w_proj, const float* b_proj, const float* ln_gamma,
+                                    const float* ln_beta, float eps, const void* w1, const float* b1, int64_t hidden,
+                                    const void* w2, const float* b2, void* out, int64_t ld_out, void* stream) {
+  CATSEG_CHECK(attn && x && w_proj && b_proj && ln_gamma && ln_beta && w1 && b1 && w2 && b2 && out,
+               "swin_proj_mlp: null pointer");
+  CATSEG_CHECK(M > 0 && hidden == HID, "swin_proj_mlp: hidden must be 512");
+  CATSEG_CHECK(ld_attn % 8 == 0 && ld_x % 8 == 0 && ld_out % 8 == 0 && ((uintptr_t)attn % 16) == 0 &&
+                   ((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0,
+               "swin_proj_mlp: 16-byte aligned rows");
+  CATSEG_CHECK(out == x ? ld_out == ld_x : true, "swin_proj_mlp: in place needs ld_out == ld_x");
+  PEpi e{};
+  e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
+  hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
+                     (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
+  return catseg_launch_status("swin_proj_mlp");
 }

@@ -121,6 +121,16 @@ int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const float* ln_gam
                      const float* ln_beta, float eps, const void* w, int64_t N,
                      const CatsegRowsEpi* epi, int dtype, void* stream);
 
+/* catseg_swin_proj_mlp — the rest of a Swin block after its window attention, in one pass
+ * (model.py:112 proj, :222-223 shortcut + Mlp(norm2)):
+ *   x1 = bf16(x + attn . w_proj^T + b_proj),  out = x1 + GELU(LN(x1) . W1^T + b1) . W2^T + b2,
+ * x1 kept on chip.  bf16 rows of 128, hidden 512, exact-erf GELU; out may alias x (ld_out == ld_x).
+ * Same arithmetic as catseg_rows_gemm (proj + residual) followed by catseg_rows_mlp. */
+int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const void* x, int64_t ld_x, int64_t M,
+                         const void* w_proj, const float* b_proj, const float* ln_gamma, const float* ln_beta,
+                         float eps, const void* w1, const float* b1, int64_t hidden, const void* w2,
+                         const float* b2, void* out, int64_t ld_out, void* stream);
+
 /* catseg_rows_mlp — out = epi(act(LN(Y) . W1^T + b1) . W2^T): the whole token MLP with
  * the hidden activations kept on chip.  Y: [M][128], W1: [hidden][128], b1 fp32,
  * W2: [128][hidden], epi.bias = b2.  Replaces timm Mlp after norm2 (model.py:223, GELU)

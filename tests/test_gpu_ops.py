@@ -907,3 +907,28 @@ def test_upconv3x3_folded_convtranspose(ci, m, cg, co, H, gn_src):
     gref = got.reshape(S, co // 16, -1)
     close(mean1, gref.mean(-1).reshape(-1), atol=1e-4, what="gn mean")
     close(rstd1, (1 / torch.sqrt(gref.var(-1, unbiased=False) + 1e-5)).reshape(-1), atol=0, rtol=2e-3, what="gn rstd")
+
+
+def test_swin_proj_mlp_equals_separate_kernels():
+    """catseg_swin_proj_mlp (model.py:112 proj, :222-223 shortcut + Mlp(norm2)) is the separate
+    catseg_rows_gemm(proj + residual) -> catseg_rows_mlp pair, bit for bit, on ragged M; and both
+    match an fp64 restatement to bf16 rounding."""
+    M, C, Hd = 3 * 577 + 5, 128, 512
+    dt = torch.bfloat16
+    x = rnd(M, C, seed=91).to(dev, dt)
+    attn = rnd(M, C, seed=92).to(dev, dt)
+    wp, bp = (rnd(C, C, seed=93) / 11).to(dev, dt), rnd(C, seed=94).to(dev)
+    g, b = (1 + rnd(C, seed=95) * 0.2).to(dev), (rnd(C, seed=96) * 0.1).to(dev)
+    w1, b1 = (rnd(Hd, C, seed=97) / 11).to(dev, dt), rnd(Hd, seed=98).to(dev)
+    w2, b2 = (rnd(C, Hd, seed=99) / 22).to(dev, dt), rnd(C, seed=100).to(dev)
+    ref = x.clone()
+    ops.rows_gemm(attn, wp, ref, bias=bp, res=ref)
+    ops.rows_mlp(ref, w1, b1, w2, ref, ln=(g, b), b2=b2, act=L.ACT_GELU, res=ref)
+    got = x.clone()
+    ops.swin_proj_mlp(attn, got, wp, bp, w1, b1, w2, b2, got, ln=(g, b))
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got.float() - ref.float()).abs().max().item()
+    x1 = x.double().cpu() + attn.double().cpu() @ wp.double().cpu().T + bp.double().cpu()
+    h = F.gelu(F.layer_norm(x1, (C,), g.double().cpu(), b.double().cpu(), 1e-5) @ w1.double().cpu().T + b1.double().cpu())
+    y = x1 + h @ w2.double().cpu().T + b2.double().cpu()
+    close(got, y, atol=0.08, rtol=0.02, what="swin proj+mlp vs fp64")
