@@ -159,6 +159,8 @@ void catseg_set_ring_variant(int variant);
 /* Swin window kernel: 0 = pipelined (head h+1's projection beside head h's attention, one
  * barrier per head; default), 1 = two barriers per head (A/B reference). */
 void catseg_set_swin_variant(int variant);
+/* Head conv (bf16, 32 channels): 0 = MFMA tap image + shift-add (default), 1 = v_dot2c band. */
+void catseg_set_head_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */

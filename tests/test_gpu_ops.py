@@ -932,3 +932,38 @@ def test_swin_proj_mlp_equals_separate_kernels():
     h = F.gelu(F.layer_norm(x1, (C,), g.double().cpu(), b.double().cpu(), 1e-5) @ w1.double().cpu().T + b1.double().cpu())
     y = x1 + h @ w2.double().cpu().T + b2.double().cpu()
     close(got, y, atol=0.08, rtol=0.02, what="swin proj+mlp vs fp64")
+
+
+@pytest.mark.parametrize("H,W", [(96, 96), (50, 37)])
+def test_head_conv_mfma_tap_image(H, W):
+    """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the MFMA tap-image
+    kernel (catseg_set_head_variant 0) vs fp64 and vs the v_dot2c band kernel (variant 1), with
+    the top-k class scatter; ragged band (H % 8 != 0) included."""
+    B, T, C = 2, 3, 32
+    S = B * T
+    lib = L.load()
+    x = rnd(S, C, H, W, seed=111)
+    mean, rstd = rnd(S * 2, seed=112) * 0.2, 1 + rnd(S * 2, seed=113).abs()
+    gam, bet = 1 + rnd(C, seed=114) * 0.2, rnd(C, seed=115) * 0.2
+    hw_ = rnd(1, C, 3, 3, seed=116) / 8
+    xb = x.to(torch.bfloat16)
+    y1 = torch.relu(((xb.double().reshape(S, 2, 16, H, W) - mean.double().reshape(S, 2, 1, 1, 1))
+                     * rstd.double().reshape(S, 2, 1, 1, 1)).reshape(S, C, H, W) * gam.double().reshape(1, C, 1, 1)
+                    + bet.double().reshape(1, C, 1, 1))
+    rh = F.conv2d(y1, hw_.double(), torch.tensor([0.25]).double(), padding=1).reshape(B, T, H, W)
+    xin = xb.permute(0, 2, 3, 1).contiguous().to(dev)
+    cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
+    outs = []
+    for v in (0, 1):
+        lib.catseg_set_head_variant(v)
+        logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
+        ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
+                         bias=0.25, out=logits, T_out=T + 2, classes=cls,
+                         gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16))
+        outs.append(logits.cpu())
+    lib.catseg_set_head_variant(0)
+    for bi in range(B):
+        for t in range(T):
+            close(outs[0][bi, cls[bi, t]], rh[bi, t], atol=2e-3, what="head mfma vs fp64")
+    assert (outs[0] == -100.0).sum() == (outs[1] == -100.0).sum()        # untouched (unselected) classes
+    close(outs[0], outs[1], atol=2e-3, what="head mfma vs band")
