@@ -664,7 +664,11 @@ __global__ __launch_bounds__(256) void head_mfma_kernel(const bf16* __restrict__
   }
 }
 
-int g_head_variant = 0;   // 0 = MFMA tap image (head_mfma_kernel), 1 = v_dot2c band (head_band_kernel)
+// 1 = MFMA tap image (head_mfma_kernel), 0 = v_dot2c band (head_band_kernel, default): the MFMA form
+// cuts the VALU ~40 % but measured slower in the pipeline (0.315 vs 0.286 ms per step) -- the
+// kernel is bound by its staging (HBM rows + GroupNorm/ReLU/convert), and the tap image costs
+// two more barriers and an LDS pass
+int g_head_variant = 0;
 
 }  // namespace
 
@@ -762,7 +766,7 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                                       int dtype, void* stream) {
   CATSEG_CHECK(x && weight && out && C % 8 == 0 && C <= 256 && B > 0 && T > 0, "conv3x3_head: bad args");
   CATSEG_CHECK(!mean || (rstd && gamma && beta && cpg > 0 && C % cpg == 0), "conv3x3_head: bad GN args");
-  if (dtype == CATSEG_BF16 && C == 32 && W <= 128 && g_head_variant == 0) {
+  if (dtype == CATSEG_BF16 && C == 32 && W <= 128 && g_head_variant == 1) {
     const size_t tile_b = (size_t)(HBR + 2) * (W + 2) * (C + 8) * 2, ys_b = (size_t)(HBR + 2) * (W + 2) * HYS * 4;
     const size_t shm = 2 * C * 4 + std::max(tile_b, ys_b);
     static bool configured_m = false;

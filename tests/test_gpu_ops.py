@@ -937,8 +937,8 @@ def test_swin_proj_mlp_equals_separate_kernels():
 @pytest.mark.parametrize("H,W", [(96, 96), (50, 37)])
 def test_head_conv_mfma_tap_image(H, W):
     """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the MFMA tap-image
-    kernel (catseg_set_head_variant 0) vs fp64 and vs the v_dot2c band kernel (variant 1), with
-    the top-k class scatter; ragged band (H % 8 != 0) included."""
+    kernel (catseg_set_head_variant 1) vs fp64 and vs the v_dot2c band kernel (variant 0, the
+    default), with the top-k class scatter; ragged band (H % 8 != 0) included."""
     B, T, C = 2, 3, 32
     S = B * T
     lib = L.load()
@@ -954,7 +954,7 @@ def test_head_conv_mfma_tap_image(H, W):
     xin = xb.permute(0, 2, 3, 1).contiguous().to(dev)
     cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
     outs = []
-    for v in (0, 1):
+    for v in (1, 0):
         lib.catseg_set_head_variant(v)
         logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
         ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
@@ -964,6 +964,7 @@ def test_head_conv_mfma_tap_image(H, W):
     lib.catseg_set_head_variant(0)
     for bi in range(B):
         for t in range(T):
-            close(outs[0][bi, cls[bi, t]], rh[bi, t], atol=2e-3, what="head mfma vs fp64")
+            # fp16 staging of relu(GN(x)) (as the band kernel): ~5e-4 per product, 288 terms
+            close(outs[0][bi, cls[bi, t]], rh[bi, t], atol=6e-3, what="head mfma vs fp64")
     assert (outs[0] == -100.0).sum() == (outs[1] == -100.0).sum()        # untouched (unselected) classes
-    close(outs[0], outs[1], atol=2e-3, what="head mfma vs band")
+    close(outs[0], outs[1], atol=1e-4, what="head mfma vs band (same fp16 staging, fp32 sums)")
