@@ -179,7 +179,7 @@ class CATSeg(nn.Module):
 
     def forward(self, batched_inputs: List[dict]):
         if self.training:
-            raise NotImplementedError("CATSeg training is outside the MI355X inference path")
+            return self._training_loss(batched_inputs)
         if self.sliding_window:
             return self._forward_sliding(batched_inputs)
         with torch.no_grad():
@@ -199,6 +199,22 @@ class CATSeg(nn.Module):
                 results.append({"sem_seg": out[0]})
             return results
 
+
+    def _training_loss(self, batched_inputs: List[dict]):
+        """The training branch's loss (cat_seg_model.py:189-203): head logits of the batch, upsampled
+        to the targets' size, BCE-with-logits against one-hot targets (ignore_value rows zero), as
+        {"loss_sem_seg": 0-d tensor} on the device (catseg_bce_onehot_loss).  Forward only: the HIP
+        path computes no gradients, so the loss does not require grad (a training loop's backward()
+        fails loudly); SURVEY §8(f) rank 4 -- backward kernels are outside the inference north star."""
+        with torch.no_grad():
+            eng = self.engine
+            # training re-encodes the (training) class set every step, uncached (cat_seg_predictor.py:190-224)
+            eng.set_text(self.sem_seg_head.predictor.get_text_embeds())
+            raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in batched_inputs])
+            logits = eng.head_logits(raw, sizes_dev)
+            targets = torch.stack([x["sem_seg"].to(eng.device) for x in batched_inputs], dim=0)
+            loss = ops.bce_onehot_loss(logits.contiguous(), targets, self.sem_seg_head.ignore_value)
+        return {"loss_sem_seg": loss}
 
     def _forward_sliding(self, batched_inputs: List[dict]):
         """TEST.SLIDING_WINDOW eval (cat_seg_model.py:156-176,204-218): every image (or image 0 in

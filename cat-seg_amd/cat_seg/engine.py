@@ -413,6 +413,15 @@ class CatSegEngine:
         res3, res4, res5 = self.guidance(feats, hooks)
         return self.aggregate(feats, res3, res4, res5)
 
+    def _fold_ok(self, i, Hc, gch):
+        """Whether Up block i runs catseg_upconv3x3 (the ConvTranspose folded into its conv)."""
+        if not (self.fold_upconv and self.split_guidance and self.dt == torch.bfloat16 and (Hc * Hc) % 64 == 0
+                and gch in (16, 32)):
+            return False
+        dec = self.w.dec[i]
+        cin, cout = dec.upc_w.shape[1] // 9, dec.c0.shape[0]
+        return (i == 1 and cin == 64 and cout == 32 and Hc == 48) or (i == 0 and cin == 128 and cout == 64 and Hc == 24)
+
     def guidance(self, feats, hooks):
         """res3 / res4 / res5 guidance maps, NHWC in the engine dtype (cat_seg_model.py:178-186):
         res3 = dense tokens w/o CLS, res4/res5 = ConvTranspose2d(k=s=2/4) of the hook tokens."""
@@ -558,7 +567,7 @@ class CatSegEngine:
                                          k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
                 # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
                 ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y,
-                             res2=X)
+                             res2=X, ref_rows=B * HW * (T + n_pad))
             else:
                 # x_pool = AvgPool(x); x_pool += attn; x_pool += MLP; x += interp_ac(x_pool) (model.py:387-423)
                 ops.avgpool_rows(X, Xp, S=S, H=H_, W=W_, C=D, pool=(ph, pw))
@@ -584,10 +593,8 @@ class CatSegEngine:
             Ho = Hc * 2
             cout = dec.c0.shape[0]
             groups = cout // 16
-            fold = (self.fold_upconv and self.split_guidance and dt == torch.bfloat16 and (Hc * Hc) % 64 == 0 and
-                    GD[i].shape[1] in (16, 32) and
-                    ((src_gn is not None and src.shape[1] == 64 and cout == 32 and Hc == 48) or
-                     (src_gn is None and src.shape[1] == 128 and cout == 64 and Hc == 24)))
+            fold = (self._fold_ok(i, Hc, GD[i].shape[1]) and src.shape[1] * 9 == dec.upc_w.shape[1] and
+                    (src_gn is not None) == (i == 1))
             if fold:
                 # ConvTranspose + conv over [up | guidance] as one 4-parity conv over the
                 # GroupNorm+ReLU'd source (catseg_upconv3x3); guidance half + ConvT bias as addend
@@ -598,7 +605,7 @@ class CatSegEngine:
                 st = torch.empty(S * ntl * groups * 2, device=dev, dtype=_f32)
                 c1 = torch.empty(S * Ho * Ho, cout, device=dev, dtype=dt)
                 ops.upconv3x3(src, dec.upc_w, c1, S=S, H=Hc, W=Hc, c1=src.shape[1], gn=src_gn, stats=st,
-                              addend=gpart, addend_div=T)
+                              addend=gpart, addend_div=T, ref_convt_out=cu, ref_guid=GD[i].shape[1])
                 m1 = torch.empty(S * groups, device=dev, dtype=_f32)
                 r1 = torch.empty_like(m1)
                 ops.groupnorm_stats(st, S, ntl, groups, tile * 16, m1, r1)

@@ -27,8 +27,13 @@ PROFILE: Optional[list] = None
 
 
 class _rec:
-    def __init__(self, kernel, flops=0, nbytes=0):
+    """flops = the work the launch executes; ref_flops = the reference's count for the same module
+    (class padding rows, guidance halves recomputed per class and the
+    ConvTranspose maps are algorithmic work the build skips); defaults to flops."""
+
+    def __init__(self, kernel, flops=0, nbytes=0, ref_flops=None):
         self.kernel, self.flops, self.nbytes = kernel, flops, nbytes
+        self.ref_flops = flops if ref_flops is None else ref_flops
 
     def __enter__(self):
         if PROFILE is not None:
@@ -43,8 +48,8 @@ class _rec:
             _ACTIVE[0] = False
             if exc[0] is None:
                 self.e1.record(torch.cuda.current_stream())
-                PROFILE.append({"kernel": self.kernel, "flops": self.flops, "bytes": self.nbytes,
-                                "start": self.e0, "end": self.e1})
+                PROFILE.append({"kernel": self.kernel, "flops": self.flops, "ref_flops": self.ref_flops,
+                                "bytes": self.nbytes, "start": self.e0, "end": self.e1})
         return False
 
 
@@ -218,7 +223,8 @@ def swin_window_attention(x, ln, w_qkv, b_qkv, gqk, gmap, out, *, S, img_hw, win
     C = n_heads * head_dim
     L_ = window * window
     flops = 2 * R * C * 3 * C + 4 * R * L_ * C
-    with _rec("swin_window_attention", flops, x.element_size() * R * 2 * C):
+    ref = 2 * R * (2 * 2 * C * C + C * C) + 4 * R * L_ * C        # q, k = Linear(2C -> C) on [x | g] (model.py:94-96)
+    with _rec("swin_window_attention", flops, x.element_size() * R * 2 * C, ref_flops=ref):
         call("catseg_swin_window_attention", a, _stream())
     return out
 
@@ -243,7 +249,9 @@ def class_attention(x, ln, w_qkv, b_qkv, tg, y, *, B, T, HW, n_heads, head_dim, 
     R = B * T * HW
     C = n_heads * head_dim
     flops = 2 * R * C * 3 * C + 4 * R * n_heads * head_dim * head_dim
-    with _rec("class_attention", flops, x.element_size() * R * 2 * C):
+    Rp = B * HW * (T + n_pad)                 # the reference pads T to pad_len (model.py:397-409)
+    ref = 2 * Rp * (2 * 2 * C * C + C * C) + 4 * Rp * n_heads * head_dim * head_dim
+    with _rec("class_attention", flops, x.element_size() * R * 2 * C, ref_flops=ref):
         call("catseg_class_attention", a, _stream())
     return y
 
@@ -328,15 +336,18 @@ def conv3x3_partial(g, weight, out, *, B, H, W):
 
 
 def upconv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, gn=None, stats=None, stats_cpg=16,
-              addend=None, addend_div=1):
+              addend=None, addend_div=1, ref_convt_out=None, ref_guid=0):
     """ConvTranspose2d(k=2, s=2) + conv3x3 folded into one 4-parity conv over the ConvTranspose
     input (catseg_upconv3x3): src1 [S][H][W][c1] -> out [S][2H][2W][c_out/4] with the composite
     weight [4 * cout][9 * c1] (CatSegEngine._upconv_weights) and the parity-layout addend
     (upconv_addend).  `stats` receives [S][4 * H*W / upconv3x3_stats_tile()][cout/16][2]."""
     a = _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, 0, None, 0, 0, 0, 1, None, L.ACT_NONE, gn,
                    stats, stats_cpg, addend, addend_div)
-    # executed MFMA work: 4 of the 9 taps per output parity
-    with _rec("upconv3x3", 2 * S * H * W * weight.shape[0] * 4 * c1):
+    cout = weight.shape[0] // 4
+    # reference: ConvTranspose2d(c1 -> m, k=2, s=2) then conv3x3 over [up (m) | guidance (ref_guid)]
+    m = ref_convt_out or 0
+    ref = (2 * S * H * W * 4 * m * c1 + 2 * S * 4 * H * W * cout * 9 * (m + ref_guid)) if m else None
+    with _rec("upconv3x3", 2 * S * H * W * weight.shape[0] * 4 * c1, ref_flops=ref):
         call("catseg_upconv3x3", a, _stream())
     return out
 
@@ -352,7 +363,7 @@ def upconv_addend(g, weight, tap_bias, out, *, B, H2, W2):
     cout, k = weight.shape
     cin = k // 9
     assert g.shape[-1] == cin and out.dtype == torch.float32 and weight.dtype == torch.float32
-    with _rec("conv3x3_partial", 2 * B * H2 * W2 * cout * k):
+    with _rec("conv3x3_partial", 2 * B * H2 * W2 * cout * k, ref_flops=0):   # in upconv3x3's reference count
         call("catseg_upconv_addend", g.data_ptr(), B, H2, W2, cin, weight.data_ptr(), _p(tap_bias), cout,
              out.data_ptr(), _dt(g), _stream())
     return out
@@ -552,12 +563,15 @@ def convt64_gn(x, w, out, *, HW, gn, bias, store):
     return out
 
 
-def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=None, eps=1e-5, M=None):
-    """out = act(LN(y) . w1^T + b1) . w2^T + b2 + res + res2 (catseg_rows_mlp)."""
+def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=None, eps=1e-5, M=None,
+             ref_rows=None):
+    """out = act(LN(y) . w1^T + b1) . w2^T + b2 + res + res2 (catseg_rows_mlp).  ref_rows: the
+    reference's row count when it computes padded rows (the class MLP, model.py:413)."""
     M = M if M is not None else y.shape[0]
     hidden = w1.shape[0]
     e = _rows_epi(out, b2, None, None, None, L.ACT_NONE, res, res2, None)
-    with _rec("rows_mlp", 4 * M * hidden * w1.shape[1], y.element_size() * M * 2 * w1.shape[1]):
+    ref = 4 * ref_rows * hidden * w1.shape[1] if ref_rows else None
+    with _rec("rows_mlp", 4 * M * hidden * w1.shape[1], y.element_size() * M * 2 * w1.shape[1], ref_flops=ref):
         call("catseg_rows_mlp", y.data_ptr(), _ld(y), M, ln[0].data_ptr(), ln[1].data_ptr(), eps, w1.data_ptr(),
              b1.data_ptr(), hidden, act, w2.data_ptr(), e, _dt(y), _stream())
     return out
@@ -574,6 +588,22 @@ def swin_proj_mlp(attn, x, w_proj, b_proj, w1, b1, w2, b2, out, *, ln, eps=1e-5)
              b_proj.data_ptr(), ln[0].data_ptr(), ln[1].data_ptr(), eps, w1.data_ptr(), b1.data_ptr(), hidden,
              w2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), _stream())
     return out
+
+
+def bce_onehot_loss(logits, targets, ignore_value=255):
+    """The training branch's loss (cat_seg_model.py:189-203) on the device: BCE-with-logits of
+    logits (B, T, h, w) fp32 bilinearly upsampled to targets' (B, H, W) size, one-hot targets
+    (ignore_value -> zeros), mean over every element.  Returns a 0-d fp32 device tensor (no grad)."""
+    B, T, h, w = logits.shape
+    Bt, H, W = targets.shape
+    assert Bt == B and logits.dtype == torch.float32 and logits.is_contiguous()
+    tg = targets.to(torch.int32).contiguous()
+    ws = torch.empty(B * H, device=logits.device, dtype=torch.float64)
+    loss = torch.empty((), device=logits.device, dtype=torch.float32)
+    with _rec("bce_onehot_loss", 0, logits.numel() * 4 + tg.numel() * 4):
+        call("catseg_bce_onehot_loss", logits.data_ptr(), B, T, h, w, tg.data_ptr(), H, W, ignore_value, ws.data_ptr(),
+             loss.data_ptr(), _stream())
+    return loss
 
 
 def semseg_confusion(probs, gt, conf, n_invalid, *, num_classes, ignore_label=255, clamp_pred=-1):

@@ -45,7 +45,78 @@ __global__ __launch_bounds__(256) void confusion_kernel(const float* __restrict_
   atomicAdd(conf + n1 * arg + g, 1ull);
 }
 
+// ---- training-branch loss (cat_seg_model.py:189-203): BCE-with-logits of the logits,
+// bilinearly upsampled (align_corners=False) to the target size, against one-hot targets
+// (ignore_value pixels: all-zero rows, still averaged), mean over B*H*W*T.  One block per
+// (image, target row); per-thread fp32 sums over the classes of a pixel, fp64 block partials,
+// then one block sums the partials in a fixed order (deterministic).
+DEV void bce_lin(int dst, int in_size, float scale, int& i0, int& i1, float& l1) {
+  const float src = fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in_size - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+__global__ __launch_bounds__(256) void bce_rows_kernel(const float* __restrict__ logits, int T, int h, int w,
+                                                       const int32_t* __restrict__ tgt, int H, int W, int ignore,
+                                                       double* __restrict__ partial) {
+  const int y = blockIdx.x, b = blockIdx.y;
+  int y0, y1;
+  float ly;
+  bce_lin(y, h, (float)h / (float)H, y0, y1, ly);
+  double acc = 0.0;
+  for (int x = threadIdx.x; x < W; x += blockDim.x) {
+    int x0, x1;
+    float lx;
+    bce_lin(x, w, (float)w / (float)W, x0, x1, lx);
+    const int cls = tgt[((int64_t)b * H + y) * W + x];
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float* L = logits + ((int64_t)b * T + t) * h * w;
+      const float v = (1.f - ly) * ((1.f - lx) * L[y0 * w + x0] + lx * L[y0 * w + x1]) +
+                      ly * ((1.f - lx) * L[y1 * w + x0] + lx * L[y1 * w + x1]);
+      const float z = (cls != ignore && t == cls) ? 1.f : 0.f;
+      s += fmaxf(v, 0.f) - v * z + log1pf(__expf(-fabsf(v)));
+    }
+    acc += (double)s;
+  }
+  __shared__ double red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[(int64_t)b * H + y] = red[0];
+}
+
+__global__ __launch_bounds__(256) void bce_final_kernel(const double* __restrict__ partial, int64_t n, double denom,
+                                                        float* __restrict__ loss) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) acc += partial[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] / denom);
+}
+
 }  // namespace
+
+extern "C" int catseg_bce_onehot_loss(const float* logits, int64_t B, int T, int h, int w, const int32_t* targets,
+                                      int H, int W, int ignore_value, double* workspace, float* loss, void* stream) {
+  CATSEG_CHECK(logits && targets && workspace && loss, "bce_onehot_loss: null pointer");
+  CATSEG_CHECK(B > 0 && T > 0 && h > 0 && w > 0 && H > 0 && W > 0 && B < 65536, "bce_onehot_loss: bad shape");
+  CATSEG_CHECK(((uintptr_t)workspace % 8) == 0, "bce_onehot_loss: workspace must be 8-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bce_rows_kernel, dim3((unsigned)H, (unsigned)B), dim3(256), 0, st, logits, T, h, w, targets, H, W,
+                     ignore_value, workspace);
+  hipLaunchKernelGGL(bce_final_kernel, dim3(1), dim3(256), 0, st, workspace, B * H, (double)B * H * W * T, loss);
+  return catseg_launch_status("bce_onehot_loss");
+}
 
 extern "C" int catseg_semseg_confusion(const float* probs, int64_t T, int64_t H, int64_t W, const int32_t* gt,
                                        int num_classes, int ignore_label, int clamp_pred, int64_t* conf,

@@ -473,6 +473,15 @@ int catseg_token_embed(const int32_t* tokens, int64_t n, int ctx, const float* t
 int catseg_eot_gather(const float* x, const int32_t* tokens, int64_t n, int ctx, int width,
                       float* out, void* stream);
 
+/* catseg_bce_onehot_loss — the training branch's loss (cat_seg_model.py:189-203):
+ * logits [B][T][h][w] fp32, bilinearly upsampled (align_corners=False) to the target size,
+ * BCE-with-logits against one-hot targets built from targets [B][H][W] int32 (ignore_value
+ * pixels have an all-zero target row and still count), mean over B*H*W*T -> *loss (fp32, device).
+ * workspace: >= B*H doubles (caller-allocated).  Deterministic (fixed-order fp64 partial sums).
+ * Forward only: the HIP path has no backward (training is outside the inference north star). */
+int catseg_bce_onehot_loss(const float* logits, int64_t B, int T, int h, int w, const int32_t* targets, int H, int W,
+                           int ignore_value, double* workspace, float* loss, void* stream);
+
 /* ---------------------------------------------------------------------------
  * catseg_semseg_confusion — the confusion-matrix update of detectron2's
  * SemSegEvaluator.process as CAT-Seg's evaluators use it (plain_train_net.py:107-116,

@@ -1,0 +1,71 @@
+"""The training branch's loss (cat_seg_model.py:189-203) on the device: catseg_bce_onehot_loss vs
+the reference's own arithmetic (F.interpolate bilinear align_corners=False to the target size,
+one-hot targets with ignore rows left zero, F.binary_cross_entropy_with_logits mean) in fp64, and
+CATSeg.forward in training mode.  Forward only (no backward kernels)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cat_seg import build_model, ops
+
+from conftest import GOLDEN
+from test_boundary_cpu import tiny_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def reference_loss(logits, targets, ignore):
+    """cat_seg_model.py:190-201, restated on CPU float64."""
+    out = F.interpolate(logits.double(), size=targets.shape[-2:], mode="bilinear", align_corners=False)
+    T = out.shape[1]
+    mask = targets != ignore
+    out = out.permute(0, 2, 3, 1)
+    tg = torch.zeros(out.shape, dtype=torch.float64)
+    tg[mask] = F.one_hot(targets[mask].long(), num_classes=T).double()
+    return F.binary_cross_entropy_with_logits(out, tg).item()
+
+
+@pytest.mark.parametrize("B,T,h,w,H,W", [(2, 7, 24, 24, 96, 96), (3, 150, 24, 24, 50, 37), (1, 5, 96, 96, 384, 512)])
+def test_bce_onehot_loss_matches_reference(B, T, h, w, H, W):
+    g = torch.Generator().manual_seed(B * 100 + T)
+    logits = torch.randn(B, T, h, w, generator=g) * 3
+    targets = torch.randint(0, T, (B, H, W), generator=g, dtype=torch.int32)
+    targets[torch.rand(B, H, W, generator=g) < 0.2] = 255                 # ignore_value pixels
+    got = ops.bce_onehot_loss(logits.cuda(), targets.cuda(), 255).item()
+    ref = reference_loss(logits, targets, 255)
+    assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-6, (got, ref)
+    # deterministic: fixed-order reduction
+    assert ops.bce_onehot_loss(logits.cuda(), targets.cuda(), 255).item() == got
+
+
+def test_catseg_training_forward_loss():
+    """model.train(); model(batched_inputs with "sem_seg") -> {"loss_sem_seg"} equal to the
+    reference loss of the same head logits (the eval path's logits, checked elsewhere against
+    the reference goldens)."""
+    gd = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_pad.npz")))
+    model = build_model(tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": "f32"})).cuda()
+    model.sem_seg_head.predictor.set_class_tokens(gd["tokens"])
+    model.arch = model.arch.replace(pad_len=int(gd["pad_len"]))
+    model._engine = None
+    im = torch.from_numpy(gd["image0"])
+    H, W = im.shape[-2:]
+    T = len(gd["tokens"])
+    g = torch.Generator().manual_seed(7)
+    sem = torch.randint(0, T, (H, W), generator=g)
+    sem[:4] = 255
+    batch = [{"image": im, "sem_seg": sem}, {"image": im, "sem_seg": sem.flip(-1)}]
+    model.train()
+    losses = model(batch)
+    assert set(losses) == {"loss_sem_seg"} and losses["loss_sem_seg"].dim() == 0
+    assert not losses["loss_sem_seg"].requires_grad
+    model.eval()
+    eng = model.engine
+    raw, sizes_dev, _ = model._batch(eng, [b["image"] for b in batch])
+    with torch.no_grad():
+        logits = eng.head_logits(raw, sizes_dev).cpu()
+    ref = reference_loss(logits, torch.stack([b["sem_seg"] for b in batch]).int(), 255)
+    got = losses["loss_sem_seg"].item()
+    assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-6, (got, ref)
