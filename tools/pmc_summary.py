@@ -7,8 +7,10 @@ counter averaged per dispatch, plus derived ratios when their inputs are present
   wait%/inst%/active% = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES,
   valu/mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA, bank% = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE,
   fetchMB = 2 x FETCH_SIZE (gfx950 tallies 128-B streaming requests at 64 B), writeMB = WRITE_SIZE,
-  clk = GRBM_GUI_ACTIVE / 8 (sum over the XCDs) / duration, each counter averaged over the
-  dispatches of the passes that collected it (GRBM_GUI_ACTIVE is in every pass).
+  clk = GRBM_GUI_ACTIVE / 8 (sum over the XCDs) / duration, printed only for dispatches of
+  >= 0.3 ms (MI355X_MICROARCH.md "DVFS give-back": the quotient reads high below that, so no
+  clock is derived for shorter kernels).  Each counter is averaged over the dispatches of the
+  passes that collected it (GRBM_GUI_ACTIVE is in every pass).
 """
 import collections
 import csv
@@ -74,9 +76,9 @@ for tot, name, per, c in rows[:top]:
         d.append(f"write {c['WRITE_SIZE'] / 1024:8.1f} MB")
     if c.get("GRBM_GUI_ACTIVE"):
         # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall (MI355X_MICROARCH.md "DVFS give-back");
-        # it reads high on dispatches shorter than ~0.3 ms: marked "~" there
+        # it reads high on dispatches shorter than ~0.3 ms, so none is derived for those
         us = tot / per
-        d.append(f"clk {'~' if us < 300 else ''}{c['GRBM_GUI_ACTIVE'] / 8 / us / 1e3:4.2f} GHz")
+        d.append(f"clk {c['GRBM_GUI_ACTIVE'] / 8 / us / 1e3:4.2f} GHz" if us >= 300 else "clk n/a (<0.3 ms)")
     print(line)
     if d:
         print("      " + "  ".join(d))
