@@ -38,6 +38,7 @@ from cat_seg.engine import CatSegEngine  # noqa: E402
 from cat_seg.weights import synthesize_state_dict  # noqa: E402
 
 GF_PER_IMAGE = 875.7          # reference eval forward FLOPs, L/14@336, T=150
+GF_PER_IMAGE_CFG4 = 1128.0    # L/14@336, T=847 (top-256)
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_FP8_TFLOPS = 5000.0      # MI355X dense fp8 MFMA (block-scaled K=128 form)
@@ -55,8 +56,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--cpu-images", type=int, default=4, help="oracle sample size for cpu_baseline (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
-                    help="3 = the headline (L/14@336, T=150, bf16); 5 = sliding-window 640², pc459 classes, "
+    ap.add_argument("--config", type=int, default=3, choices=[3, 4, 5],
+                    help="3 = the headline (L/14@336, T=150, bf16); 4 = ade847 (top-256) at 4 images/GPU "
+                         "(SURVEY §8 config 4: bs=32 over 8 GPUs); 5 = sliding-window 640², pc459 classes, "
                          "fp8 ViT GEMMs (SURVEY §8 config 5)")
     ap.add_argument("--vit-fp8", action="store_true",
                     help="config 5's e4m3 CLIP image-encoder GEMMs (not the headline: the headline is bf16)")
@@ -108,6 +110,13 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     arch = VIT_L14_336
     cfg5 = args.config == 5
+    cfg4 = args.config == 4
+    if cfg4:      # the class-attention stress config: T = 847 -> top-256, 4 images per GPU
+        if args.classes == 150:
+            args.classes = 847
+        if args.batch == 8:
+            args.batch = 4
+    gf_per_image = GF_PER_IMAGE_CFG4 if cfg4 else GF_PER_IMAGE
     if cfg5:
         if world > 1:
             raise SystemExit("--config 5 is a single-GPU measurement (the scaling runs use the headline config)")
@@ -201,12 +210,14 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_images > 0:
         cpu = (cpu_baseline_sliding(arch, sd, text.cpu()) if cfg5 else
-               cpu_baseline(arch, sd, text.cpu(), args.cpu_images))
+               cpu_baseline(arch, sd, text.cpu(), min(args.cpu_images, 2) if cfg4 else args.cpu_images))
     if rank == 0:
-        path_tflops = GF_PER_IMAGE * value / 1e3
+        path_tflops = gf_per_image * value / 1e3
         line = {
             "metric": ("images/sec @ ViT-L/14 sliding-window 640² (5 crops/image), 459 classes, fp8 ViT GEMMs "
                        "(SURVEY §8 config 5; not the headline)" if cfg5 else
+                       "images/sec @ ViT-L/14 336², 847 classes (top-256), 4 images/GPU "
+                       "(SURVEY §8 config 4; not the headline)" if cfg4 else
                        "images/sec @ ViT-L/14 336², 150 classes, bs=8; 1/2/4/8-GPU scaling"),
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -214,7 +225,7 @@ def main():
             "gather_bit_identical": gather_ok,
             "dtype": args.dtype + ("+fp8e4m3 ViT GEMMs" if args.vit_fp8 else ""),
             "data": "synthetic (seeded rand*255 images, deterministic synthetic weights, "
-                    f"{'pc459' if cfg5 else 'ade150'} prompt tokens)",
+                    f"{'pc459' if cfg5 else 'ade847' if cfg4 else 'ade150'} prompt tokens)",
             "config": {"workload": (f"CATSeg eval forward, TEST.SLIDING_WINDOW: {B} images/GPU of 640², "
                                     f"{5 * B} crops through ViT-L/14@336, T={T} (top-256 per crop), "
                                     "Fold/avg merge to 640² probabilities" if cfg5 else
@@ -226,7 +237,7 @@ def main():
             "roofline": roofline,
             "path_roofline": None if cfg5 else {"bound": "mfma", "achieved": round(path_tflops, 2),
                               "peak": PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS,
-                              "unit": "TFLOP/s", "gf_per_image": GF_PER_IMAGE,
+                              "unit": "TFLOP/s", "gf_per_image": gf_per_image,
                               "frac": round(path_tflops / (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
                                                            else PEAK_F32_TFLOPS), 4)},
             "cpu_baseline": cpu,

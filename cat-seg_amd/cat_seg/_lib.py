@@ -150,7 +150,7 @@ _SIGS = {
     "catseg_conv3x3_head": [vp, i64, i32, i32, i32, i32, vp, f32, vp, i32, vp, i32, vp],
     "catseg_conv3x3_head_gn": [vp, i64, i32, i32, i32, i32, vp, f32, vp, vp, vp, vp, i32, vp, i32, vp, i32, vp],
     "catseg_corr_embed": [vp, i64, i64, vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, vp],
-    "catseg_topk_classes": [vp, i64, i64, i64, i32, i32, i32, vp, vp],
+    "catseg_topk_classes": [vp, i64, i64, i64, i32, i32, i32, vp, vp, vp],
     "catseg_gather_rows": [vp, i64, vp, i64, i64, vp, i64, i32, vp],
     "catseg_transpose_rows": [vp, i64, i64, i64, i64, i64, vp, i64, i32, vp],
     "catseg_convert": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, vp],

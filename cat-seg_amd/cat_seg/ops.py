@@ -403,7 +403,10 @@ def corr_embed(corr, *, t_stride, b_stride, B, T, H, W, weight, bias, out, class
 
 
 def topk_classes(corr, *, t_stride, b_stride, B, T, HW, k, out):
-    call("catseg_topk_classes", corr.data_ptr(), t_stride, b_stride, B, T, HW, k, out.data_ptr(), _stream())
+    """The k classes of largest max-over-pixels cost per image, sorted (catseg_topk_classes)."""
+    ws = torch.empty(B * T, device=corr.device, dtype=torch.float32)
+    call("catseg_topk_classes", corr.data_ptr(), t_stride, b_stride, B, T, HW, k, out.data_ptr(), ws.data_ptr(),
+         _stream())
     return out
 
 

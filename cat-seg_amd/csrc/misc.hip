@@ -267,42 +267,49 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
   }
 }
 
-// ---------------- top-k classes per image (bitonic sort of (max corr, idx)) ---------
-__global__ void topk_kernel(const float* corr, int64_t ts, int64_t bs, int Tn, int HW, int k, int32_t* classes) {
-  __shared__ float sv[2048];
-  __shared__ int si[2048];
+// ---------------- top-k classes per image --------------------------------------------
+// (1) class maxima: one wave per (image, class) row of HW contiguous costs, 4 waves per
+//     workgroup, the grid spread over every CU (a single workgroup per image is bound by one
+//     CU's load rate: ~80 us for 847 x 576 costs);  the maxima go to the caller's workspace.
+// (2) selection, one 1024-thread workgroup per image: class t's rank is the number of classes
+//     ordered before it by (max descending, index ascending) -- a broadcast LDS scan, every rank
+//     distinct -- and the classes of rank < k are written at their rank: the k largest, sorted.
+constexpr int TOPK_NT = 1024;
+__global__ __launch_bounds__(256) void class_max_kernel(const float* corr, int64_t ts, int64_t bs, int Tn, int HW,
+                                                        float* cmax) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = blockIdx.y;
+  if (t >= Tn) return;
+  const float* src = corr + (int64_t)t * ts + b * bs;
+  float m = -INFINITY;
+#pragma unroll 4
+  for (int p = lane; p < HW; p += 64) m = fmaxf(m, src[p]);
+  m = warp_max(m);
+  if (lane == 0) cmax[b * Tn + t] = m;
+}
+
+__global__ __launch_bounds__(TOPK_NT) void topk_select_kernel(const float* cmax, int Tn, int k, int32_t* classes) {
+  // 16-byte broadcast reads of the maxima (one ds_read_b128 per 4 classes: the scan is LDS-issue
+  // bound with 4-byte reads); entries past Tn are -inf and rank after every real class
+  __shared__ __attribute__((aligned(16))) float sv[2048];
   const int64_t b = blockIdx.x;
-  int n = 1;
-  while (n < Tn) n <<= 1;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) {
-    float m = -INFINITY;
-    if (t < Tn) {
-      const float* src = corr + (int64_t)t * ts + b * bs;
-      for (int p = 0; p < HW; ++p) m = fmaxf(m, src[p]);
-    }
-    sv[t] = m;
-    si[t] = t < Tn ? t : 0x7fffffff;
-  }
+  const int T4 = (Tn + 3) & ~3;
+  for (int t = threadIdx.x; t < T4; t += TOPK_NT) sv[t] = t < Tn ? cmax[b * Tn + t] : -INFINITY;
   __syncthreads();
-  // sort descending by value, ascending by index on ties
-  for (int size = 2; size <= n; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool desc = (i & size) == 0;
-          const float a = sv[i], c = sv[j];
-          const int ia = si[i], ic = si[j];
-          const bool a_first = (a > c) || (a == c && ia < ic);
-          if (desc != a_first) {
-            sv[i] = c; sv[j] = a; si[i] = ic; si[j] = ia;
-          }
-        }
-      }
-      __syncthreads();
+  for (int t = threadIdx.x; t < Tn; t += TOPK_NT) {
+    const float v = sv[t];
+    int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+    for (int u = 0; u < T4; u += 4) {
+      const float4 w = *reinterpret_cast<const float4*>(&sv[u]);
+      r0 += (w.x > v) | ((w.x == v) & (u < t));
+      r1 += (w.y > v) | ((w.y == v) & (u + 1 < t));
+      r2 += (w.z > v) | ((w.z == v) & (u + 2 < t));
+      r3 += (w.w > v) | ((w.w == v) & (u + 3 < t));
     }
+    const int rank = (r0 + r1) + (r2 + r3);
+    if (rank < k) classes[b * k + rank] = t;
   }
-  for (int i = threadIdx.x; i < k; i += blockDim.x) classes[b * k + i] = si[i];
 }
 
 template <typename E>
@@ -582,11 +589,14 @@ extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64
 }
 
 extern "C" int catseg_topk_classes(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride, int64_t B, int T,
-                                   int HW, int k, int32_t* classes, void* stream) {
-  CATSEG_CHECK(corr && classes && B > 0 && T > 0 && HW > 0, "topk: bad args");
+                                   int HW, int k, int32_t* classes, float* workspace, void* stream) {
+  CATSEG_CHECK(corr && classes && workspace && B > 0 && T > 0 && HW > 0, "topk: bad args");
   CATSEG_CHECK(T <= 2048 && k > 0 && k <= T, "topk: need 0 < k <= T <= 2048");
-  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
-                     corr_b_stride, T, HW, k, classes);
+  CATSEG_CHECK(B <= 65535, "topk: at most 65535 images per call");
+  hipLaunchKernelGGL(class_max_kernel, dim3((unsigned)((T + 3) / 4), (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                     corr, corr_t_stride, corr_b_stride, T, HW, workspace);
+  hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)B), dim3(TOPK_NT), 0, (hipStream_t)stream, workspace, T, k,
+                     classes);
   return catseg_launch_status("topk");
 }
 

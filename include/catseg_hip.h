@@ -324,10 +324,11 @@ int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_s
 void catseg_set_corr_mfma(int enable);
 
 /* catseg_topk_classes — per image, the top-k classes by max-over-pixels cosine
- * (model.py:694-696; ties broken by lower class index).  corr fp32 laid out as
- * corr[t*corr_t_stride + b*corr_b_stride + p]. */
+ * (model.py:694-696), written sorted by (max descending, class index ascending): the set
+ * torch.topk selects, ties to the lower class index.  corr fp32 laid out as
+ * corr[t*corr_t_stride + b*corr_b_stride + p]; workspace: B*T floats (the class maxima). */
 int catseg_topk_classes(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
-                        int64_t B, int T, int HW, int k, int32_t* classes, void* stream);
+                        int64_t B, int T, int HW, int k, int32_t* classes, float* workspace, void* stream);
 
 /* catseg_transpose_rows — out[b][c][r] = in[b*in_bstride + r][c] for r < rows, 0 for
  * rows <= r < ld_out (the transposed text-guidance k half of catseg_class_attention). */

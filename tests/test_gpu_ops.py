@@ -563,6 +563,24 @@ def test_corr_embed_topk(dt):
             lib.catseg_set_corr_mfma(1)
 
 
+@pytest.mark.parametrize("B,T,HW,k", [(4, 847, 576, 256), (3, 459, 576, 256), (2, 300, 37, 256), (1, 2048, 64, 1000)])
+def test_topk_classes_exact(B, T, HW, k):
+    """model.py:694-702: max over (P, H, W) of the cost per class, then the k largest.  The kernel
+    returns them sorted by (max descending, class index ascending) -- the set torch.topk selects,
+    in a fixed order (the class aggregation is permutation-equivariant and the final scatter is by
+    index).  Exact, including forced ties (one shared maximum for a run of classes)."""
+    corr = rnd(T, B * HW, seed=171)
+    c3 = corr.reshape(T, B, HW)
+    c3[10:20, :, 5] = 7.0                   # ten classes tie at the top in every image
+    c3[30:34, :, :] = -3.0                  # and four tie at a constant row
+    cls = torch.empty(B, k, device=dev, dtype=torch.int32)
+    ops.topk_classes(corr.to(dev), t_stride=B * HW, b_stride=HW, B=B, T=T, HW=HW, k=k, out=cls)
+    m = c3.max(-1)[0].T                     # (B, T)
+    for b in range(B):
+        order = sorted(range(T), key=lambda t: (-m[b, t].item(), t))[:k]
+        assert cls[b].cpu().tolist() == order
+
+
 def test_preprocess_im2col():
     arch_mean = torch.tensor([122.7709383, 116.7460125, 104.09373615])
     arch_std = torch.tensor([68.5005327, 66.6321579, 70.3231630])
