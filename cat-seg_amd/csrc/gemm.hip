@@ -854,26 +854,35 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (v < 0) return false;
   if (v == 0) {
     if (g->M < 1024 || g->K < 256) return false;
-    // Tile choice by wave quantization over the 256 CUs, measured on the ViT-L/14 shapes
-    // (M = 4616, tools/micro_gemm.py; hipBLASLt in brackets):
-    //  * a 224x256 tile when its tiles fill one round (QKV: 35.1 us vs 38.0 for 256x256 [32.3]);
-    //  * a 160x128 8-wave BK=128 tile when its tiles fit one round, one workgroup per CU
-    //    (fc2: 47.9 us vs 61.9 for 128x128 [42.2]; out-proj: 19.8 vs 24.7 [18.2]);
-    //  * otherwise 160x128 with 8 waves at two workgroups per CU (fc1: 54.2 us vs 71.3 [55.4]).
-    // Deeper rings (S = 3 / 4 at BK = 64, variants 21 / 22) measured slower on fc2 (53 us);
-    // a one-round 320x256 tile for fc1 (240 tiles) 58.4 us vs 54.5 (288x256: 102 us).
-    const int64_t t224 = ((g->M + 223) / 224) * (g->N / 256);
-    const int64_t t256 = ((g->M + 255) / 256) * (g->N / 256);
-    const int64_t t160 = ((g->M + 159) / 160) * (g->N / 128);
-    if (g->N % 256 == 0 && t224 >= 200 && t224 <= 256) v = 20;
-    else if (g->N % 256 == 0 && t256 >= 160 && t256 <= 256) v = 1;
-    else if (g->N % 128 == 0 && g->K % 128 == 0 && t160 >= 160 && t160 <= 256) v = 15;
-    else if (g->N % 128 == 0) v = 17;
-    else return false;
+    // Tile choice by wave quantization over the 256 CUs (tools/micro_gemm.py, MG_M for other M):
+    // score = fill x w / (1 + 0.15 (rounds - 1)), fill = tiles / (rounds x slots), slots = 256
+    // or 512 (two workgroups per CU), w = the tile's measured per-CU efficiency.  Picks, e.g.:
+    //  M = 4616 (bs 8): QKV 224x256 (35.1 us; hipBLASLt 32.3), fc1 160x128 two per CU (54.2 vs
+    //    71.3 for 256x256), out-proj / fc2 160x128 BK=128 (19.8 / 47.9 us);
+    //  M = 2308 (bs 4, config 4): QKV 128x128 8-wave two per CU (22.9 vs 24.2 us), fc1 160x128
+    //    two per CU (31.4 vs 47.6 for 256x256), out-proj / fc2 96x128 BK=128 (13.9 / 35.2 vs
+    //    18.8 / 50.9 us).
+    // (Earlier measurements: deeper rings S = 3 / 4 slower on fc2; a one-round 320x256 fc1 tile
+    // 58.4 us vs 54.5; 288x256 102 us.)  The tile never changes the arithmetic: every variant
+    // accumulates the full K of an output in the same k order.
+    struct Cand { int v, bm, bn, slots, bk; float w; };
+    static const Cand cands[] = {{20, 224, 256, 1, 64, 1.0f}, {1, 256, 256, 1, 64, 0.95f}, {15, 160, 128, 1, 128, 0.95f},
+                                 {17, 160, 128, 2, 64, 0.9f}, {19, 128, 128, 2, 64, 0.85f}, {24, 96, 128, 1, 128, 0.85f}};
+    float best = 0.f;
+    for (const Cand& c : cands) {
+      if (g->N % c.bn != 0 || g->K % c.bk != 0) continue;
+      const int64_t tiles = ((g->M + c.bm - 1) / c.bm) * (g->N / c.bn), slots = 256LL * c.slots;
+      const int64_t rounds = (tiles + slots - 1) / slots;
+      const float score = (float)tiles / (float)(rounds * slots) * c.w / (1.f + 0.15f * (float)(rounds - 1));
+      if (score > best) { best = score; v = c.v; }
+    }
+    if (v == 0) return false;
   }
-  if (g->store_mode != 0) {   // ConvTranspose scatter epilogue: instantiated for the two auto tiles only
-    if (v == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, true>(g, st);
-    if (v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, true>(g, st);
+  if (g->store_mode != 0) {   // ConvTranspose scatter epilogue: instantiated for the 160x128 tiles only
+    int sv = v;
+    if (g_gemm_variant == 0 && sv != 15 && sv != 17) sv = g->K % 128 == 0 ? 15 : 17;
+    if (sv == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, true>(g, st);
+    if (sv == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, true>(g, st);
     return false;
   }
   // lean epilogues for the automatic ViT tiles
@@ -885,6 +894,10 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 2 && v == 15) return launch3<TO, 160, 128, 2, 4, 2, 128, false, 2>(g, st);
   if (epi == 2 && v == 17) return launch3<TO, 160, 128, 2, 4, 2, 64, false, 2>(g, st);
   if (epi == 2 && v == 20) return launch3<TO, 224, 256, 2, 4, 2, 64, false, 2>(g, st);
+  if (epi == 1 && v == 19) return launch3<TO, 128, 128, 2, 4, 2, 64, false, 1>(g, st);
+  if (epi == 2 && v == 19) return launch3<TO, 128, 128, 2, 4, 2, 64, false, 2>(g, st);
+  if (epi == 1 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 1>(g, st);
+  if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
   switch (v) {
     case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
     case 2: return launch3<TO, 256, 256, 2, 4, 4, 32>(g, st);
@@ -905,6 +918,8 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     case 21: return launch3<TO, 160, 128, 2, 4, 3, 64>(g, st);
     case 22: return launch3<TO, 160, 128, 2, 4, 4, 64>(g, st);
     case 23: return launch3<TO, 224, 256, 2, 4, 4, 32>(g, st);
+    case 24: return launch3<TO, 96, 128, 2, 4, 2, 128>(g, st);
+    case 25: return launch3<TO, 96, 128, 2, 4, 2, 64>(g, st);
     default: return false;
   }
 }

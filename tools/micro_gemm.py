@@ -25,7 +25,7 @@ torch.manual_seed(0)
 lib = L.load()
 res = {}
 for name, (N, K, act, has_res) in shapes.items():
-    M = 4096 if name == "sq4k" else 8 * 577
+    M = 4096 if name == "sq4k" else int(os.environ.get("MG_M", 8 * 577))   # MG_M=2308: config 4's 4 images
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
     W = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
     bias = torch.rand(N, device=dev) - 0.5
