@@ -8,7 +8,7 @@ from cat_seg import ops
 from cat_seg import _lib as L
 
 variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,15,17,19,20,21,23,24").split(",")]
-M = 8 * 577
+M = int(os.environ.get("MG_M", 8 * 577))     # MG_M=23080: config 5's 40 crops
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True)}
 dev = "cuda"
