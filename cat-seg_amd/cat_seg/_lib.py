@@ -169,6 +169,7 @@ _SIGS = {
     "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
     "catseg_set_persistent": [i32],
+    "catseg_set_ln_variant": [i32],
     "catseg_set_conv_lds": [i32],
     "catseg_set_corr_mfma": [i32],
     "catseg_set_gemm_variant": [i32],

@@ -96,6 +96,62 @@ __global__ void rownorm_kernel(const TI* __restrict__ in, int64_t ld_in, RowMap 
   }
 }
 
+// ---------------- LayerNorm, fp32 rows -> bf16, NV float4 per lane (cols = 256 NV) --------
+// The ViT's ln_1 / ln_2 / ln_post (1024-wide fp32 residual stream -> bf16 GEMM operand):
+// persistent waves walk rows r, r + nw, ... with the next row's loads issued before the
+// current row is reduced and stored, so each wave keeps a load and a store stream in flight
+// (the one-row-per-wave form loads every row, then stores every row: 8.4 us per 4616 x 1024
+// launch against 28 MB / 6 TB/s = 4.7 us).  Same arithmetic as rownorm_kernel, bit for bit.
+template <int NV>
+__global__ __launch_bounds__(256) void ln_pipe_kernel(const float* __restrict__ in, int64_t ld_in, RowMap inmap,
+                                                      bf16* __restrict__ out, int64_t ld_out, const float* gamma,
+                                                      const float* beta, int64_t rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float4 gv[NV], bv[NV], cur[NV], nxt[NV];
+#pragma unroll
+  for (int it = 0; it < NV; ++it) {
+    const int c = (it * 64 + lane) * 4;
+    gv[it] = *reinterpret_cast<const float4*>(gamma + c);
+    bv[it] = *reinterpret_cast<const float4*>(beta + c);
+  }
+  auto load = [&](int64_t r, float4 (&v)[NV]) {
+    const float* x = in + rowmap(inmap, r) * ld_in;
+#pragma unroll
+    for (int it = 0; it < NV; ++it) v[it] = *reinterpret_cast<const float4*>(x + (it * 64 + lane) * 4);
+  };
+  if (row < rows) load(row, cur);
+  for (; row < rows; row += nw) {
+    if (row + nw < rows) load(row + nw, nxt);
+    float s = 0.f;
+#pragma unroll
+    for (int it = 0; it < NV; ++it) s += cur[it].x + cur[it].y + cur[it].z + cur[it].w;
+    const float mean = warp_sum(s) / (NV * 256);
+    float q = 0.f;
+    float v[NV][4];
+#pragma unroll
+    for (int it = 0; it < NV; ++it) {
+      v[it][0] = cur[it].x - mean; v[it][1] = cur[it].y - mean; v[it][2] = cur[it].z - mean; v[it][3] = cur[it].w - mean;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q += v[it][r] * v[it][r];
+    }
+    const float rstd = rsqrtf(warp_sum(q) / (NV * 256) + eps);
+#pragma unroll
+    for (int it = 0; it < NV; ++it) {
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = v[it][r] * rstd * (&gv[it].x)[r] + (&bv[it].x)[r];
+      store4<bf16>(out + row * ld_out + (it * 64 + lane) * 4, o);
+    }
+#pragma unroll
+    for (int it = 0; it < NV; ++it) cur[it] = nxt[it];
+  }
+}
+
+static int g_ln_variant = 0;   // 0 = pipelined persistent fp32 -> bf16 LayerNorm where it applies, 1 = one row per wave
+extern "C" void catseg_set_ln_variant(int v) { g_ln_variant = v; }
+
 template <bool LN>
 int rownorm(const void* in, int64_t ld_in, CatsegRowMap m, int dti, void* out, int64_t ld_out, int dto,
             const float* gamma, const float* beta, int64_t rows, int64_t cols, float eps, void* stream) {
@@ -108,6 +164,14 @@ int rownorm(const void* in, int64_t ld_in, CatsegRowMap m, int dti, void* out, i
   RowMap rm{m.d1, m.m1, m.s1, m.d2, m.m2, m.s2, m.off};
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t st = (hipStream_t)stream;
+  if (LN && g_ln_variant != 1 && dti == CATSEG_F32 && dto == CATSEG_BF16 && cols == 1024 && rows >= 2048) {
+    // 2 waves per SIMD over the 256 CUs: ~2-5 rows per wave at the ViT's 2308-4616 rows
+    const int64_t cap = g_ln_variant == 2 ? 256 : g_ln_variant == 3 ? 1024 : 512;
+    const unsigned pg = (unsigned)std::min<int64_t>((rows + 3) / 4, cap);
+    hipLaunchKernelGGL((ln_pipe_kernel<4>), dim3(pg), block, 0, st, (const float*)in, ld_in, rm, (bf16*)out, ld_out,
+                       gamma, beta, rows, eps);
+    return catseg_launch_status("layernorm");
+  }
 #define RN_LAUNCH(TI, TO)                                                                                   \
   hipLaunchKernelGGL((rownorm_kernel<TI, TO, LN>), grid, block, 0, st, (const TI*)in, ld_in, rm, (TO*)out, \
                      ld_out, gamma, beta, rows, (int)cols, eps)

@@ -173,6 +173,10 @@ int catseg_layernorm(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtyp
                      void* out, int64_t ld_out, int dtype_out,
                      const float* gamma, const float* beta, int64_t rows, int64_t cols,
                      float eps, void* stream);
+/* fp32 -> bf16 LayerNorm of >= 2048 rows of 1024 (the ViT's ln_1 / ln_2 / ln_post): 0 = persistent
+ * waves with the next row's loads in flight, 512 workgroups (default), 1 = one row per wave (A/B
+ * reference; bit-identical), 2 / 3 = the persistent form on 256 / 1024 workgroups.  Process-wide. */
+void catseg_set_ln_variant(int variant);
 
 /* catseg_l2normalize — x / max(||x||, eps) per row (F.normalize, model.py:649-650,
  * cat_seg_predictor.py:216, model.py:714). */

@@ -268,6 +268,28 @@ def test_layernorm_l2(cols, dt):
     close(out, F.normalize(x.double(), dim=-1), atol=1e-6 if dt == torch.float32 else 4e-3, what="l2")
 
 
+@pytest.mark.parametrize("rows", [4616, 2308, 2049])
+def test_layernorm_pipelined_rows(rows):
+    """The ViT's ln_1 / ln_2 / ln_post shape (fp32 rows of 1024 -> bf16): the persistent pipelined
+    kernel (catseg_set_ln_variant 0, default) equals the one-row-per-wave kernel bit for bit and
+    meets fp64 LayerNorm to bf16 rounding (model_vpt.py:156-162)."""
+    cols = 1024
+    x = rnd(rows, cols, seed=18) * 3 + 0.5
+    x[::97, :7] *= 40.0                     # CLIP-like outlier channels
+    g, b = rnd(cols, seed=19) + 1, rnd(cols, seed=20)
+    lib = L.load()
+    outs = []
+    for v in (0, 1):
+        lib.catseg_set_ln_variant(v)
+        o = torch.empty(rows, cols, device=dev, dtype=torch.bfloat16)
+        ops.layernorm(x.to(dev), g.to(dev), b.to(dev), o)
+        outs.append(o)
+    lib.catseg_set_ln_variant(0)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    close(outs[0], F.layer_norm(x.double(), (cols,), g.double(), b.double(), 1e-5), atol=3e-2, rtol=1e-2, what="LN pipe")
+
+
 # ----------------------------------------------------------------------------- attention
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("L_,H,causal", [(577, 4, False), (77, 2, True), (50, 3, False)])
