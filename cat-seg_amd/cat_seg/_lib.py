@@ -174,6 +174,7 @@ _SIGS = {
     "catseg_set_corr_mfma": [i32],
     "catseg_set_gemm_variant": [i32],
     "catseg_set_gemm_group": [i32],
+    "catseg_set_mlp_pair": [i32],
     "catseg_set_attn_variant": [i32],
     "catseg_set_ring_variant": [i32],
     "catseg_set_classattn_variant": [i32],

@@ -224,7 +224,12 @@ constexpr int HID = 512, LDH = HID + 16;
 // on x1 (Y = the attention rows, res2 slot = the x rows); x1 never reaches HBM, and the
 // arithmetic (MFMA order, bias then residual, one bf16 rounding) is the separate
 // pgemm_kernel<128, false, true> + pmlp_kernel pair's, bit for bit.
-template <int ACT, bool RES2, bool PROJ = false>
+// PAIR: fragments 2hf and 2hf+1 of wave w take the 32 hidden units 64w + 32hf + [0, 32) in
+// the order  row r of fragment i -> unit 8 (r / 4) + 4 i + r % 4,  so lane quad q ends GEMM1
+// holding units 8q .. 8q+7 of the pair: one 16-byte ds_write_b128 per row instead of two
+// 8-byte stores 16 units apart (whose 16 lanes sat 4-way on one bank pair at the 264-dword
+// row stride).  Every hidden unit is still one MFMA chain over the same k order: bit-identical.
+template <int ACT, bool RES2, bool PROJ = false, bool PAIR = true>
 __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
                                                      const float* ln_g, const float* ln_b, float eps,
                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
@@ -262,7 +267,9 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      uint4 u = ld16(W1 + (int64_t)(64 * wave + 16 * i + r16) * KD + ks * 32 + 8 * q);
+      const int unit = PAIR ? 64 * wave + 32 * (i >> 1) + 8 * (r16 >> 2) + 4 * (i & 1) + (r16 & 3)
+                            : 64 * wave + 16 * i + r16;
+      uint4 u = ld16(W1 + (int64_t)unit * KD + ks * 32 + 8 * q);
       w1f[i][ks] = *reinterpret_cast<s16x8*>(&u);
     }
 #pragma unroll
@@ -324,7 +331,8 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
       f32x4 acc1[2][FM];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float4 bv = *reinterpret_cast<const float4*>(sb1 + 64 * wave + 16 * (2 * hf + i) + 4 * q);
+        const int u0 = PAIR ? 64 * wave + 32 * hf + 8 * q + 4 * i : 64 * wave + 16 * (2 * hf + i) + 4 * q;
+        const float4 bv = *reinterpret_cast<const float4*>(sb1 + u0);
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc1[i][j] = f32x4{bv.x, bv.y, bv.z, bv.w};
       }
@@ -338,6 +346,21 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
           for (int j = 0; j < FM; ++j) acc1[i][j] = mfma_bf16(w1f[2 * hf + i][ks], xf[j], acc1[i][j]);
       }
+      if constexpr (PAIR) {
+        const int hh = 64 * wave + 32 * hf + 8 * q;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
+              else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
+            }
+          st16(&sH[(16 * j + r16) * LDH + hh], pack8(v));
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int hh = 64 * wave + 16 * (2 * hf + i) + 4 * q;
@@ -353,6 +376,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
           }
           store4<bf16>(&sH[(16 * j + r16) * LDH + hh], v);
         }
+      }
       }
     }
     __syncthreads();
@@ -568,28 +592,37 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
   return catseg_launch_status("convt64_gn");
 }
 
+int g_mlp_pair = 1;   // persistent MLP hidden-unit order: 1 = paired 16-byte hidden stores (default), 0 = 8-byte
+extern "C" void catseg_set_mlp_pair(int on) { g_mlp_pair = on; }
+
+template <bool PAIR>
+int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
+                        const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e, bool res2,
+                        hipStream_t st) {
+  const dim3 grid(persist_grid(M)), blk(NT);
+  if (act == ACT_GELU && !res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+  else if (act == ACT_RELU && res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, true, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+  else if (act == ACT_RELU && !res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, false, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+  else if (act == ACT_GELU && res2)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, true, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+  else return 1;
+  return 0;
+}
+
 int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
                                const void* w1, const float* b1, int64_t hidden, int act, const void* w2,
                                const CatsegRowsEpi* epi, hipStream_t st) {
   // residual must be the input rows themselves (both reference MLPs: model.py:223, :413)
   if (hidden != HID || !epi->bias || epi->res != y || epi->ld_res != ld_y || epi->add || epi->store_mode) return 1;
   const PEpi e = make_pepi(epi);
-  const dim3 grid(persist_grid(M)), blk(NT);
-  const bf16* Yb = (const bf16*)y;
-  if (act == ACT_GELU && !epi->res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
-                       (const bf16*)w2, e);
-  else if (act == ACT_RELU && epi->res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
-                       (const bf16*)w2, e);
-  else if (act == ACT_RELU && !epi->res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
-                       (const bf16*)w2, e);
-  else if (act == ACT_GELU && epi->res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, (const bf16*)w1, b1,
-                       (const bf16*)w2, e);
-  else return 1;
-  return 0;
+  const bool r2 = epi->res2 != nullptr;
+  return g_mlp_pair ? rows_mlp_persistent<true>((const bf16*)y, ld_y, M, g, b, eps, (const bf16*)w1, b1, act,
+                                                (const bf16*)w2, e, r2, st)
+                    : rows_mlp_persistent<false>((const bf16*)y, ld_y, M, g, b, eps, (const bf16*)w1, b1, act,
+                                                 (const bf16*)w2, e, r2, st);
 }
 
 extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const void* x, int64_t ld_x, int64_t M,
@@ -605,8 +638,13 @@ extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const voi
   CATSEG_CHECK(out == x ? ld_out == ld_x : true, "swin_proj_mlp: in place needs ld_out == ld_x");
   PEpi e{};
   e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
-  hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
-                     (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
-                     (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
+  if (g_mlp_pair)
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
+                       (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
+  else
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, false>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
+                       (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
   return catseg_launch_status("swin_proj_mlp");
 }

@@ -95,6 +95,9 @@ void catseg_set_gemm_variant(int variant);
 /* tile order of the pipelined bf16/fp8 GEMM: 0 = row-major, G > 0 = grouped (G m-tiles swept
  * across all n-tiles, so an XCD's contiguous tile range is a 2-D block of the output) */
 void catseg_set_gemm_group(int group_m);
+/* persistent MLP (Swin / class MLP): 1 (default) = paired hidden-unit order with 16-byte hidden-tile
+ * stores, 0 = the 8-byte-store order; bit-identical results (A/B only) */
+void catseg_set_mlp_pair(int on);
 
 /* ---------------------------------------------------------------------------
  * Row-block kernels over the 128-channel cost-embedding rows (K = 128).

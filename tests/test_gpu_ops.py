@@ -974,6 +974,37 @@ def test_swin_proj_mlp_equals_separate_kernels():
     close(got, y, atol=0.08, rtol=0.02, what="swin proj+mlp vs fp64")
 
 
+@pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
+def test_mlp_pair_order_bit_identical(act):
+    """The persistent MLP's paired hidden-unit order (catseg_set_mlp_pair 1, the default: 16-byte
+    hidden-tile stores) equals the 8-byte-store order (0) bit for bit, for the Swin MLP (GELU),
+    the class MLP (ReLU, + res2) and the fused Swin proj + MLP, on ragged M."""
+    lib = L.load()
+    M, C, Hd = 2 * 577 + 9, 128, 512
+    dt = torch.bfloat16
+    y = (rnd(M, C, seed=120) * 2).to(dev, dt)
+    x = rnd(M, C, seed=121).to(dev, dt)
+    g, b = (1 + rnd(C, seed=122) * 0.2).to(dev), (rnd(C, seed=123) * 0.1).to(dev)
+    w1, b1 = (rnd(Hd, C, seed=124) / 11).to(dev, dt), rnd(Hd, seed=125).to(dev)
+    w2, b2 = (rnd(C, Hd, seed=126) / 22).to(dev, dt), rnd(C, seed=127).to(dev)
+    wp, bp = (rnd(C, C, seed=128) / 11).to(dev, dt), rnd(C, seed=129).to(dev)
+    outs = {}
+    try:
+        for pair in (1, 0):
+            lib.catseg_set_mlp_pair(pair)
+            o1 = torch.empty_like(y)
+            ops.rows_mlp(y, w1, b1, w2, o1, ln=(g, b), b2=b2, act=act, res=y,
+                         res2=x if act == L.ACT_RELU else None)
+            o2 = x.clone()
+            ops.swin_proj_mlp(y, o2, wp, bp, w1, b1, w2, b2, o2, ln=(g, b))
+            torch.cuda.synchronize()
+            outs[pair] = (o1, o2)
+    finally:
+        lib.catseg_set_mlp_pair(1)
+    assert torch.equal(outs[1][0], outs[0][0]), (outs[1][0].float() - outs[0][0].float()).abs().max().item()
+    assert torch.equal(outs[1][1], outs[0][1]), (outs[1][1].float() - outs[0][1].float()).abs().max().item()
+
+
 @pytest.mark.parametrize("H,W", [(96, 96), (50, 37)])
 def test_head_conv_mfma_tap_image(H, W):
     """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the MFMA tap-image
