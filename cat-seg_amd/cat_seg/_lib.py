@@ -176,6 +176,7 @@ _SIGS = {
     "catseg_set_gemm_group": [i32],
     "catseg_set_mlp_pair": [i32],
     "catseg_set_attn_variant": [i32],
+    "catseg_set_attn_tail_skip": [i32],
     "catseg_set_ring_variant": [i32],
     "catseg_set_classattn_variant": [i32],
     "catseg_set_swin_variant": [i32],

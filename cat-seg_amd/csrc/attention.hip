@@ -26,6 +26,7 @@ struct AttnP {
   void* out; int64_t ldo;
   int64_t n_seq; int L; int H; float scale; int causal;
   int mode; int img_h, img_w, ws, shift;
+  int skip_tail;   // skip the MFMAs of key tiles wholly past L (catseg_set_attn_tail_skip A/B)
 };
 
 // GEO != 0: the window geometry is compile-time (GEO x GEO image, GEO/2 windows — CAT-Seg's
@@ -191,7 +192,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
-        if (kt < KTV) {
+        // a key tile wholly past L (the tail block: L = 577 leaves one key in the last 64-key
+        // block) is all -inf after the mask below: its MFMAs are skipped (block-uniform branch)
+        if (kt < KTV && (!tail || !p.skip_tail || k0 + kt * 16 < L)) {
           const int kr = kt * 16 + (lane & 15);
 #pragma unroll
           for (int ks = 0; ks < QF + QX; ++ks) {
@@ -241,6 +244,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
 #pragma unroll
         for (int u = 0; u < KB / 32; ++u) {
           if (2 * u >= KTV) continue;
+          if (tail && p.skip_tail && k0 + 32 * u >= L) continue;          // P = 0 on all 32 keys: O, l unchanged
           uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
                                 f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
           const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
@@ -303,6 +307,7 @@ void launch_win(const AttnP& p, hipStream_t st) {
   else launch<T, D, NW, KB, QT, GEO, false, false>(p, st);
 }
 
+int g_attn_tail_skip = 1;
 int g_attn_variant = 0;   // dense-path tiling (catseg_set_attn_variant; 0 = default)
 
 template <typename T, int D>
@@ -344,6 +349,7 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
 }  // namespace
 
 extern "C" void catseg_set_attn_variant(int v) { g_attn_variant = v; }
+extern "C" void catseg_set_attn_tail_skip(int on) { g_attn_tail_skip = on; }
 
 extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");
@@ -355,6 +361,7 @@ extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   AttnP p;
   p.q = a->q; p.k = a->k; p.v = a->v; p.ld = a->ld_qkv; p.out = a->out; p.ldo = a->ld_out;
   p.n_seq = a->n_seq; p.L = a->seq_len; p.H = a->n_heads; p.scale = a->scale; p.causal = a->causal;
+  p.skip_tail = g_attn_tail_skip;
   p.mode = a->mode; p.img_h = a->img_h; p.img_w = a->img_w; p.ws = a->window; p.shift = a->shift;
   if (a->mode == 1) {
     CATSEG_CHECK(a->window > 0 && a->img_h % a->window == 0 && a->img_w % a->window == 0,

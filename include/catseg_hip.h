@@ -211,6 +211,9 @@ int catseg_attention(const CatsegAttnArgs* args, void* stream);
 /* Tiling of the dense (mode 0, non-causal) bf16/fp32 path, for A/B tests (process-wide):
  * 0 = default; 1..5 = alternative waves / key-block / query-tile configurations. */
 void catseg_set_attn_variant(int variant);
+/* dense attention: 1 (default) skips the MFMAs of key tiles wholly past the sequence end (the
+ * last 64-key block of L = 577 holds one key); 0 computes and masks them.  Bit-identical (A/B only). */
+void catseg_set_attn_tail_skip(int on);
 
 /* catseg_linear_attention — class aggregation attention (LinearAttention,
  * model.py:256-286, inside AttentionLayer model.py:338-354 and the padding of
