@@ -455,8 +455,10 @@ __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 constexpr int HBR = 8;            // output rows per workgroup
 
-template <int C>
-__global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__ x, int Tn, int H, int W,
+// WC != 0: the map width is compile-time (96 at both CAT-Seg geometries), so the staging loop's
+// per-chunk (row, column) split and the output loop's are multiplies, not integer divisions.
+template <int C, int WC = 0>
+__global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__ x, int Tn, int H, int W_,
                                                         const float* __restrict__ w, float bias, const float* mean,
                                                         const float* rstd, const float* gamma, const float* beta,
                                                         int cpg, const int32_t* classes, int Tout, float* out) {
@@ -469,6 +471,7 @@ __global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__
   const int64_t s = blockIdx.y;
   const int y0 = blockIdx.x * HBR;
   const int rows = min(HBR, H - y0);
+  const int W = WC ? WC : W_;
   const int WP = W + 2;
   const int tid = threadIdx.x;
   for (int i = tid; i < 9 * C; i += 256) wl[i] = (_Float16)w[i];
@@ -668,7 +671,7 @@ __global__ __launch_bounds__(256) void head_mfma_kernel(const bf16* __restrict__
 // cuts the VALU ~40 % but measured slower in the pipeline (0.315 vs 0.286 ms per step) -- the
 // kernel is bound by its staging (HBM rows + GroupNorm/ReLU/convert), and the tap image costs
 // two more barriers and an LDS pass
-int g_head_variant = 0;
+int g_head_variant = 0;   // 2 = the band kernel with a runtime map width (A/B of the compile-time 96)
 
 }  // namespace
 
@@ -788,9 +791,21 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       configured = true;
     }
-    hipLaunchKernelGGL(head_band_kernel<32>, dim3((unsigned)((H + HBR - 1) / HBR), (unsigned)(B * T)), dim3(256), shb,
-                       (hipStream_t)stream, (const bf16*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg,
-                       classes, T_out, out);
+    if (W == 96 && g_head_variant != 2) {
+      static bool configured96 = false;
+      if (!configured96) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_band_kernel<32, 96>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        configured96 = true;
+      }
+      hipLaunchKernelGGL((head_band_kernel<32, 96>), dim3((unsigned)((H + HBR - 1) / HBR), (unsigned)(B * T)), dim3(256),
+                         shb, (hipStream_t)stream, (const bf16*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg,
+                         classes, T_out, out);
+    } else {
+      hipLaunchKernelGGL(head_band_kernel<32>, dim3((unsigned)((H + HBR - 1) / HBR), (unsigned)(B * T)), dim3(256), shb,
+                         (hipStream_t)stream, (const bf16*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg,
+                         classes, T_out, out);
+    }
     return catseg_launch_status("conv3x3_head");
   }
   const dim3 grid((unsigned)(((int64_t)H * W + 255) / 256), (unsigned)(B * T));

@@ -162,7 +162,8 @@ void catseg_set_ring_variant(int variant);
 /* Swin window kernel: 0 = pipelined (head h+1's projection beside head h's attention, one
  * barrier per head; default), 1 = two barriers per head (A/B reference). */
 void catseg_set_swin_variant(int variant);
-/* Head conv (bf16, 32 channels): 0 = v_dot2c band (default), 1 = MFMA tap image + shift-add. */
+/* Head conv (bf16, 32 channels): 0 = v_dot2c band (default; compile-time width at W = 96), 1 = MFMA tap
+ * image + shift-add, 2 = the band kernel with a runtime width (A/B). */
 void catseg_set_head_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;

@@ -1009,7 +1009,8 @@ def test_mlp_pair_order_bit_identical(act):
 def test_head_conv_mfma_tap_image(H, W):
     """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the MFMA tap-image
     kernel (catseg_set_head_variant 1) vs fp64 and vs the v_dot2c band kernel (variant 0, the
-    default), with the top-k class scatter; ragged band (H % 8 != 0) included."""
+    default; compile-time width at W = 96), with the top-k class scatter; ragged band (H % 8 != 0)
+    included; variant 2 (runtime width) equals variant 0 bit for bit."""
     B, T, C = 2, 3, 32
     S = B * T
     lib = L.load()
@@ -1025,7 +1026,7 @@ def test_head_conv_mfma_tap_image(H, W):
     xin = xb.permute(0, 2, 3, 1).contiguous().to(dev)
     cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
     outs = []
-    for v in (1, 0):
+    for v in (1, 0, 2):
         lib.catseg_set_head_variant(v)
         logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
         ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
@@ -1039,3 +1040,5 @@ def test_head_conv_mfma_tap_image(H, W):
             close(outs[0][bi, cls[bi, t]], rh[bi, t], atol=6e-3, what="head mfma vs fp64")
     assert (outs[0] == -100.0).sum() == (outs[1] == -100.0).sum()        # untouched (unselected) classes
     close(outs[0], outs[1], atol=1e-4, what="head mfma vs band (same fp16 staging, fp32 sums)")
+    # the band kernel with the compile-time width (W = 96) is the runtime-width one, bit for bit
+    assert torch.equal(outs[1], outs[2])
