@@ -576,6 +576,58 @@ __global__ __launch_bounds__(256) void post_band_kernel(const float* lg, int h, 
   }
 }
 
+// The same band with a compile-time output width WC (336 / 384: the CAT-Seg eval outputs):
+// thread t owns the 4-column group (t mod WC/4) for rows t / (WC/4), +G, ... of the band, so the
+// column taps (lin_idx of x, the LDS column offsets, lx) are derived once per thread instead of
+// once per store, and no integer division is left in the store loop.  Same taps, same fma order
+// as post_band_kernel: bit-identical.
+template <bool SIG, int WC>
+__global__ __launch_bounds__(256) void post_band_col_kernel(const float* lg, int h, int w, int ch, int cw, float* out,
+                                                            int H) {
+  constexpr int W4 = WC / 4, G = 256 / W4;
+  static_assert(WC % 4 == 0 && G >= 1, "output width");
+  extern __shared__ float sgm[];
+  const int64_t pl = blockIdx.y;
+  const int oy0 = blockIdx.x * POST_ROWS, oy1 = min(H, oy0 + POST_ROWS);
+  const float sy = (float)ch / (float)H, sx = (float)cw / (float)WC;
+  int ya, yb, yt;
+  float lt;
+  lin_idx(oy0, ch, sy, ya, yt, lt);
+  lin_idx(oy1 - 1, ch, sy, yt, yb, lt);
+  const int nrows = yb - ya + 1;
+  const float* src = lg + pl * (int64_t)h * w;
+  for (int i = threadIdx.x; i < nrows * cw; i += 256) {
+    const int r = i / cw, c = i - r * cw;
+    const float v = src[(int64_t)(ya + r) * w + c];
+    sgm[i] = SIG ? 1.f / (1.f + __expf(-v)) : v;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= G * W4) return;                 // no barrier below
+  const int x4 = (t % W4) * 4;
+  int x0[4], x1[4];
+  float lx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lin_idx(x4 + k, cw, sx, x0[k], x1[k], lx[k]);
+  float* o = out + pl * (int64_t)H * WC + x4;
+  for (int ry = t / W4; ry < oy1 - oy0; ry += G) {
+    const int y = oy0 + ry;
+    int y0, y1;
+    float ly;
+    lin_idx(y, ch, sy, y0, y1, ly);
+    const float* r0 = sgm + (y0 - ya) * cw;
+    const float* r1 = sgm + (y1 - ya) * cw;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float top = fmaf(lx[k], r0[x1[k]] - r0[x0[k]], r0[x0[k]]);
+      const float bot = fmaf(lx[k], r1[x1[k]] - r1[x0[k]], r1[x0[k]]);
+      v[k] = fmaf(ly, bot - top, top);
+    }
+    *reinterpret_cast<float4*>(o + (int64_t)y * WC) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // ---------------- text: token embedding + EOT gather ------------------------------
 __global__ void token_embed_kernel(const int32_t* tok, int64_t n, int ctx, const float* emb, const float* pos, int width,
                                    float* x) {
@@ -740,6 +792,7 @@ extern "C" int catseg_bicubic_resize(const float* in, int S_in, int D, float* ou
 }
 
 namespace {
+int g_post_variant = 0;   // 0 = compile-time-width band kernel at W = 336 / 384, 1 = runtime-width band kernel (A/B)
 template <bool SIG>
 int launch_post(const char* what, const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
                 float* out, int H, int W, void* stream) {
@@ -749,6 +802,18 @@ int launch_post(const char* what, const float* logits, int64_t B, int T, int h, 
   // banded kernel: source rows of one band (<= POST_ROWS * ch / H + 2) fit LDS
   const int64_t band_src_rows = (int64_t)POST_ROWS * crop_h / H + 3;
   if (W % 4 == 0 && band_src_rows * crop_w * 4 <= 64 * 1024) {
+    const dim3 grid((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T));
+    const size_t shb = (size_t)(band_src_rows * crop_w * 4);
+    if (g_post_variant == 0 && W == 336) {
+      hipLaunchKernelGGL((post_band_col_kernel<SIG, 336>), grid, dim3(256), shb, (hipStream_t)stream, logits, h, w,
+                         crop_h, crop_w, out, H);
+      return catseg_launch_status(what);
+    }
+    if (g_post_variant == 0 && W == 384) {
+      hipLaunchKernelGGL((post_band_col_kernel<SIG, 384>), grid, dim3(256), shb, (hipStream_t)stream, logits, h, w,
+                         crop_h, crop_w, out, H);
+      return catseg_launch_status(what);
+    }
     hipLaunchKernelGGL(post_band_kernel<SIG>, dim3((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T)),
                        dim3(256), (size_t)(band_src_rows * crop_w * 4), (hipStream_t)stream, logits, h, w, crop_h,
                        crop_w, out, H, W);
@@ -759,6 +824,8 @@ int launch_post(const char* what, const float* logits, int64_t B, int T, int h, 
   return catseg_launch_status(what);
 }
 }  // namespace
+
+extern "C" void catseg_set_post_variant(int v) { g_post_variant = v; }
 
 extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
                                   float* out, int H, int W, void* stream) {

@@ -165,6 +165,9 @@ void catseg_set_swin_variant(int variant);
 /* Head conv (bf16, 32 channels): 0 = v_dot2c band (default; compile-time width at W = 96), 1 = MFMA tap
  * image + shift-add, 2 = the band kernel with a runtime width (A/B). */
 void catseg_set_head_variant(int variant);
+/* Postprocess / resize band kernel: 0 (default) = compile-time output width at W = 336 / 384 (column
+ * taps hoisted per thread), 1 = runtime width.  Bit-identical (A/B only). */
+void catseg_set_post_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */

@@ -640,6 +640,32 @@ def test_bicubic_postprocess():
     close(o, ref, atol=2e-6, what="postprocess")
 
 
+@pytest.mark.parametrize("HW,crop", [(336, None), (384, None), (336, (90, 77))])
+def test_postprocess_compile_time_width(HW, crop):
+    """The band kernel with a compile-time output width (catseg_set_post_variant 0, W = 336 / 384, the
+    CAT-Seg eval outputs) vs torch (sigmoid -> bilinear, align_corners=False, sem_seg_postprocess crop)
+    and bit for bit vs the runtime-width band kernel (variant 1)."""
+    lib = L.load()
+    lg = (rnd(2, 5, 96, 96, seed=36) * 4).to(dev)
+    outs = []
+    try:
+        for v in (0, 1):
+            lib.catseg_set_post_variant(v)
+            o = torch.empty(2, 5, HW, HW, device=dev)
+            if crop is None:
+                ops.postprocess(lg, o)
+            else:
+                ops.postprocess(lg, o, crop=crop)
+            torch.cuda.synchronize()
+            outs.append(o)
+    finally:
+        lib.catseg_set_post_variant(0)
+    src = lg.cpu() if crop is None else lg.cpu()[:, :, :crop[0], :crop[1]]
+    ref = F.interpolate(src.sigmoid(), size=(HW, HW), mode="bilinear", align_corners=False)
+    close(outs[0], ref, atol=2e-6, what="postprocess W=%d" % HW)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.fixture(params=["persistent", "tiled"])
 def rows_variant(request):
     L.load().catseg_set_persistent(1 if request.param == "persistent" else 0)
