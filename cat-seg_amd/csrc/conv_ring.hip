@@ -476,12 +476,20 @@ template <int CIN, bool PAR = false>
 __global__ __launch_bounds__(256) void conv_partial_vec_kernel(const bf16* __restrict__ g, int64_t B, int H, int W,
                                                               const float* __restrict__ w, int cout, float* out,
                                                               const float* __restrict__ tap_bias = nullptr) {
-  extern __shared__ float sw[];        // [9][CIN][cout] (+ PAR: [9][cout] tap bias)
+  extern __shared__ float sw[];        // [9][CIN][cout + 4] (+ PAR: [9][cout] tap bias)
+  // Transposing staging: 32 lanes = 8 consecutive ci (32 contiguous global bytes) x 4 co, so a
+  // wave-load touches 8 cache lines (indexing in LDS order made each lane touch its own line),
+  // and the LDS row stride cout + 4 puts those 32 lanes on 32 distinct banks (4 ci + co mod 32)
+  const int ldw = cout + 4;
+  static_assert(CIN % 8 == 0, "CIN");
   for (int i = threadIdx.x; i < 9 * CIN * cout; i += blockDim.x) {
-    const int co = i % cout, ci = (i / cout) % CIN, tap = i / (cout * CIN);
-    sw[i] = w[((int64_t)co * 9 + tap) * CIN + ci];
+    const int lo = i & 31, rest = i >> 5;
+    const int ci_lo = lo & 7, co_lo = lo >> 3;
+    const int cib = rest % (CIN / 8), rest2 = rest / (CIN / 8);
+    const int tap = rest2 % 9, co = (rest2 / 9) * 4 + co_lo, ci = cib * 8 + ci_lo;
+    sw[(tap * CIN + ci) * ldw + co] = w[((int64_t)co * 9 + tap) * CIN + ci];
   }
-  float* stb = sw + 9 * CIN * cout;
+  float* stb = sw + 9 * CIN * ldw;
   if constexpr (PAR)
     for (int i = threadIdx.x; i < 9 * cout; i += blockDim.x) stb[i] = tap_bias ? tap_bias[i] : 0.f;
   __syncthreads();
@@ -503,11 +511,11 @@ __global__ __launch_bounds__(256) void conv_partial_vec_kernel(const bf16* __res
 #pragma unroll
       for (int v = 0; v < CIN / 8; ++v) u[v] = ld16(src + 8 * v);
       const bf16* e = reinterpret_cast<const bf16*>(u);
-      const float* wt = sw + tap * CIN * cout + cg * 4;
+      const float* wt = sw + tap * CIN * ldw + cg * 4;
 #pragma unroll
       for (int ci = 0; ci < CIN; ++ci) {
         const float v = bf2f(e[ci]);
-        const float4 ww = *reinterpret_cast<const float4*>(wt + ci * cout);
+        const float4 ww = *reinterpret_cast<const float4*>(wt + ci * ldw);
         a0 += v * ww.x; a1 += v * ww.y; a2 += v * ww.z; a3 += v * ww.w;
       }
     }
@@ -608,8 +616,8 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
   const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
   const bool vec = dtype == CATSEG_BF16 && ((uintptr_t)g % 16) == 0 && (cin == 16 || cin == 32);
   if (vec) {
-    // grid-stride over the pixels with ~2 workgroups per CU: the [9][cin][cout] weight image
-    // (up to 73 KB, a strided gather) is staged once per workgroup, not once per 256 pixels
+    // grid-stride over the pixels with ~2 workgroups per CU: the [9][cin][cout + 4] weight image
+    // (up to 78 KB) is staged once per workgroup, not once per 256 pixels
     const unsigned vgrid = (unsigned)std::min<int64_t>((total + 255) / 256, 512);
     static bool vconfigured = false;
     if (!vconfigured) {
@@ -619,12 +627,14 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
       vconfigured = true;
     }
+    const size_t shv = (size_t)9 * cin * (cout + 4) * 4;   // padded LDS rows (conv_partial_vec_kernel)
+    CATSEG_CHECK(shv <= 128 * 1024, "conv3x3_partial: weights <= 128 KB");
     if (cin == 16)
-      hipLaunchKernelGGL(conv_partial_vec_kernel<16>, dim3(vgrid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B,
-                         H, W, weight, cout, out);
+      hipLaunchKernelGGL(conv_partial_vec_kernel<16>, dim3(vgrid), dim3(256), shv, (hipStream_t)stream, (const bf16*)g,
+                         B, H, W, weight, cout, out);
     else
-      hipLaunchKernelGGL(conv_partial_vec_kernel<32>, dim3(vgrid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B,
-                         H, W, weight, cout, out);
+      hipLaunchKernelGGL(conv_partial_vec_kernel<32>, dim3(vgrid), dim3(256), shv, (hipStream_t)stream, (const bf16*)g,
+                         B, H, W, weight, cout, out);
   } else if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(conv_partial_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, (const bf16*)g, B, H,
                        W, cin, weight, cout, out);
@@ -648,10 +658,10 @@ extern "C" int catseg_upconv_addend(const void* g, int64_t B, int H2, int W2, in
   CATSEG_CHECK(g && weight && out && B > 0 && H2 > 0 && W2 > 0 && H2 % 2 == 0 && W2 % 2 == 0, "upconv_addend: bad args");
   CATSEG_CHECK(dtype == CATSEG_BF16 && (cin == 16 || cin == 32) && ((uintptr_t)g % 16) == 0,
                "upconv_addend: bf16 guidance with 16 or 32 channels, 16B aligned");
-  CATSEG_CHECK(cout % 4 == 0 && (size_t)(9 * cin * cout + 9 * cout) * 4 <= 128 * 1024 && ((uintptr_t)out % 16) == 0 &&
+  CATSEG_CHECK(cout % 4 == 0 && (size_t)(9 * cin * (cout + 4) + 9 * cout) * 4 <= 128 * 1024 && ((uintptr_t)out % 16) == 0 &&
                    (!tap_bias || ((uintptr_t)tap_bias % 16) == 0),
                "upconv_addend: cout % 4, weights <= 128 KB, 16B aligned out / tap_bias");
-  const size_t sh = (size_t)(9 * cin * cout + 9 * cout) * 4;
+  const size_t sh = (size_t)(9 * cin * (cout + 4) + 9 * cout) * 4;   // padded weight rows + tap bias
   static bool configured = false;
   if (!configured) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_vec_kernel<16, true>),
