@@ -226,7 +226,7 @@ __global__ void corr_embed_kernel(const float* corr, int64_t ts, int64_t bs, con
 // rounding.  One 4-wave workgroup per slice: the zero-padded slice sits in LDS, every wave
 // keeps all 128 x 64 weights as MFMA A fragments in registers and walks 16-pixel tiles:
 // D[c][pix] with 4 consecutive channels per lane (8-byte stores).
-int g_corr_mfma = 1;   // A/B switch (catseg_set_corr_mfma)
+int g_corr_mfma = 1;   // A/B switch (catseg_set_corr_mfma): 1 = MFMA, weights staged in LDS; 2 = MFMA, weights gathered from global; 0 = VALU
 
 DEV void split_bf16(float v, bf16& hi, bf16& lo) {
   hi = f2bf(v);
@@ -235,15 +235,25 @@ DEV void split_bf16(float v, bf16& hi, bf16& lo) {
 
 __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr, int64_t ts, int64_t bs,
                                                               const int32_t* classes, int64_t S, int Tn, int H,
-                                                              int W, const float* w, const float* bias, bf16* out) {
+                                                              int W, const float* w, const float* bias, bf16* out,
+                                                              int stage_w) {
   constexpr int HID = 128;
   __shared__ float sin[1024];          // (H + 6) x (W + 6) zero-padded slice (host-checked)
   __shared__ float sbias[HID];
+  __shared__ float sw[HID * 49];       // stage_w: the [128][49] weights, one coalesced sweep
   const int PW = W + 6, PH = H + 6;
   const int HW = H * W;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
-  // persistent over slices: the hi/lo weight fragments are built once per workgroup
+  // persistent over slices: the hi/lo weight fragments are built once per workgroup, from LDS
+  // (stage_w: 25 KB read coalesced; a fragment's 8 k values of one row are 8 scattered scalar
+  // loads otherwise, 128 per thread)
+  const float* wsrc = w;
+  if (stage_w) {
+    for (int i = threadIdx.x; i < HID * 49; i += 256) sw[i] = w[i];
+    __syncthreads();
+    wsrc = sw;
+  }
   s16x8 whi[8][2], wlo[8][2];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -253,7 +263,7 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 32 * ks + 8 * q + j;
-        split_bf16(k < 49 ? w[(16 * i + r16) * 49 + k] : 0.f, h[j], l[j]);
+        split_bf16(k < 49 ? wsrc[(16 * i + r16) * 49 + k] : 0.f, h[j], l[j]);
       }
       whi[i][ks] = *reinterpret_cast<const s16x8*>(h);
       wlo[i][ks] = *reinterpret_cast<const s16x8*>(l);
@@ -693,7 +703,7 @@ extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64
     }
     const unsigned pgrid = (unsigned)std::min<int64_t>(B * T, (int64_t)cus * 2);
     hipLaunchKernelGGL(corr_embed_mfma_kernel, dim3(pgrid), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
-                       corr_b_stride, classes, B * (int64_t)T, T, H, W, weight, bias, (bf16*)out);
+                       corr_b_stride, classes, B * (int64_t)T, T, H, W, weight, bias, (bf16*)out, g_corr_mfma != 2 ? 1 : 0);
   }
   else if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(corr_embed_kernel<bf16>, dim3(grid), dim3(256), sh, (hipStream_t)stream, corr, corr_t_stride,

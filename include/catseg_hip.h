@@ -334,7 +334,8 @@ int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_s
                       const float* weight, const float* bias, int hidden,
                       void* out, int dtype, void* stream);
 /* bf16, hidden = 128: the 7x7 conv runs as an MFMA GEMM over the 49 taps with hi/lo bf16
- * operand splits (default 1; 0 = the VALU kernel, for A/B tests).  Process-wide. */
+ * operand splits (default 1: weights staged in LDS by one coalesced sweep; 2 = the same kernel
+ * gathering its weight fragments from global memory; 0 = the VALU kernel; A/B tests).  Process-wide. */
 void catseg_set_corr_mfma(int enable);
 
 /* catseg_topk_classes — per image, the top-k classes by max-over-pixels cosine
