@@ -182,6 +182,7 @@ _SIGS = {
     "catseg_set_swin_variant": [i32],
     "catseg_set_head_variant": [i32],
     "catseg_set_post_variant": [i32],
+    "catseg_set_merge_variant": [i32],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
     "catseg_abi_version": [],
     "catseg_last_error": [],

@@ -254,6 +254,99 @@ __global__ __launch_bounds__(256) void sliding_merge_band_kernel(const float* __
   }
 }
 
+// The banded merge with the tile planes' source rows staged in LDS (nb <= 2: every X is covered
+// by at most two tile columns, every band by at most two tile rows): the <= (BY-1) h/k + 3 source
+// rows of each covering tile plane that the band's output rows interpolate from are copied once per
+// workgroup (coalesced), so each tile term blends 4 LDS values with 32-bit offsets instead of 4
+// gathers through L1 with 64-bit plane addressing.  Same taps, same blend / sigmoid / Fold order as
+// sliding_merge_band_kernel: bit-identical.
+__global__ __launch_bounds__(256) void sliding_merge_stage_kernel(const float* __restrict__ lg, int T, int h, int w,
+                                                                  int k, int stride, int nb, int out_res, int bands,
+                                                                  int grows, int trows, float* __restrict__ out) {
+  extern __shared__ float smem_m[];
+  float* gsig = smem_m;                        // [grows][k]: sigmoid of the global k-res map rows
+  float* tsl = smem_m + grows * k;             // [2 tile rows][2 tile cols][trows][w]
+  const int L = nb * nb + 1;
+  const int64_t nt = blockIdx.x / bands;
+  const int band = blockIdx.x % bands;
+  const int t = (int)(nt % T);
+  const int64_t n = nt / T;
+  const int Y0 = band * MERGE_BY, Y1 = min(Y0 + MERGE_BY, out_res);
+  const float sg = (float)k / (float)out_res, st_ = (float)h / (float)k;
+  int r_lo, r_hi, tmp;
+  float tl;
+  lin_src(Y0, k, sg, r_lo, tmp, tl);
+  lin_src(Y1 - 1, k, sg, tmp, r_hi, tl);
+  const int nr = r_hi - r_lo + 1;
+  const int64_t plane = (int64_t)h * w;
+  const float* gp = lg + ((n * L + L - 1) * T + t) * plane;
+  for (int idx = threadIdx.x; idx < nr * k; idx += blockDim.x) {
+    const int r = r_lo + idx / k, x = idx % k;
+    gsig[idx] = up_sig_fast(gp, h, w, k, r, x);
+  }
+  // tile rows bi covering the band: source rows [tlo[bi], thi[bi]] of planes (bi, 0..nb-1)
+  int tlo[2] = {0, 0};
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    if (bi >= nb) break;
+    const int ya = max(Y0, stride * bi), yb = min(Y1, stride * bi + k) - 1;
+    if (ya > yb) continue;
+    int a0, a1, b0, b1;
+    float la;
+    lin_src(ya - stride * bi, h, st_, a0, a1, la);
+    lin_src(yb - stride * bi, h, st_, b0, b1, la);
+    tlo[bi] = a0;
+    const int rows = b1 - a0 + 1;
+    for (int bj = 0; bj < nb; ++bj) {
+      const float* pl = lg + ((n * L + bi * nb + bj) * T + t) * plane + (int64_t)a0 * w;
+      float* dst = tsl + (bi * 2 + bj) * trows * w;
+      for (int i = threadIdx.x; i < rows * w; i += blockDim.x) dst[i] = pl[i];
+    }
+  }
+  __syncthreads();
+  float* ob = out + nt * (int64_t)out_res * out_res;
+  for (int X = threadIdx.x; X < out_res; X += blockDim.x) {
+    int gx0, gx1;
+    float glx;
+    lin_src(X, k, sg, gx0, gx1, glx);
+    int tx0[2], tx1[2], tbj[2];
+    float tlx[2];
+    int ncol = 0;
+    for (int bj = 0; bj < nb && ncol < 2; ++bj) {
+      const int xx = X - stride * bj;
+      if (xx < 0 || xx >= k) continue;
+      lin_src(xx, w, (float)w / (float)k, tx0[ncol], tx1[ncol], tlx[ncol]);
+      tbj[ncol++] = bj;
+    }
+#pragma unroll 4
+    for (int Y = Y0; Y < Y1; ++Y) {
+      int y0, y1;
+      float ly;
+      lin_src(Y, k, sg, y0, y1, ly);
+      const float* g0 = gsig + (y0 - r_lo) * k;
+      const float* g1 = gsig + (y1 - r_lo) * k;
+      const float glob = blend(g0[gx0], g0[gx1], g1[gx0], g1[gx1], ly, glx);
+      float sum = 0.f, cnt = 0.f;
+      for (int bi = 0; bi < nb; ++bi) {
+        const int yy = Y - stride * bi;
+        if (yy < 0 || yy >= k) continue;
+        int ty0, ty1;
+        float tly;
+        lin_src(yy, h, (float)h / (float)k, ty0, ty1, tly);
+        for (int c = 0; c < ncol; ++c) {
+          const float* pl = tsl + (bi * 2 + tbj[c]) * trows * w - tlo[bi] * w;
+          sum += sigm_fast(blend(pl[ty0 * w + tx0[c]], pl[ty0 * w + tx1[c]], pl[ty1 * w + tx0[c]],
+                                 pl[ty1 * w + tx1[c]], tly, tlx[c]));
+          cnt += 1.f;
+        }
+      }
+      ob[(int64_t)Y * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
+    }
+  }
+}
+
+int g_merge_variant = 0;   // 0 = tile rows staged in LDS where nb <= 2 (sliding_merge_stage_kernel), 1 = band kernel
+
 }  // namespace
 
 extern "C" int catseg_avgpool_rows(const void* in, int64_t S, int H, int W, int C, int ph, int pw, void* out,
@@ -295,6 +388,8 @@ extern "C" int catseg_sliding_crops(const float* raw, const int32_t* sizes, int6
   return catseg_launch_status("sliding_crops");
 }
 
+extern "C" void catseg_set_merge_variant(int v) { g_merge_variant = v; }
+
 extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h, int w, int kernel, int stride,
                                     int out_res, float* out, void* stream) {
   CATSEG_CHECK(logits && out && N > 0 && T > 0 && h > 0 && w > 0, "sliding_merge: bad args");
@@ -308,6 +403,14 @@ extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h
     CATSEG_CHECK(blocks < ((int64_t)1 << 31), "sliding_merge: grid too large");
     // LDS rows: the k-res rows under MERGE_BY output rows, + 2 for the bilinear taps
     const int rows = (int)((int64_t)(MERGE_BY - 1) * kernel / out_res) + 3;
+    // tile-plane rows under one band: (MERGE_BY - 1) output rows span (MERGE_BY - 1) h / k source rows
+    const int trows = (int)((int64_t)(MERGE_BY - 1) * h / kernel) + 3;
+    const size_t sh2 = ((size_t)rows * kernel + (size_t)4 * trows * w) * sizeof(float);
+    if (g_merge_variant == 0 && nb <= 2 && sh2 <= 64 * 1024) {
+      hipLaunchKernelGGL(sliding_merge_stage_kernel, dim3((unsigned)blocks), dim3(256), sh2, (hipStream_t)stream, logits,
+                         T, h, w, kernel, stride, nb, out_res, bands, rows, trows, out);
+      return catseg_launch_status("sliding_merge");
+    }
     hipLaunchKernelGGL(sliding_merge_band_kernel, dim3((unsigned)blocks), dim3(256), rows * kernel * sizeof(float),
                        (hipStream_t)stream, logits, T, h, w, kernel, stride, nb, out_res, bands, out);
   } else {

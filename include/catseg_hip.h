@@ -168,6 +168,10 @@ void catseg_set_head_variant(int variant);
 /* Postprocess / resize band kernel: 0 (default) = compile-time output width at W = 336 / 384 (column
  * taps hoisted per thread), 1 = runtime width.  Bit-identical (A/B only). */
 void catseg_set_post_variant(int variant);
+/* Sliding-window merge: 0 (default) = tile-plane source rows staged in LDS per band where at most 2 x 2
+ * tiles cover the output (the CAT-Seg 640 / 384 / 256 geometry), 1 = the band kernel gathering them
+ * from global memory.  Bit-identical (A/B only). */
+void catseg_set_merge_variant(int variant);
 
 /* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
  * 0 = the tiled variants, for A/B tests).  Process-wide. */
