@@ -81,46 +81,53 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
   const T* S2 = reinterpret_cast<const T*>(p.s2);
   const T* Wt = reinterpret_cast<const T*>(p.w);
 
+  // gload issues every chunk's load unconditionally (out-of-image / past-K / past-cout chunks read
+  // a clamped in-bounds address) and records what sstore must do with it (zero it, or apply the
+  // GroupNorm prologue): a load inside a per-lane branch, or a GroupNorm applied right after it,
+  // made the compiler retire each load before issuing the next (s_waitcnt vmcnt(0) between them),
+  // so a K-step paid two or three serial memory latencies.  Same values reach LDS as before.
   uint4 ra[A_CH], rw[W_CH];
+  bool a_zero[A_CH], w_zero[W_CH];
+  int a_gci[A_CH];                      // >= 0: GroupNorm+ReLU on load, channel base
   auto gload = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int64_t k = k0 + a_col[i];
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (a_ok[i] && k < K) {
-        const int tap = (int)(k / cin), ci = (int)(k % cin);
-        const int yy = a_y[i] + tap / 3 - 1, xx = a_x[i] + tap % 3 - 1;
-        if (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
-          const int64_t pix = (int64_t)yy * p.W + xx;
-          if (ci < p.c1) {
-            u = ld16(S1 + a_s[i] * p.s1_ss + p.s1_off + pix * p.c1 + ci);
-            if (p.gmean) u = gn_chunk<T>(u, gsc, gsh, ci);
-          } else {
-            u = ld16(S2 + (a_s[i] / p.s2_div) * p.s2_ss + p.s2_off + pix * p.c2 + (ci - p.c1));
-          }
-        }
-      }
-      ra[i] = u;
+      const int64_t kc = k < K ? k : K - VN;
+      const int tap = (int)(kc / cin), ci = (int)(kc % cin);
+      const int yy = a_y[i] + tap / 3 - 1, xx = a_x[i] + tap % 3 - 1;
+      const bool inside = yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+      a_zero[i] = !(a_ok[i] && k < K && inside);
+      const int64_t pix = (int64_t)min(max(yy, 0), p.H - 1) * p.W + min(max(xx, 0), p.W - 1);
+      const bool first = ci < p.c1;
+      const T* base = first ? S1 : S2;   // S2 is only selected when c2 > 0 (then it is set)
+      const int64_t off = first ? a_s[i] * p.s1_ss + p.s1_off + pix * p.c1 + ci
+                                : (a_s[i] / p.s2_div) * p.s2_ss + p.s2_off + pix * p.c2 + (ci - p.c1);
+      const T* src = base + off;
+      a_gci[i] = (first && p.gmean) ? ci : -1;
+      ra[i] = ld16(src);
     }
 #pragma unroll
     for (int i = 0; i < W_CH; ++i) {
-      const int c = tid + i * NT;
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (c < W_TOT) {
-        const int n = n0 + c / CPR;
-        const int64_t k = k0 + (c % CPR) * VN;
-        if (n < p.cout && k < K) u = ld16(Wt + (int64_t)n * K + k);
-      }
-      rw[i] = u;
+      const int c = min(tid + i * NT, W_TOT - 1);
+      const int n = n0 + c / CPR;
+      const int64_t k = k0 + (c % CPR) * VN;
+      w_zero[i] = !(n < p.cout && k < K);
+      rw[i] = ld16(Wt + (int64_t)min(n, p.cout - 1) * K + (k < K ? k : K - VN));
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], ra[i]);
+    for (int i = 0; i < A_CH; ++i) {
+      uint4 u = ra[i];
+      if (a_zero[i]) u = make_uint4(0, 0, 0, 0);
+      else if (a_gci[i] >= 0) u = gn_chunk<T>(u, gsc, gsh, a_gci[i]);
+      st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], u);
+    }
 #pragma unroll
     for (int i = 0; i < W_CH; ++i) {
       const int c = tid + i * NT;
-      if (c < W_TOT) st16(&sW[buf][(c / CPR) * LDR + (c % CPR) * VN], rw[i]);
+      if (c < W_TOT) st16(&sW[buf][(c / CPR) * LDR + (c % CPR) * VN], w_zero[i] ? make_uint4(0, 0, 0, 0) : rw[i]);
     }
   };
 
