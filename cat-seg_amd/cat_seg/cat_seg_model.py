@@ -208,8 +208,9 @@ class CATSeg(nn.Module):
         fails loudly); SURVEY §8(f) rank 4 -- backward kernels are outside the inference north star."""
         with torch.no_grad():
             eng = self.engine
-            # training re-encodes the (training) class set every step, uncached (cat_seg_predictor.py:190-224)
-            eng.set_text(self.sem_seg_head.predictor.get_text_embeds())
+            # training re-encodes the (training) class set every step, uncached (cat_seg_predictor.py:190-224);
+            # get_text_embeds installs it on the engine, and the next eval call re-installs the test cache
+            self.sem_seg_head.predictor.get_text_embeds()
             raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in batched_inputs])
             logits = eng.head_logits(raw, sizes_dev)
             targets = torch.stack([x["sem_seg"].to(eng.device) for x in batched_inputs], dim=0)

@@ -60,7 +60,13 @@ def gather_logits(local: torch.Tensor, n_total: int, group=None, out: Optional[t
         local = padded
     even = all(s == bmax for s in sizes)
     buf = out if (even and out is not None) else local.new_empty((world * bmax,) + rest)
-    dist.all_gather_into_tensor(buf, local.contiguous(), group=group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device all-gather: stage through the host (rehearsing N ranks on fewer GPUs)
+        hbuf = torch.empty(buf.shape, dtype=buf.dtype)
+        dist.all_gather_into_tensor(hbuf, local.cpu().contiguous(), group=group)
+        buf.copy_(hbuf)
+    else:
+        dist.all_gather_into_tensor(buf, local.contiguous(), group=group)
     if even:
         return buf
     if out is None:

@@ -327,9 +327,18 @@ class CatSegEngine:
         return x
 
     # ------------------------------------------------------------------ text
-    def encode_text(self, tokens: torch.Tensor) -> torch.Tensor:
-        """CLIP.encode_text + L2 norm (cat_seg_predictor.py:214-216).  tokens (T, ctx) int."""
+    def encode_text(self, tokens: torch.Tensor, truncate: bool = True) -> torch.Tensor:
+        """CLIP.encode_text + L2 norm (cat_seg_predictor.py:214-216).  tokens (T, ctx) int.
+
+        truncate: run the text transformer on the first max_t(argmax tokens[t]) + 1 positions only
+        (SURVEY Appendix B #6).  The blocks are causal (model_vpt.py:400-406) and only the EOT row
+        (the argmax id, :436) is read, so positions after the last EOT never reach the output; the
+        CLIP prompts end by position 14 of 77.  Every kernel computes a row from the same keys /
+        weights in the same order either way, so the embeddings are bit-identical (tested)."""
         a, dev = self.arch, self.device
+        if truncate:
+            last = int(torch.as_tensor(tokens).argmax(dim=1).max()) + 1
+            tokens = torch.as_tensor(tokens)[:, :last]
         tokens = tokens.to(dev, torch.int32).contiguous()
         n, ctx = tokens.shape
         TW = a.text_width
@@ -345,6 +354,10 @@ class CatSegEngine:
         out = torch.empty_like(t)
         ops.l2normalize(t, out)
         return out
+
+    def text_source(self):
+        """The class-embedding tensor the current set_text() call was given (None before any)."""
+        return None if self._text is None else self._text.src
 
     def set_text(self, text: torch.Tensor):
         """Cache the per-class-set terms (the predictor's eval cache, cat_seg_predictor.py:191-192,221-222).

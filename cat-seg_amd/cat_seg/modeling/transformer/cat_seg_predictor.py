@@ -56,7 +56,9 @@ class CATSegPredictor(nn.Module):
         self.clip_pretrained = clip_pretrained
         self.bpe_vocab = bpe_vocab
         self.engine = None
-        self.tokens = None
+        # class-prompt token ids per mode: the training step encodes TRAIN_CLASS_JSON every step,
+        # eval encodes TEST_CLASS_JSON once and caches it (cat_seg_predictor.py:190-224)
+        self.tokens = {"train": None, "test": None}
         self.cache = None
 
     @staticmethod
@@ -100,28 +102,40 @@ class CATSegPredictor(nn.Module):
         return torch.from_numpy(toks)
 
     def get_text_embeds(self, classnames=None, templates=None, clip_model=None, prompt=None):
-        """Encode + L2-normalize, cached at eval (cat_seg_predictor.py:190-224).  Returns (T, 1, C_o)."""
-        if self.cache is not None and not self.training:
+        """Encode + L2-normalize (cat_seg_predictor.py:190-224).  Returns (T, 1, C_o).
+
+        Eval: the test class set is encoded once and cached; whenever the engine holds another
+        class set (a training step ran in between) the cache is re-installed, so train / eval
+        alternation (Trainer with EVAL_PERIOD) always evaluates on the test classes.
+        Training: the train class set is re-encoded every call (uncached, as the reference)."""
+        mode = "train" if self.training else "test"
+        if mode == "test" and self.cache is not None and classnames is None:
+            if self.engine.text_source() is not self.cache:
+                self.engine.set_text(self.cache)
             return self.cache
-        classnames = classnames if classnames is not None else (
-            self.class_texts if self.training else self.test_class_texts)
-        if self.tokens is None:
-            self.tokens = self.tokenize(classnames)
-        emb = self.engine.encode_text(self.tokens).unsqueeze(1)
-        if not self.training:
+        if classnames is not None:
+            toks = self.tokenize(classnames)
+        else:
+            if self.tokens[mode] is None:
+                self.tokens[mode] = self.tokenize(self.class_texts if mode == "train" else self.test_class_texts)
+            toks = self.tokens[mode]
+        emb = self.engine.encode_text(toks).unsqueeze(1)
+        self.engine.set_text(emb)
+        if mode == "test" and classnames is None:
             self.cache = emb
-            self.engine.set_text(emb)
         return emb
 
-    def set_class_tokens(self, tokens):
-        """Use pre-tokenized prompts (T, context) for the evaluated class set."""
-        self.tokens = torch.as_tensor(tokens).long()
+    def set_class_tokens(self, tokens, mode: str = "both"):
+        """Use pre-tokenized prompts (T, context) for the train / test / both class sets."""
+        t = torch.as_tensor(tokens).long()
+        for m in (("train", "test") if mode == "both" else (mode,)):
+            self.tokens[m] = t
         self.cache = None
 
     def set_class_texts(self, class_texts: List[str]):
         """Switch the evaluated class set (a new TEST_CLASS_JSON)."""
         self.test_class_texts = list(class_texts)
-        self.tokens = None
+        self.tokens["test"] = None
         self.cache = None
 
     def forward(self, x, vis_guidance, prompt=None, gt_cls=None):

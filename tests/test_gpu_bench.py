@@ -1,0 +1,48 @@
+"""bench.py's multi-rank path on the one leased GPU (VERDICT r2 "exercise the multi-GPU bench
+path before the driver does"): `--gpus 2` self-launches two spawned ranks (detectron2 `launch`,
+train_net.py:314-324), both mapped to device local % device_count, over gloo with the logits
+staged through the host; rank 0 recomputes both ranks' seeded batches and the gathered logits
+must match them bit for bit.  The N=1 line keeps its contract fields."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench(*args, timeout=400):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(500)
+def test_bench_two_ranks_gloo_on_one_gpu():
+    line = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-images", "0", "--no-roofline",
+                  "--backend", "gloo")
+    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["backend"] == "gloo"
+    assert line["gather_matches_1gpu"] is True
+    assert line["config"]["global_batch"] == 16
+    assert line["value"] > 0 and line["steps"] == 2
+
+
+@pytest.mark.timeout(400)
+def test_bench_one_gpu_line_contract():
+    line = _bench("--steps", "2", "--warmup", "1", "--cpu-images", "0")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["gather_matches_1gpu"] is None
+    assert line["metric"].startswith("images/sec @ ViT-L/14 336², 150 classes, bs=8")
+    r = line["roofline"]
+    assert r["bound"] in ("mfma", "hbm") and 0 < r["frac"] < 1 and r["lib_sha16"]

@@ -141,6 +141,22 @@ def test_l14_ade847_reference_golden(dtype):
     gate(got[live], forced[live], dtype, "L/14 ade847 vs oracle (GPU selection)")
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_text_encoder_truncation_bit_identical(dtype):
+    """encode_text runs the causal text transformer on the first
+    max(argmax tokens) + 1 positions (14 of 77 for ade847); the embeddings must equal, bit for
+    bit, those of the full 77-position run (model_vpt.py:400-406,421-438), at T = 847."""
+    arch = VIT_L14_336
+    eng = CatSegEngine(arch, sd_of(arch), dtype=dtype)
+    tokens = torch.from_numpy(np.load(os.path.join(GOLDEN, "class_tokens.npz"))["ade847"]).int()
+    assert tokens.shape[1] == 77 and int(tokens.argmax(1).max()) + 1 <= 16
+    short = eng.encode_text(tokens).cpu()
+    full = eng.encode_text(tokens, truncate=False).cpu()
+    assert short.shape == full.shape == (847, arch.embed_dim)
+    assert torch.equal(short, full), (short - full).abs().max().item()
+
+
 # ---------------------------------------------------------------- the benchmarked batches
 @pytest.mark.timeout(900)
 def test_l14_config3_bs8_vs_oracle():

@@ -69,3 +69,34 @@ def test_catseg_training_forward_loss():
     ref = reference_loss(logits, torch.stack([b["sem_seg"] for b in batch]).int(), 255)
     got = losses["loss_sem_seg"].item()
     assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-6, (got, ref)
+
+
+def test_train_eval_alternation_keeps_the_test_class_set():
+    """eval -> train step -> eval with different train / test class lists (Trainer with EVAL_PERIOD):
+    the second eval must run on the test classes again, bit for bit the first eval's output, and the
+    training step must see the train classes (its loss equals the loss of the train-class logits)."""
+    gd = dict(np.load(os.path.join(GOLDEN, "e2e_tiny_pad.npz")))
+    model = build_model(tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": "f32"})).cuda()
+    test_tok, train_tok = gd["tokens"], gd["tokens"][::-1][:7].copy()      # 10 test classes, 7 train classes
+    model.sem_seg_head.predictor.set_class_tokens(test_tok, mode="test")
+    model.sem_seg_head.predictor.set_class_tokens(train_tok, mode="train")
+    model.arch = model.arch.replace(pad_len=int(gd["pad_len"]))
+    model._engine = None
+    im = torch.from_numpy(gd["image0"])
+    model.eval()
+    first = model([{"image": im}])[0]["sem_seg"].clone()
+    assert first.shape[0] == len(test_tok)
+    sem = torch.randint(0, len(train_tok), im.shape[-2:], generator=torch.Generator().manual_seed(3))
+    model.train()
+    loss = model([{"image": im, "sem_seg": sem}])["loss_sem_seg"].item()
+    eng = model.engine
+    assert eng.text_source().shape[0] == len(train_tok)
+    raw, sizes_dev, _ = model._batch(eng, [im])
+    with torch.no_grad():
+        train_logits = eng.head_logits(raw, sizes_dev).cpu()
+    assert train_logits.shape[1] == len(train_tok)
+    ref = reference_loss(train_logits, sem[None].int(), 255)
+    assert abs(loss - ref) <= 1e-5 * abs(ref) + 1e-6, (loss, ref)
+    model.eval()
+    second = model([{"image": im}])[0]["sem_seg"]
+    assert second.shape == first.shape and torch.equal(second, first)

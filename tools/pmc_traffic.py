@@ -9,6 +9,7 @@ families bench.py's roofline pass uses, and reports per launch:
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import re
@@ -42,7 +43,7 @@ def family(name):
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("-")]
+    args = [a for i, a in enumerate(sys.argv[1:], 1) if not a.startswith("-") and sys.argv[i - 1] not in ("-o", "--head")]
     out = sys.argv[sys.argv.index("-o") + 1] if "-o" in sys.argv else None
     fetch = load(args[0], "FETCH_SIZE")
     write = load(args[1], "WRITE_SIZE")
@@ -64,8 +65,12 @@ def main():
                   "avg_us_under_pmc": round(e["ns"] / n / 1e3, 2)}
         print(f"{k:40s} x{n:4d} fetch {res[k]['fetch_bytes_per_launch'] / 1e6:9.2f} MB  "
               f"write {res[k]['write_bytes_per_launch'] / 1e6:9.2f} MB  {res[k]['avg_us_under_pmc']:9.1f} us")
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cat-seg_amd", "cat_seg",
+                       "libcatseg_hip.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    head = sys.argv[sys.argv.index("--head") + 1] if "--head" in sys.argv else None
     if out:
-        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/pmc_step.py "
+        json.dump({"lib_sha16": sha, "git_head": head, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/pmc_step.py "
                              "(one L/14@336 T=150 bs=8 bf16 forward, eager); fetch = 2 x FETCH_SIZE",
                    "families": res}, open(out, "w"), indent=1)
 
