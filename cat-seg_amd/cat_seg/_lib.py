@@ -127,7 +127,6 @@ _SIGS = {
     "catseg_gemm_fp8": [C.POINTER(GemmArgs), vp, vp, vp],
     "catseg_quant_fp8_rows": [vp, i32, i64, i64, i64, vp, i64, vp, vp],
     "catseg_layernorm_fp8": [vp, i64, RowMap, i32, vp, i64, vp, vp, vp, i64, i64, f32, vp],
-    "catseg_set_gemm_fp8_variant": [i32],
     "catseg_semseg_confusion": [vp, i64, i64, i64, vp, i32, i32, i32, vp, vp, vp],
     "catseg_rows_gemm": [vp, i64, i64, vp, vp, f32, vp, i64, C.POINTER(RowsEpi), i32, vp],
     "catseg_rows_mlp": [vp, i64, i64, vp, vp, f32, vp, vp, i64, i32, vp, C.POINTER(RowsEpi), i32, vp],
@@ -168,24 +167,15 @@ _SIGS = {
     "catseg_sliding_merge": [vp, i64, i32, i32, i32, i32, i32, i32, vp, vp],
     "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
-    "catseg_set_persistent": [i32],
-    "catseg_set_ln_variant": [i32],
-    "catseg_set_conv_lds": [i32],
-    "catseg_set_corr_mfma": [i32],
-    "catseg_set_gemm_variant": [i32],
-    "catseg_set_gemm_group": [i32],
-    "catseg_set_mlp_pair": [i32],
-    "catseg_set_attn_variant": [i32],
-    "catseg_set_attn_tail_skip": [i32],
-    "catseg_set_ring_variant": [i32],
-    "catseg_set_classattn_variant": [i32],
-    "catseg_set_swin_variant": [i32],
-    "catseg_set_head_variant": [i32],
-    "catseg_set_post_variant": [i32],
-    "catseg_set_merge_variant": [i32],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
     "catseg_abi_version": [],
     "catseg_last_error": [],
+}
+# diagnostics entry (include/catseg_hip_tuning.h), not part of the product ABI
+_TUNING = {
+    "catseg_tuning_set": [C.c_char_p, i32],
+    "catseg_tuning_get": [C.c_char_p, C.POINTER(C.c_int)],
+    "catseg_tuning_list": [],
 }
 
 EXPORTED = tuple(_SIGS)
@@ -203,13 +193,10 @@ def load() -> C.CDLL:
             f"libcatseg_hip.so not found at {LIB_PATH}: build it with "
             "`make -C cat-seg_amd/csrc` (or __graft_entry__.build()); the CAT-Seg HIP path has no fallback")
     lib = C.CDLL(LIB_PATH)
-    for name, args in _SIGS.items():
-        if name.startswith("catseg_set_") and not hasattr(lib, name):
-            continue    # a tuning knob an older build (same-box A/B reference) lacks; compute entries must exist
+    for name, args in list(_SIGS.items()) + list(_TUNING.items()):
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = (C.c_char_p if name == "catseg_last_error" else
-                      None if name.startswith("catseg_set_") else
+        fn.restype = (C.c_char_p if name in ("catseg_last_error", "catseg_tuning_list") else
                       C.c_int64 if name == "catseg_conv3x3_workspace" else C.c_int)
     _lib = lib
     return lib
@@ -221,6 +208,22 @@ def call(name: str, *args) -> None:
     if rc != 0:
         msg = lib.catseg_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def tune(name: str, value: int) -> None:
+    """Force an A/B knob (include/catseg_hip_tuning.h; tests / tools only): process-wide, read at
+    launch.  Raises on an unknown name."""
+    call("catseg_tuning_set", name.encode(), int(value))
+
+
+def tuning(name: str) -> int:
+    v = C.c_int(0)
+    call("catseg_tuning_get", name.encode(), C.byref(v))
+    return v.value
+
+
+def tuning_knobs():
+    return load().catseg_tuning_list().decode().split(",")
 
 
 def require_gpu():

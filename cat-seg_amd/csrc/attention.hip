@@ -348,8 +348,8 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
 
 }  // namespace
 
-extern "C" void catseg_set_attn_variant(int v) { g_attn_variant = v; }
-extern "C" void catseg_set_attn_tail_skip(int on) { g_attn_tail_skip = on; }
+CATSEG_KNOB(g_attn_variant, "attn_variant");
+CATSEG_KNOB(g_attn_tail_skip, "attn_tail_skip");
 
 extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");

@@ -6,6 +6,11 @@
 
 void catseg_set_error(const char* fmt, ...);
 
+// A/B knob registration (tuning.hip, include/catseg_hip_tuning.h): a process-wide int read at
+// launch, settable by name through catseg_tuning_set; not part of the product ABI.
+struct CatsegKnobReg { CatsegKnobReg(const char* name, int* value); };
+#define CATSEG_KNOB(var, name) static CatsegKnobReg var##_knob_reg(name, &(var))
+
 #define CATSEG_CHECK(cond, msg)                      \
   do {                                               \
     if (!(cond)) {                                   \

@@ -329,7 +329,7 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 }  // namespace
 
 int g_classattn_variant = 0;   // 0 = register-resident kernel (this file), 1 = classattn_fused.hip
-extern "C" void catseg_set_classattn_variant(int v) { g_classattn_variant = v; }
+CATSEG_KNOB(g_classattn_variant, "classattn_variant");
 
 // launched by catseg_class_attention (classattn_fused.hip) after its argument checks
 int classattn2_launch(const CatsegClassAttnArgs* a, hipStream_t st) {

@@ -686,9 +686,9 @@ extern "C" int catseg_conv_tile_rows(void) { return BM; }
 
 int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st);    // conv_lds.hip
 int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st);   // conv_ring.hip
-static int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = im2col only
-extern "C" void catseg_set_conv_lds(int mode) { g_conv_mode = mode; }
-extern "C" void catseg_set_head_variant(int v) { g_head_variant = v; }
+int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = im2col only
+CATSEG_KNOB(g_conv_mode, "conv_mode");
+CATSEG_KNOB(g_head_variant, "head_variant");
 
 int catseg_conv3x3_ring_tile(const CatsegConvArgs* a);   // conv_ring.hip
 // fp32 workspace the im2col kernel would use for split-K on these args (0 = none needed)

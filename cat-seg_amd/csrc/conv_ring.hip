@@ -644,7 +644,7 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
   return catseg_launch_status("conv3x3_partial");
 }
 
-extern "C" void catseg_set_ring_variant(int v) { g_ring_variant = v; }
+CATSEG_KNOB(g_ring_variant, "ring_variant");
 
 // ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
 // The conv over the ConvTranspose output y (2H x 2W, no nonlinearity between them) equals, per

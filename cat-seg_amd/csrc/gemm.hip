@@ -1003,9 +1003,9 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
 
 }  // namespace
 
-extern "C" void catseg_set_gemm_variant(int v) { g_gemm_variant = v; }
-extern "C" void catseg_set_gemm_group(int g) { g_gemm_group = g; }
-extern "C" void catseg_set_gemm_fp8_variant(int v) { g_gemm_f8_variant = v; }
+CATSEG_KNOB(g_gemm_variant, "gemm_variant");
+CATSEG_KNOB(g_gemm_group, "gemm_group");
+CATSEG_KNOB(g_gemm_f8_variant, "gemm_fp8_variant");
 
 extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {
   CATSEG_CHECK(g && g->A && g->W && g->out && scale_a && scale_w, "gemm_fp8: null pointer");

@@ -149,8 +149,8 @@ __global__ __launch_bounds__(256) void ln_pipe_kernel(const float* __restrict__ 
   }
 }
 
-static int g_ln_variant = 0;   // 0 = pipelined persistent fp32 -> bf16 LayerNorm where it applies, 1 = one row per wave
-extern "C" void catseg_set_ln_variant(int v) { g_ln_variant = v; }
+int g_ln_variant = 0;   // 0 = pipelined persistent fp32 -> bf16 LayerNorm where it applies, 1 = one row per wave
+CATSEG_KNOB(g_ln_variant, "ln_variant");
 
 template <bool LN>
 int rownorm(const void* in, int64_t ld_in, CatsegRowMap m, int dti, void* out, int64_t ld_out, int dto,
@@ -683,7 +683,7 @@ extern "C" int catseg_l2normalize(const void* in, int64_t ld_in, CatsegRowMap in
   return rownorm<false>(in, ld_in, inmap, dtype_in, out, ld_out, dtype_out, nullptr, nullptr, rows, cols, eps, stream);
 }
 
-extern "C" void catseg_set_corr_mfma(int enable) { g_corr_mfma = enable != 0; }
+CATSEG_KNOB(g_corr_mfma, "corr_mfma");
 
 extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_stride,
                                  const int32_t* classes, int64_t B, int T, int H, int W, const float* weight,
@@ -835,7 +835,7 @@ int launch_post(const char* what, const float* logits, int64_t B, int T, int h, 
 }
 }  // namespace
 
-extern "C" void catseg_set_post_variant(int v) { g_post_variant = v; }
+CATSEG_KNOB(g_post_variant, "post_variant");
 
 extern "C" int catseg_postprocess(const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
                                   float* out, int H, int W, void* stream) {

@@ -388,7 +388,7 @@ extern "C" int catseg_sliding_crops(const float* raw, const int32_t* sizes, int6
   return catseg_launch_status("sliding_crops");
 }
 
-extern "C" void catseg_set_merge_variant(int v) { g_merge_variant = v; }
+CATSEG_KNOB(g_merge_variant, "merge_variant");
 
 extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h, int w, int kernel, int stride,
                                     int out_res, float* out, void* stream) {

@@ -350,8 +350,8 @@ int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const flo
                                const void* w1, const float* b1, int64_t hidden, int act, const void* w2,
                                const CatsegRowsEpi* epi, hipStream_t st);
 
-static bool g_persistent = true;
-extern "C" void catseg_set_persistent(int enable) { g_persistent = enable != 0; }
+int g_persistent = 1;
+CATSEG_KNOB(g_persistent, "persistent");
 
 extern "C" int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const float* ln_gamma, const float* ln_beta,
                                 float eps, const void* w, int64_t N, const CatsegRowsEpi* epi, int dtype,

@@ -593,7 +593,7 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
 }
 
 int g_mlp_pair = 1;   // persistent MLP hidden-unit order: 1 = paired 16-byte hidden stores (default), 0 = 8-byte
-extern "C" void catseg_set_mlp_pair(int on) { g_mlp_pair = on; }
+CATSEG_KNOB(g_mlp_pair, "mlp_pair");
 
 template <bool PAIR>
 int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,

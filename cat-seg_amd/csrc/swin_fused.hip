@@ -456,7 +456,7 @@ int g_swin_variant = 0;   // 0 = pipelined (swin_fused2_kernel), 1 = two barrier
 
 }  // namespace
 
-extern "C" void catseg_set_swin_variant(int v) { g_swin_variant = v; }
+CATSEG_KNOB(g_swin_variant, "swin_variant");
 
 extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->x && a->ln_g && a->ln_b && a->w_qkv && a->b_qkv && a->gqk && a->out,

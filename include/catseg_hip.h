@@ -15,6 +15,8 @@
  *
  * Each entry names the reference function(s) it replaces (paths relative to the
  * reference repo root).  The Python host mirror is cat-seg_amd/cat_seg/ops.py.
+ * Kernel variants are chosen automatically per shape; the A/B knobs used by the tests and
+ * tools/ live behind a separate diagnostics header (catseg_hip_tuning.h), not in this ABI.
  */
 #ifndef CATSEG_HIP_H
 #define CATSEG_HIP_H
@@ -86,18 +88,7 @@ int catseg_quant_fp8_rows(const void* x, int dtype, int64_t ld_x, int64_t rows, 
 int catseg_layernorm_fp8(const void* x, int64_t ld_x, CatsegRowMap inmap, int dtype_x, void* q, int64_t ld_q,
                          float* scale, const float* gamma, const float* beta, int64_t rows, int64_t cols, float eps,
                          void* stream);
-void catseg_set_gemm_fp8_variant(int variant);
 
-/* Tile selection of the bf16 GEMM: 0 = automatic (default), -1 = never the LDS-DMA
- * pipelined kernel, 1..8 = force one of its tile / stage / K-depth configurations
- * (gemm.hip try_gemm3) where the shape allows.  For A/B tests and tuning; process-wide. */
-void catseg_set_gemm_variant(int variant);
-/* tile order of the pipelined bf16/fp8 GEMM: 0 = row-major, G > 0 = grouped (G m-tiles swept
- * across all n-tiles, so an XCD's contiguous tile range is a 2-D block of the output) */
-void catseg_set_gemm_group(int group_m);
-/* persistent MLP (Swin / class MLP): 1 (default) = paired hidden-unit order with 16-byte hidden-tile
- * stores, 0 = the 8-byte-store order; bit-identical results (A/B only) */
-void catseg_set_mlp_pair(int on);
 
 /* ---------------------------------------------------------------------------
  * Row-block kernels over the 128-channel cost-embedding rows (K = 128).
@@ -151,31 +142,7 @@ int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const float* mean, c
                       const float* gamma, const float* beta, int cpg, const void* w, int64_t N,
                       const CatsegRowsEpi* epi, void* stream);
 
-/* Select the bf16 conv3x3 kernel family, for A/B tests (process-wide): 2 = row-ring kernel
- * with register-resident weights (default), 1 = LDS-tile kernel, 0 = im2col only.  Shapes a
- * family does not cover fall through to the next one down. */
-void catseg_set_conv_lds(int mode);
-/* Row-ring conv A/B knobs (process-wide, for tools/micro_ring.py): 0 = default; 1 / 2 =
- * alternative wave splits of the 48- / 32-channel wide-map variants; 3 / 4 = half / double
- * band length. */
-void catseg_set_ring_variant(int variant);
-/* Swin window kernel: 0 = pipelined (head h+1's projection beside head h's attention, one
- * barrier per head; default), 1 = two barriers per head (A/B reference). */
-void catseg_set_swin_variant(int variant);
-/* Head conv (bf16, 32 channels): 0 = v_dot2c band (default; compile-time width at W = 96), 1 = MFMA tap
- * image + shift-add, 2 = the band kernel with a runtime width (A/B). */
-void catseg_set_head_variant(int variant);
-/* Postprocess / resize band kernel: 0 (default) = compile-time output width at W = 336 / 384 (column
- * taps hoisted per thread), 1 = runtime width.  Bit-identical (A/B only). */
-void catseg_set_post_variant(int variant);
-/* Sliding-window merge: 0 (default) = tile-plane source rows staged in LDS per band where at most 2 x 2
- * tiles cover the output (the CAT-Seg 640 / 384 / 256 geometry), 1 = the band kernel gathering them
- * from global memory.  Bit-identical (A/B only). */
-void catseg_set_merge_variant(int variant);
 
-/* Select the persistent register-weight bf16 variants of the two row kernels (default 1;
- * 0 = the tiled variants, for A/B tests).  Process-wide. */
-void catseg_set_persistent(int enable);
 
 /* catseg_layernorm — LayerNorm over the last dim (fp32 math).  Replaces
  * model_vpt.py:156-162 (ln_pre/ln_1/ln_2/ln_post/ln_final) and the nn.LayerNorm of
@@ -184,10 +151,6 @@ int catseg_layernorm(const void* in, int64_t ld_in, CatsegRowMap inmap, int dtyp
                      void* out, int64_t ld_out, int dtype_out,
                      const float* gamma, const float* beta, int64_t rows, int64_t cols,
                      float eps, void* stream);
-/* fp32 -> bf16 LayerNorm of >= 2048 rows of 1024 (the ViT's ln_1 / ln_2 / ln_post): 0 = persistent
- * waves with the next row's loads in flight, 512 workgroups (default), 1 = one row per wave (A/B
- * reference; bit-identical), 2 / 3 = the persistent form on 256 / 1024 workgroups.  Process-wide. */
-void catseg_set_ln_variant(int variant);
 
 /* catseg_l2normalize — x / max(||x||, eps) per row (F.normalize, model.py:649-650,
  * cat_seg_predictor.py:216, model.py:714). */
@@ -216,12 +179,6 @@ typedef struct {
   int dtype;
 } CatsegAttnArgs;
 int catseg_attention(const CatsegAttnArgs* args, void* stream);
-/* Tiling of the dense (mode 0, non-causal) bf16/fp32 path, for A/B tests (process-wide):
- * 0 = default; 1..5 = alternative waves / key-block / query-tile configurations. */
-void catseg_set_attn_variant(int variant);
-/* dense attention: 1 (default) skips the MFMAs of key tiles wholly past the sequence end (the
- * last 64-key block of L = 577 holds one key); 0 computes and masks them.  Bit-identical (A/B only). */
-void catseg_set_attn_tail_skip(int on);
 
 /* catseg_linear_attention — class aggregation attention (LinearAttention,
  * model.py:256-286, inside AttentionLayer model.py:338-354 and the padding of
@@ -337,10 +294,6 @@ int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64_t corr_b_s
                       const int32_t* classes, int64_t B, int T, int H, int W,
                       const float* weight, const float* bias, int hidden,
                       void* out, int dtype, void* stream);
-/* bf16, hidden = 128: the 7x7 conv runs as an MFMA GEMM over the 49 taps with hi/lo bf16
- * operand splits (default 1: weights staged in LDS by one coalesced sweep; 2 = the same kernel
- * gathering its weight fragments from global memory; 0 = the VALU kernel; A/B tests).  Process-wide. */
-void catseg_set_corr_mfma(int enable);
 
 /* catseg_topk_classes — per image, the top-k classes by max-over-pixels cosine
  * (model.py:694-696), written sorted by (max descending, class index ascending): the set
@@ -449,10 +402,6 @@ typedef struct {
   const void* tgk_t; int64_t ld_tgk_t; int64_t tgk_t_bstride;
 } CatsegClassAttnArgs;
 int catseg_class_attention(const CatsegClassAttnArgs* args, void* stream);
-/* kernel choice for catseg_class_attention (A/B and tests): 0 = register-resident form, one
- * pixel per 4-wave workgroup (classattn2.hip, default, T <= 256); 1 = the chunked two-pass form
- * (classattn_fused.hip). */
-void catseg_set_classattn_variant(int variant);
 
 /* ---------------------------------------------------------------------------
  * Class-attention pooling (POOLING_SIZES != [1,1]; ClassTransformerLayer,

@@ -73,6 +73,19 @@ def test_capi_library_exports_every_header_symbol():
     assert not missing, missing
     assert declared <= set(L.EXPORTED) | {"catseg_conv3x3_head_gn"}
     assert lib.catseg_abi_version() == 1
+    # no A/B switches in the product ABI: they sit behind the diagnostics header only
+    assert not any(s.startswith("catseg_set_") or "tuning" in s for s in declared)
+    thdr = open(os.path.join(ROOT, "include", "catseg_hip_tuning.h")).read()
+    tdecl = set(re.findall(r"\b(catseg_[a-z0-9_]+)\s*\(", thdr))
+    assert tdecl == {"catseg_tuning_set", "catseg_tuning_get", "catseg_tuning_list"}
+    assert all(hasattr(lib, s) for s in tdecl)
+    knobs = L.tuning_knobs()
+    assert "gemm_variant" in knobs and len(knobs) == len(set(knobs))
+    L.tune("gemm_variant", 5)
+    assert L.tuning("gemm_variant") == 5
+    L.tune("gemm_variant", 0)
+    with pytest.raises(RuntimeError):
+        L.tune("no_such_knob", 1)
     assert lib.catseg_conv_tile_rows() == 128
 
 

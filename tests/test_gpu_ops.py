@@ -122,7 +122,7 @@ def test_gemm_pipelined_variants(variant):
     arow = A.reshape(B, L_, K)[:, 1:].reshape(-1, K)
     lib = L.load()
     try:
-        lib.catseg_set_gemm_variant(variant)
+        L.tune("gemm_variant", variant)
         for act, odt in ((L.ACT_QUICKGELU, torch.bfloat16), (L.ACT_NONE, torch.float32)):
             out = torch.full((M, N), float("nan"), device=dev, dtype=odt)
             r = res.to(dev, odt)
@@ -135,7 +135,7 @@ def test_gemm_pipelined_variants(variant):
             close(out, ref, atol=1e-4 if odt == torch.float32 else 2e-2, rtol=0 if odt == torch.float32 else 1e-2,
                   what=f"gemm3 variant {variant} act {act}")
     finally:
-        lib.catseg_set_gemm_variant(0)
+        L.tune("gemm_variant", 0)
 
 
 # ----------------------------------------------------------------------------- fp8 (config 5)
@@ -206,7 +206,7 @@ def test_gemm_fp8_variants(variant):
     wd = qw.double() * sw.double()[:, None]
     lib = L.load()
     try:
-        lib.catseg_set_gemm_fp8_variant(variant)
+        L.tune("gemm_fp8_variant", variant)
         for act, odt in ((L.ACT_QUICKGELU, torch.bfloat16), (L.ACT_NONE, torch.float32)):
             out = torch.full((M, N), float("nan"), device=dev, dtype=odt)
             r = res.to(dev, odt)
@@ -219,7 +219,7 @@ def test_gemm_fp8_variants(variant):
             close(out, ref, atol=1e-4 if odt == torch.float32 else 2e-2, rtol=0 if odt == torch.float32 else 1e-2,
                   what=f"gemm_fp8 variant {variant} act {act}")
     finally:
-        lib.catseg_set_gemm_fp8_variant(0)
+        L.tune("gemm_fp8_variant", 0)
 
 
 def test_gemm_fp8_vit_shapes_vs_bf16():
@@ -271,7 +271,7 @@ def test_layernorm_l2(cols, dt):
 @pytest.mark.parametrize("rows", [4616, 2308, 2049])
 def test_layernorm_pipelined_rows(rows):
     """The ViT's ln_1 / ln_2 / ln_post shape (fp32 rows of 1024 -> bf16): the persistent pipelined
-    kernel (catseg_set_ln_variant 0, default) equals the one-row-per-wave kernel bit for bit and
+    kernel (tuning knob ln_variant 0, default) equals the one-row-per-wave kernel bit for bit and
     meets fp64 LayerNorm to bf16 rounding (model_vpt.py:156-162)."""
     cols = 1024
     x = rnd(rows, cols, seed=18) * 3 + 0.5
@@ -280,11 +280,11 @@ def test_layernorm_pipelined_rows(rows):
     lib = L.load()
     outs = []
     for v in (0, 1):
-        lib.catseg_set_ln_variant(v)
+        L.tune("ln_variant", v)
         o = torch.empty(rows, cols, device=dev, dtype=torch.bfloat16)
         ops.layernorm(x.to(dev), g.to(dev), b.to(dev), o)
         outs.append(o)
-    lib.catseg_set_ln_variant(0)
+    L.tune("ln_variant", 0)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     close(outs[0], F.layer_norm(x.double(), (cols,), g.double(), b.double(), 1e-5), atol=3e-2, rtol=1e-2, what="LN pipe")
@@ -310,7 +310,7 @@ def test_attention_dense(dt, L_, H, causal):
 
 @pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_attention_dense_tilings(variant):
-    """Every A/B tiling of the dense path (catseg_set_attn_variant) == the default tiling."""
+    """Every A/B tiling of the dense path (tuning knob attn_variant) == the default tiling."""
     B, L_, H, d = 2, 577, 4, 64
     q = (rnd(B * L_, 3 * H * d, seed=19) * 2).to(dev, torch.bfloat16)
     args = (q[:, :H * d], q[:, H * d:2 * H * d], q[:, 2 * H * d:])
@@ -319,11 +319,11 @@ def test_attention_dense_tilings(variant):
     ops.attention(*args, ref, **kw)
     lib = L.load()
     try:
-        lib.catseg_set_attn_variant(variant)
+        L.tune("attn_variant", variant)
         out = torch.empty_like(ref)
         ops.attention(*args, out, **kw)
     finally:
-        lib.catseg_set_attn_variant(0)
+        L.tune("attn_variant", 0)
     close(out, ref, atol=8e-3, what=f"attention tiling {variant}")
 
 
@@ -574,7 +574,7 @@ def test_corr_embed_topk(dt):
         lib = L.load()
         try:
             for mode in (1, 0):
-                lib.catseg_set_corr_mfma(mode)
+                L.tune("corr_mfma", mode)
                 X.zero_()
                 ops.corr_embed(cd, t_stride=B * H * W, b_stride=H * W, B=B, T=k, H=H, W=W,
                                weight=w.reshape(hid, 49).to(dev), bias=b.to(dev), out=X, classes=cls)
@@ -582,7 +582,7 @@ def test_corr_embed_topk(dt):
                 err = (got - ref).abs() - 2.0 ** -8 * ref.abs()
                 assert err.max().item() <= 1e-6, (mode, err.max().item())
         finally:
-            lib.catseg_set_corr_mfma(1)
+            L.tune("corr_mfma", 1)
 
 
 @pytest.mark.parametrize("B,T,HW,k", [(4, 847, 576, 256), (3, 459, 576, 256), (2, 300, 37, 256), (1, 2048, 64, 1000)])
@@ -642,7 +642,7 @@ def test_bicubic_postprocess():
 
 @pytest.mark.parametrize("HW,crop", [(336, None), (384, None), (336, (90, 77))])
 def test_postprocess_compile_time_width(HW, crop):
-    """The band kernel with a compile-time output width (catseg_set_post_variant 0, W = 336 / 384, the
+    """The band kernel with a compile-time output width (tuning knob post_variant 0, W = 336 / 384, the
     CAT-Seg eval outputs) vs torch (sigmoid -> bilinear, align_corners=False, sem_seg_postprocess crop)
     and bit for bit vs the runtime-width band kernel (variant 1)."""
     lib = L.load()
@@ -650,7 +650,7 @@ def test_postprocess_compile_time_width(HW, crop):
     outs = []
     try:
         for v in (0, 1):
-            lib.catseg_set_post_variant(v)
+            L.tune("post_variant", v)
             o = torch.empty(2, 5, HW, HW, device=dev)
             if crop is None:
                 ops.postprocess(lg, o)
@@ -659,7 +659,7 @@ def test_postprocess_compile_time_width(HW, crop):
             torch.cuda.synchronize()
             outs.append(o)
     finally:
-        lib.catseg_set_post_variant(0)
+        L.tune("post_variant", 0)
     src = lg.cpu() if crop is None else lg.cpu()[:, :, :crop[0], :crop[1]]
     ref = F.interpolate(src.sigmoid(), size=(HW, HW), mode="bilinear", align_corners=False)
     close(outs[0], ref, atol=2e-6, what="postprocess W=%d" % HW)
@@ -668,9 +668,9 @@ def test_postprocess_compile_time_width(HW, crop):
 
 @pytest.fixture(params=["persistent", "tiled"])
 def rows_variant(request):
-    L.load().catseg_set_persistent(1 if request.param == "persistent" else 0)
+    L.tune("persistent", 1 if request.param == "persistent" else 0)
     yield request.param
-    L.load().catseg_set_persistent(1)
+    L.tune("persistent", 1)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
@@ -756,7 +756,7 @@ def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
     if c2:
         xin = torch.cat([xin, x2.to(dt).double().repeat_interleave(T, 0)], -1)
     ref = F.conv2d(xin.permute(0, 3, 1, 2), w.to(dt).double(), padding=1)
-    L.load().catseg_set_conv_lds(lds)
+    L.tune("conv_mode", lds)
     try:
         out = torch.empty(S * H * W_, co, device=dev, dtype=dt)
         xs = x1.reshape(-1, c1).contiguous().to(dev, dt)
@@ -774,7 +774,7 @@ def test_conv3x3_decoder_shapes(W_, c1, c2, co, gn, lds):
         gref = ref.reshape(S, co // 16, 16, H * W_)
         close(m_, gref.mean((-1, -2)).reshape(-1), atol=2e-3, what="gn mean")
     finally:
-        L.load().catseg_set_conv_lds(2)
+        L.tune("conv_mode", 2)
 
 
 def test_convt64_gn():
@@ -867,11 +867,11 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
     lib = L.load()
     merged1 = torch.empty_like(merged)
     try:
-        lib.catseg_set_merge_variant(1)
+        L.tune("merge_variant", 1)
         ops.sliding_merge(lg.to(dev), merged1, kernel=k, stride=stride, out_res=res)
         torch.cuda.synchronize()
     finally:
-        lib.catseg_set_merge_variant(0)
+        L.tune("merge_variant", 0)
     assert torch.equal(merged, merged1)
     out = torch.empty(1, T, 480, 400, device=dev)
     ops.resize_bilinear(merged[:1], out, crop=(res, res))
@@ -1012,7 +1012,7 @@ def test_swin_proj_mlp_equals_separate_kernels():
 
 @pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
 def test_mlp_pair_order_bit_identical(act):
-    """The persistent MLP's paired hidden-unit order (catseg_set_mlp_pair 1, the default: 16-byte
+    """The persistent MLP's paired hidden-unit order (tuning knob mlp_pair 1, the default: 16-byte
     hidden-tile stores) equals the 8-byte-store order (0) bit for bit, for the Swin MLP (GELU),
     the class MLP (ReLU, + res2) and the fused Swin proj + MLP, on ragged M."""
     lib = L.load()
@@ -1027,7 +1027,7 @@ def test_mlp_pair_order_bit_identical(act):
     outs = {}
     try:
         for pair in (1, 0):
-            lib.catseg_set_mlp_pair(pair)
+            L.tune("mlp_pair", pair)
             o1 = torch.empty_like(y)
             ops.rows_mlp(y, w1, b1, w2, o1, ln=(g, b), b2=b2, act=act, res=y,
                          res2=x if act == L.ACT_RELU else None)
@@ -1036,7 +1036,7 @@ def test_mlp_pair_order_bit_identical(act):
             torch.cuda.synchronize()
             outs[pair] = (o1, o2)
     finally:
-        lib.catseg_set_mlp_pair(1)
+        L.tune("mlp_pair", 1)
     assert torch.equal(outs[1][0], outs[0][0]), (outs[1][0].float() - outs[0][0].float()).abs().max().item()
     assert torch.equal(outs[1][1], outs[0][1]), (outs[1][1].float() - outs[0][1].float()).abs().max().item()
 
@@ -1044,7 +1044,7 @@ def test_mlp_pair_order_bit_identical(act):
 @pytest.mark.parametrize("H,W", [(96, 96), (50, 37)])
 def test_head_conv_mfma_tap_image(H, W):
     """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the MFMA tap-image
-    kernel (catseg_set_head_variant 1) vs fp64 and vs the v_dot2c band kernel (variant 0, the
+    kernel (tuning knob head_variant 1) vs fp64 and vs the v_dot2c band kernel (variant 0, the
     default; compile-time width at W = 96), with the top-k class scatter; ragged band (H % 8 != 0)
     included; variant 2 (runtime width) equals variant 0 bit for bit."""
     B, T, C = 2, 3, 32
@@ -1063,13 +1063,13 @@ def test_head_conv_mfma_tap_image(H, W):
     cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
     outs = []
     for v in (1, 0, 2):
-        lib.catseg_set_head_variant(v)
+        L.tune("head_variant", v)
         logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
         ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
                          bias=0.25, out=logits, T_out=T + 2, classes=cls,
                          gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16))
         outs.append(logits.cpu())
-    lib.catseg_set_head_variant(0)
+    L.tune("head_variant", 0)
     for bi in range(B):
         for t in range(T):
             # fp16 staging of relu(GN(x)) (as the band kernel): ~5e-4 per product, 288 terms

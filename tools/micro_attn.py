@@ -1,4 +1,4 @@
-"""Time the dense attention tilings (catseg_set_attn_variant) on the ViT-L/14@336 shape
+"""Time the dense attention tilings (tuning knob attn_variant) on the ViT-L/14@336 shape
 (8 images x 16 heads x 577 tokens, head_dim 64, bf16) and check them against variant 0.
 usage: python tools/micro_attn.py [variants, default "0,1,2,3,4,5"]"""
 import os, sys
@@ -17,12 +17,12 @@ out = torch.empty(B * Lq, H * d, device="cuda", dtype=torch.bfloat16)
 def run():
     ops.attention(qkv[:, :H * d], qkv[:, H * d:2 * H * d], qkv[:, 2 * H * d:], out, n_seq=B, seq_len=Lq, n_heads=H,
                   head_dim=d, scale=d ** -0.5)
-lib.catseg_set_attn_variant(0); run(); ref = out.clone()
+L.tune("attn_variant", 0); run(); ref = out.clone()
 flops = 4 * B * H * Lq * Lq * d
 res = {}
 for rnd in range(5):
     for v in variants:
-        lib.catseg_set_attn_variant(v)
+        L.tune("attn_variant", v)
         run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -31,8 +31,8 @@ for rnd in range(5):
         e1.record(); torch.cuda.synchronize()
         res.setdefault(v, []).append(e0.elapsed_time(e1) / 20)
 for v in variants:
-    lib.catseg_set_attn_variant(v); run(); torch.cuda.synchronize()
+    L.tune("attn_variant", v); run(); torch.cuda.synchronize()
     err = (out.float() - ref.float()).abs().max().item()
     t = sorted(res[v])[2]
     print(f"variant {v}: {t * 1e3:7.1f} us  {flops / t / 1e9:6.1f} TF/s  max diff vs v0 {err:.2e}", flush=True)
-lib.catseg_set_attn_variant(0)
+L.tune("attn_variant", 0)

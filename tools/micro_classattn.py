@@ -29,7 +29,7 @@ def main():
         times = {v: [] for v in variants}
         for rnd in range(7):
             for v in variants:
-                lib.catseg_set_classattn_variant(v)
+                L.tune("classattn_variant", v)
                 y = torch.empty_like(X)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -40,7 +40,7 @@ def main():
                 if rnd > 0:
                     times[v].append(e0.elapsed_time(e1) * 1e3)
                 ys[v] = y
-        lib.catseg_set_classattn_variant(0)
+        L.tune("classattn_variant", 0)
         d = (ys[variants[0]].float() - ys[variants[-1]].float()).abs()
         med = {v: sorted(t)[len(t) // 2] for v, t in times.items()}
         print(f"T={T}: max|diff| first/last variant {d.max().item():.3e} mean {d.mean().item():.3e}"

@@ -12,7 +12,7 @@ from cat_seg import ops
 from cat_seg import _lib as L
 
 variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").split(",")]
-# variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (catseg_set_gemm_group)
+# variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (tuning knob gemm_group)
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True),
@@ -40,8 +40,8 @@ for name, (N, K, act, has_res) in shapes.items():
     def run():
         ops.gemm(A, W, out, bias=bias, act=act, res=R)
     def setv(v):
-        lib.catseg_set_gemm_variant(0 if v >= 1000 else v)
-        lib.catseg_set_gemm_group(v - 1000 if v >= 1000 else 0)
+        L.tune("gemm_variant", 0 if v >= 1000 else v)
+        L.tune("gemm_group", v - 1000 if v >= 1000 else 0)
     for v in variants:
         setv(v)
         out.zero_()
@@ -76,5 +76,5 @@ for name, (N, K, act, has_res) in shapes.items():
         t = sorted(res[(name, v)]["t"])[3]
         print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  "
               f"max_err {res[(name, v)]['err']:.3e}", flush=True)
-lib.catseg_set_gemm_variant(0)
-lib.catseg_set_gemm_group(0)
+L.tune("gemm_variant", 0)
+L.tune("gemm_group", 0)

@@ -39,8 +39,8 @@ for N, outdt in ((3072, torch.bfloat16), (1024, torch.float32)):
         out = torch.empty(M, N, device=dev, dtype=outdt)
         row = []
         for v in (9, 10, 5):
-            row.append(timeit(lambda: (lib.catseg_set_gemm_variant(v), ops.gemm(A, W, out))))
+            row.append(timeit(lambda: (L.tune("gemm_variant", v), ops.gemm(A, W, out))))
         tm = timeit(lambda: torch.mm(A, W.t()))
         print(f"N={N} K={K:5d} out={str(outdt)[6:]:9s} gemm8 {row[0]:7.1f} us  mainloop-only {row[1]:7.1f} us  "
               f"128x128 {row[2]:7.1f} us  torch.mm {tm:7.1f} us", flush=True)
-lib.catseg_set_gemm_variant(0)
+L.tune("gemm_variant", 0)

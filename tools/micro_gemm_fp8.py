@@ -1,4 +1,4 @@
-"""Time the fp8 GEMM tiles (catseg_set_gemm_fp8_variant) on the ViT-L/14@336 (B=8) shapes.
+"""Time the fp8 GEMM tiles (tuning knob gemm_fp8_variant) on the ViT-L/14@336 (B=8) shapes.
 usage: python tools/micro_gemm_fp8.py [variants, default "0,1,15,17,19,20,21,23,24"]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -26,7 +26,7 @@ for name, (N, K, act, has_res) in shapes.items():
     res = {}
     for rnd in range(5):
         for v in variants:
-            lib.catseg_set_gemm_fp8_variant(v)
+            L.tune("gemm_fp8_variant", v)
             try:
                 ops.gemm_fp8(qa, sa, qw, sw, out, bias=bias, act=act, res=R)
             except RuntimeError:
@@ -41,4 +41,4 @@ for name, (N, K, act, has_res) in shapes.items():
     for v, t in res.items():
         t = sorted(t)[len(t) // 2]
         print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us {flops / t / 1e9:8.1f} TF/s")
-lib.catseg_set_gemm_fp8_variant(0)
+L.tune("gemm_fp8_variant", 0)

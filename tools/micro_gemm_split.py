@@ -31,7 +31,7 @@ for name, m, n, k, v, f32 in cases:
     W = ((torch.rand(n, k, device="cuda") * 2 - 1) / k ** 0.5).to(torch.bfloat16)
     out = torch.empty(m, n, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
     bias = torch.rand(n, device="cuda")
-    lib.catseg_set_gemm_variant(v)
+    L.tune("gemm_variant", v)
     ts = []
     for r in range(7):
         ops.gemm(A, W, out, bias=bias)
@@ -43,4 +43,4 @@ for name, m, n, k, v, f32 in cases:
         ts.append(e0.elapsed_time(e1) / 20)
     t = sorted(ts)[3]
     print(f"{name:28s} M={m:6d} N={n:5d} K={k:5d}: {t * 1e3:7.1f} us  {2 * m * n * k / t / 1e9:7.1f} TF/s", flush=True)
-lib.catseg_set_gemm_variant(0)
+L.tune("gemm_variant", 0)

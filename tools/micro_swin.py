@@ -1,4 +1,4 @@
-"""Time the fused Swin window kernel variants (catseg_set_swin_variant) at config 3 (S = 1200 slices,
+"""Time the fused Swin window kernel variants (tuning knob swin_variant) at config 3 (S = 1200 slices,
 24x24, 12x12 windows, 4 heads x 32) for shift 0 and 6, and compare their outputs.
 usage: python tools/micro_swin.py [variants, default 0,1]"""
 import os, sys
@@ -28,14 +28,14 @@ for shift in (0, 6):
                                   n_heads=4, head_dim=32, scale=32 ** -0.5)
     res, ref = {}, None
     for v in variants:
-        lib.catseg_set_swin_variant(v)
+        L.tune("swin_variant", v)
         run(); torch.cuda.synchronize()
         o = out.float().clone()
         ref = o if ref is None else ref
         res[v] = {"diff": (o - ref).abs().max().item(), "t": []}
     for r in range(5):
         for v in variants:
-            lib.catseg_set_swin_variant(v)
+            L.tune("swin_variant", v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(5):
@@ -45,4 +45,4 @@ for shift in (0, 6):
     for v in variants:
         print(f"shift {shift} variant {v}: {sorted(res[v]['t'])[2] * 1e3:7.1f} us  max diff vs first {res[v]['diff']:.3e}",
               flush=True)
-lib.catseg_set_swin_variant(0)
+L.tune("swin_variant", 0)

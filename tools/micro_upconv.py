@@ -1,4 +1,4 @@
-"""Time catseg_upconv3x3 tiling variants (catseg_set_ring_variant) at the L/14@336 bs=8 T=150 decoder shapes
+"""Time catseg_upconv3x3 tiling variants (tuning knob ring_variant) at the L/14@336 bs=8 T=150 decoder shapes
 (S = 1200 slices): Up1 = 24x24x128 -> 48x48x64, Up2 = relu(GN(48x48x64)) -> 96x96x32, addend included.
 usage: python tools/micro_upconv.py [variants, default 0]"""
 import os, sys
@@ -28,7 +28,7 @@ for name, H, ci, co, gn in (("up1", 24, 128, 64, False), ("up2", 48, 64, 32, Tru
     ref = None
     res = {}
     for v in variants:
-        lib.catseg_set_ring_variant(v)
+        L.tune("ring_variant", v)
         ops.upconv3x3(src, w, out, S=S, H=H, W=H, c1=ci, gn=g, stats=st, addend=add, addend_div=T)
         torch.cuda.synchronize()
         o = out.float().clone()
@@ -37,7 +37,7 @@ for name, H, ci, co, gn in (("up1", 24, 128, 64, False), ("up2", 48, 64, 32, Tru
         res[v] = {"same": bool(torch.equal(o, ref)), "t": []}
     for r in range(7):
         for v in variants:
-            lib.catseg_set_ring_variant(v)
+            L.tune("ring_variant", v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(5):
@@ -47,4 +47,4 @@ for name, H, ci, co, gn in (("up1", 24, 128, 64, False), ("up2", 48, 64, 32, Tru
     for v in variants:
         t = sorted(res[v]["t"])[3]
         print(f"{name} variant {v:2d}: {t * 1e3:7.1f} us  bit-identical to first: {res[v]['same']}", flush=True)
-lib.catseg_set_ring_variant(0)
+L.tune("ring_variant", 0)

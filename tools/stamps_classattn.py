@@ -19,7 +19,7 @@ bias = 0.1 * torch.randn(3 * D, device=dev)
 tg = (0.5 * torch.randn(T, 2 * D, device=dev)).to(torch.bfloat16)
 kp, vp = torch.randn(D, device=dev), torch.randn(D, device=dev)
 for v in (16 + 4, 16 + 4 + 3):
-    lib.catseg_set_classattn_variant(v)
+    L.tune("classattn_variant", v)
     for _ in range(3):
         y = torch.zeros_like(X)
         ops.class_attention(X, (g1, b1), W, bias, tg, y, B=B, T=T, HW=HW, n_heads=4, head_dim=32, n_pad=106,
@@ -30,4 +30,4 @@ for v in (16 + 4, 16 + 4 + 3):
     tot = st[:, 7, 3] - st[:, 0, 0]
     print(f"variant {v}: cycles per pixel (median over WGs, pixels 1-7): LN {ln[:, 1:].median():.0f}  "
           f"A {A[:, 1:].median():.0f}  B {Bq[:, 1:].median():.0f}  8 pixels total {tot.median():.0f}", flush=True)
-lib.catseg_set_classattn_variant(0)
+L.tune("classattn_variant", 0)
