@@ -294,6 +294,166 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// CLIP ViT MHA (bf16, head_dim 64, dense, non-causal; model_vpt.py:202-206), one wave per
+// 16 queries of one (image, head), NW waves sharing 64-key K/V blocks in LDS.
+//   * K/V staging is register-double-buffered: block b+1's global loads are issued before
+//     block b's MFMAs and written to the other LDS buffer after them, one barrier per block.
+//     Rows past L read the clamped row L-1 (no per-element branch); their scores are masked.
+//   * Defer-max online softmax (cdna_hip_programming.md T13): the running max m of a query
+//     moves only when a block's scores exceed it by more than 2^THR in exp2 units, so the
+//     common block costs one max chain per lane and one wave vote -- no cross-lane reduction,
+//     no rescale of O.  The softmax is invariant to the subtracted constant; p <= 2^THR.
+//   * Row sums l from the MFMA (all-ones A fragment times P^T), as attn_kernel.
+// ------------------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
+  constexpr int D = 64, KB = 64, KP = D + 16, NT = NW * 64;
+  constexpr int CH = KB * D / 8;                        // 16-byte chunks per K (or V) block
+  constexpr int BUF = 2 * KB * KP;                      // K then V of one block
+  constexpr int NC = (2 * CH + NT - 1) / NT;            // chunks staged per thread
+  constexpr float THR = 16.f;                           // defer-max threshold (log2 units)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int s = blockIdx.y / p.H, h = blockIdx.y % p.H;
+  const int g = lane >> 4, col = lane & 15;
+  const int L = p.L;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const int q0 = (blockIdx.x * NW + wave) * 16;
+  const bool live = q0 < L;                             // wave-uniform
+  const int qi = q0 + col;
+  const bool q_ok = qi < L;
+  const int64_t row0 = (int64_t)s * L;
+
+  s16x8 qf[2];
+  {
+    const bf16* Q = reinterpret_cast<const bf16*>(p.q) + (row0 + (q_ok ? qi : 0)) * p.ld + h * D;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  }
+  // staging: chunk c < CH is K (key c/8, d 8*(c%8)), CH <= c < 2CH the same for V
+  const bf16* src[NC];
+  int dst[NC], skey[NC];
+  bool sok[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = tid + i * NT;
+    sok[i] = c < 2 * CH;
+    const int cc = sok[i] ? c : 0, which = cc / CH, kk = (cc % CH) / 8, d0 = (cc % 8) * 8;
+    skey[i] = kk;
+    src[i] = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + d0;
+    dst[i] = which * KB * KP + kk * KP + d0;
+  }
+  uint4 stg[NC];
+  auto gload = [&](int blk) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int key = min(blk * KB + skey[i], L - 1);
+      if (sok[i]) stg[i] = ld16(src[i] + (int64_t)key * p.ld);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+      if (sok[i]) st16(&smem[buf * BUF + dst[i]], stg[i]);
+  };
+
+  f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f;
+  s16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
+
+  const int nblk = (L + KB - 1) / KB;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int buf = blk & 1;
+    if (blk + 1 < nblk) gload(blk + 1);
+    const bf16* Ks = smem + buf * BUF;
+    const bf16* Vs = Ks + KB * KP;
+    const int k0 = blk * KB;
+    const bool tail = k0 + KB > L;                       // block-uniform
+    if (live) {
+      f32x4 st[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        if (!tail || k0 + kt * 16 < L) {
+          const int kr = kt * 16 + col;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]), qf[ks], a);
+        }
+        st[kt] = a;
+      }
+      if (tail) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
+      }
+      float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
+#pragma unroll
+      for (int kt = 1; kt < 4; ++kt)
+        lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+      if (__any((lm - m_run) * sl2 > THR)) {             // rare after the first block
+        const float m_new = fmaxf(m_run, xrow4_max(lm));
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
+        m_run = m_new;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] *= alpha;
+        osum *= alpha;
+      }
+      const float nb = -m_run * sl2;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (tail && k0 + 32 * u >= L) continue;          // P = 0 on all 32 keys
+        uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                              f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+        const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          // V^T fragment (d = 16 dt + col over keys 32u + 4g + r and + 16): transposed reads
+          const bf16* vr = &Vs[(32 * u + 4 * g + (col >> 2)) * KP + dt * 16 + 4 * (col & 3)];
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * KP));
+          o[dt] = mfma_bf16(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, pb, o[dt]);
+        }
+        osum = mfma_bf16(ones, pb, osum);
+      }
+    }
+    if (blk + 1 < nblk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  if (!q_ok) return;
+  const float inv = 1.f / osum[0];
+  bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
+    store4<bf16>(O + dt * 16 + 4 * g, v);
+  }
+}
+
+template <int NW>
+void launch_vit(const AttnP& p, hipStream_t st) {
+  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
+  hipLaunchKernelGGL((vit_attn_kernel<NW>), grid, dim3(NW * 64), 0, st, p);
+}
+
 template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
 void launch(const AttnP& p, hipStream_t st) {
   constexpr int QW = 16 * NW * QT;
@@ -316,6 +476,17 @@ void launch_dense(const AttnP& p, hipStream_t st) {
   // measured on the ViT-L/14 shape (tools/micro_attn.py): 8 waves x 16 queries per
   // workgroup, 64-key blocks: 35.3 us vs 40.3 for 4 waves x 2 query tiles (more waves in
   // flight hide the per-block softmax chain)
+  if constexpr (sizeof(T) == 2 && D == 64) {
+    // the ViT MHA kernel; 10 waves x 16 queries when that needs fewer query blocks than 8 x 16
+    // (L = 577: 4 blocks of 160, 512 workgroups, two per CU)
+    if (g_attn_variant == 0) {
+      if ((p.L + 159) / 160 < (p.L + 127) / 128) launch_vit<10>(p, st);
+      else launch_vit<8>(p, st);
+      return;
+    }
+    if (g_attn_variant == 8) { launch_vit<8>(p, st); return; }
+    if (g_attn_variant == 9) { launch_vit<4>(p, st); return; }
+  }
   switch (g_attn_variant) {
     case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;
     case 2: launch<T, D, 4, 128, 2, 0, false, false>(p, st); break;
@@ -323,6 +494,7 @@ void launch_dense(const AttnP& p, hipStream_t st) {
     case 4: launch<T, D, 8, 64, 2, 0, false, false>(p, st); break;
     case 5: launch<T, D, 10, 64, 1, 0, false, false>(p, st); break;
     case 6: launch<T, D, 8, 64, 1, 0, false, false>(p, st); break;
+    case 7:
     default:
       // 10 waves x 16 queries when that needs fewer query blocks than 8 x 16 (ViT L = 577:
       // 4 blocks of 160 vs 5 of 128 -> 512 workgroups, two per CU, no ragged third round):

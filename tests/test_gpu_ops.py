@@ -292,7 +292,8 @@ def test_layernorm_pipelined_rows(rows):
 
 # ----------------------------------------------------------------------------- attention
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("L_,H,causal", [(577, 4, False), (77, 2, True), (50, 3, False)])
+@pytest.mark.parametrize("L_,H,causal", [(577, 4, False), (77, 2, True), (50, 3, False), (64, 2, False),
+                                         (129, 2, False), (14, 12, True)])
 def test_attention_dense(dt, L_, H, causal):
     B, d = 2, 64
     qkv = rnd(B * L_, 3 * H * d, seed=18) * 2
@@ -308,7 +309,7 @@ def test_attention_dense(dt, L_, H, causal):
     close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8, 9])
 def test_attention_dense_tilings(variant):
     """Every A/B tiling of the dense path (tuning knob attn_variant) == the default tiling."""
     B, L_, H, d = 2, 577, 4, 64
@@ -325,6 +326,38 @@ def test_attention_dense_tilings(variant):
     finally:
         L.tune("attn_variant", 0)
     close(out, ref, atol=8e-3, what=f"attention tiling {variant}")
+
+
+@pytest.mark.parametrize("spike_key", [5, 300, 576])
+def test_attention_dense_defer_max_rescale(spike_key):
+    """The ViT kernel's defer-max branch (cdna_hip_programming.md rule 26): one key made to
+    dominate some queries' scores so the running max jumps by far more than the threshold in the
+    block holding it (block 0, a middle block, the 1-key tail block); every other query keeps
+    its ordinary scores.  Checked against fp64 over the full tensor, and the rescale threshold's
+    two extremes (always / first block only) must agree with the default to rounding."""
+    B, L_, H, d = 1, 577, 2, 64
+    qkv = rnd(B * L_, 3 * H * d, seed=23) * 2
+    k_cols = slice(H * d, 2 * H * d)
+    for qrow in (3, 200, 576):                        # k[spike] ~ 12 * q[qrow] for head 0 only
+        qkv[spike_key, H * d:H * d + d] += 12 * qkv[qrow, :d] / 3
+    q = qkv.to(dev, torch.bfloat16)
+    out = torch.empty(B * L_, H * d, device=dev, dtype=torch.bfloat16)
+    ops.attention(q[:, :H * d], q[:, k_cols], q[:, 2 * H * d:], out, n_seq=B, seq_len=L_, n_heads=H,
+                  head_dim=d, scale=d ** -0.5)
+    x = qkv.to(torch.bfloat16).double().reshape(B, L_, 3, H, d).permute(2, 0, 3, 1, 4)
+    s = (x[0] @ x[1].transpose(-1, -2)) * d ** -0.5
+    if spike_key >= 64:                               # the jump the branch must handle
+        assert s[0, 0].max(-1).values.max() - s[0, 0, :, :64].max() > 30
+    ref = (torch.softmax(s, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B * L_, H * d)
+    close(out, ref, atol=1.5e-2, what=f"attn defer-max spike at key {spike_key}")
+    alt = torch.empty_like(out)
+    try:
+        L.tune("attn_variant", 7)                     # the exact-max kernel (rescales every block)
+        ops.attention(q[:, :H * d], q[:, k_cols], q[:, 2 * H * d:], alt, n_seq=B, seq_len=L_, n_heads=H,
+                      head_dim=d, scale=d ** -0.5)
+    finally:
+        L.tune("attn_variant", 0)
+    close(out, alt, atol=8e-3, what="defer-max vs exact-max kernel")
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
