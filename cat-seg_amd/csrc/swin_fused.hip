@@ -452,11 +452,14 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
   }
 }
 
-int g_swin_variant = 0;   // 0 = pipelined (swin_fused2_kernel), 1 = two barriers per head (swin_fused_kernel)
+int g_swin_variant = 0;   // 0 = head-per-SIMD (swin_window.hip), 2 = pipelined row-tile waves (swin_fused2_kernel),
+                          // 1 = two barriers per head (swin_fused_kernel)
 
 }  // namespace
 
 CATSEG_KNOB(g_swin_variant, "swin_variant");
+
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st);   // swin_window.hip
 
 extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->x && a->ln_g && a->ln_b && a->w_qkv && a->b_qkv && a->gqk && a->out,
@@ -485,7 +488,9 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   }
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (g_swin_variant == 1) {
+  if (g_swin_variant == 0) {
+    swin_win3_launch(a, n_cu, (hipStream_t)stream);
+  } else if (g_swin_variant == 1) {
     if (a->shift > 0)
       hipLaunchKernelGGL(swin_fused_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);
     else

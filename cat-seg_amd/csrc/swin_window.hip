@@ -1,0 +1,303 @@
+// Swin window attention, head-per-SIMD form (bf16) -- the default kernel behind
+// catseg_swin_window_attention (swin_fused.hip holds the argument checks and the older forms).
+// Reference: SwinTransformerBlock.forward model.py:191-199 (norm1, concat guidance, roll,
+// window_partition) and WindowAttention.forward model.py:86-114 up to the output projection;
+// the -100 region mask of model.py:161-183.
+//
+// A window is 144 tokens = 9 row tiles of 16.  With one wave per row tile (swin_fused2_kernel)
+// the 9 waves sit 3 / 2 / 2 / 2 on the CU's four SIMDs and the 3-wave SIMD paces every window.
+// Here the work is cut by HEAD instead: 8 waves, wave w computes head h = w % 4 (waves w and
+// w + 4 share a SIMD -- a workgroup's waves are dealt to the SIMDs cyclically), so every SIMD
+// does exactly one head's q/k/v projection and attention for all 144 tokens.
+//
+// Per window (persistent workgroup per CU, windows strided by the grid):
+//   P1  LayerNorm(norm1) of the 144 rows in place in Xn (bf16, chunk-major XOR-swizzled), 16
+//       lanes per row.  The raw rows were brought in by LDS-DMA during the previous window's P3.
+//   --  barrier
+//   P2  wave (h, sub) projects row tiles sub, sub + 2, ... of head h against W_q / W_k of the head
+//       held in REGISTERS (64 x 128 rows as MFMA fragments, loaded once) and W_v from LDS:
+//         q^T = W_q Xn^T + b + guidance   -> registers (already the B operand of S^T = K Q^T)
+//         k^T = W_k Xn^T + b + guidance   -> LDS K_h [key][32] (same permuted d order as q)
+//         v   = Xn W_v^T + b              -> LDS V_h^T [d][key] (operands swapped: 4 keys per lane)
+//       (the region one-hot of the shifted windows is written here too)
+//   --  barrier
+//   P3  the same row tiles as queries: S^T = K Q^T (+ the -100 region mask as a second MFMA on
+//       one-hot key dims, skipped for the window location with a single region), softmax over
+//       the 144 keys of the window in registers, O^T = V^T P^T and the row sums on the MFMA,
+//       8-byte stores of the head's 32 output channels.  The next window's rows are requested
+//       (LDS-DMA into Xn, free once P2 is done everywhere).
+//   --  vmcnt(0) + barrier (the DMA is visible; every wave is past P3)
+// HBM traffic per window: the 144 input rows, the 144 output rows, the guidance rows (shared by
+// every class of an image: L2-resident).
+#include "common.h"
+#include "capi.h"
+
+namespace {
+
+constexpr int IMG = 24, WS = 12, NWIN = 4, L = WS * WS;    // 144 tokens per window
+constexpr int C = 128, D = 32, NH = 4;
+constexpr int NW = 8, NT = NW * 64;
+constexpr int NTILE = L / 16;                              // 9 row tiles
+constexpr int MYT = (NTILE + 1) / 2;                       // row tiles of a wave (5 / 4)
+constexpr int KBV = 160;                                   // keys of V^T (5 x 32-key MFMA steps)
+constexpr int VP = KBV + 4;                                // V^T row stride (elements)
+constexpr int LNS = (L + 4 * NW - 1) / (4 * NW);           // LayerNorm steps (4 rows per wave each)
+
+struct Swin3P {
+  const bf16* x; int64_t ld_x;
+  const float* ln_g; const float* ln_b; float eps;
+  const bf16* w; const float* bias;
+  const bf16* g; int64_t ld_g; RowMap gmap;
+  bf16* out; int64_t ld_out;
+  int shift; float scale;
+};
+
+// 16-byte chunk c of row r of a chunk-major image with ROWS rows, row XOR swizzle in the low 4 bits
+template <int ROWS>
+DEV int cs(int c, int r) { return (c * ROWS + (r ^ (c & 15))) * 8; }
+
+DEV int win_row3(int slice, int wloc, int i, int shift) {     // roll(-shift) + window_partition
+  const int Y = (wloc >> 1) * WS + i / WS, X = (wloc & 1) * WS + i % WS;
+  const int y = Y + shift < IMG ? Y + shift : Y + shift - IMG;
+  const int x = X + shift < IMG ? X + shift : X + shift - IMG;
+  return slice * IMG * IMG + y * IMG + x;
+}
+
+DEV int region3(int wloc, int i, int shift) {                  // model.py:161-176 label
+  const int Y = (wloc >> 1) * WS + i / WS, X = (wloc & 1) * WS + i % WS;
+  const int hb = Y < IMG - WS ? 0 : (Y < IMG - shift ? 1 : 2);
+  const int wb = X < IMG - WS ? 0 : (X < IMG - shift ? 1 : 2);
+  return hb * 3 + wb;
+}
+
+DEV s16x8 pk8(const f32x4& a, const f32x4& b) {
+  return __builtin_bit_cast(s16x8, make_uint4(f2bf2(a[0], a[1]), f2bf2(a[2], a[3]), f2bf2(b[0], b[1]), f2bf2(b[2], b[3])));
+}
+DEV f32x4 unpack4(uint2 u) {
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+
+template <bool SWM>
+__global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total) {
+  __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
+  __shared__ __attribute__((aligned(16))) bf16 Ks[NH][4 * L * 8];       // [head][chunk][key] (chunk-major)
+  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? 4 * L * 8 : 8]; // region one-hot of the keys
+  __shared__ __attribute__((aligned(16))) bf16 Vt[NH][D * VP];          // [head][d][key]
+  __shared__ __attribute__((aligned(16))) bf16 sWv[C * C];              // W_v (every head), chunk-major
+  __shared__ __attribute__((aligned(16))) float sP[2 * C + 3 * C];      // LN gamma | beta | qkv bias
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = wave & 3, sub = wave >> 2;
+  const int r16 = lane & 15, g = lane >> 4;
+  for (int i = tid; i < 5 * C; i += NT) sP[i] = i < C ? p.ln_g[i] : i < 2 * C ? p.ln_b[i - C] : p.bias[i - 2 * C];
+  for (int i = tid; i < NH * D * (KBV - L); i += NT) {       // V^T key columns 144..159 stay zero
+    const int hh = i / (D * (KBV - L)), j = i % (D * (KBV - L));
+    Vt[hh][(j / (KBV - L)) * VP + L + j % (KBV - L)] = 0;
+  }
+  for (int c = tid; c < C * 16; c += NT) {                  // W_v rows -> LDS (read as B fragments)
+    const int lr = c >> 4, ch = c & 15;
+    st16(&sWv[cs<C>(ch, lr)], ld16(p.w + (int64_t)(2 * C + lr) * C + ch * 8));
+  }
+  // head h's q / k weight rows as MFMA fragments: wf[part][dt][ks] = W[part*C + h*D + 16dt + r16][32ks + 8g ..]
+  s16x8 wf[2][2][4];
+#pragma unroll
+  for (int part = 0; part < 2; ++part)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        wf[part][dt][ks] = __builtin_bit_cast(
+            s16x8, ld16(p.w + (int64_t)(part * C + h * D + dt * 16 + r16) * C + ks * 32 + 8 * g));
+  __syncthreads();
+  s16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  // LayerNorm rows: step s, row s*32 + 4*wave + (lane >> 4), 16-byte chunk lane & 15
+  const int lc = lane & 15, lrow0 = 4 * wave + (lane >> 4);
+  // raw rows of a window -> Xn by LDS-DMA (no VGPRs held across the attention phase): the image
+  // is lane-linear per wave-instruction, so slot s (16 bytes) of the chunk-major swizzled Xn
+  // receives chunk c = s / L of token row (s % L) ^ (c & 15), and the LayerNorm then runs in place
+  constexpr int NDMA = L * 16 / 64;                       // 36 wave-instructions per window
+  auto fetch = [&](int win) {
+    const int slice = win / NWIN, wloc = win % NWIN;
+    for (int k = wave; k < NDMA; k += NW) {
+      const int sl = k * 64 + lane, c = sl / L, i = (sl % L) ^ (c & 15);
+      const bf16* src = p.x + (int64_t)win_row3(slice, wloc, i, p.shift) * p.ld_x + c * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Xn + k * 64 * 8), 16, 0, 0);
+    }
+  };
+  int win = blockIdx.x;
+  if (win < nwin_total) fetch(win);
+  for (; win < nwin_total; win += gridDim.x) {
+    const int slice = win / NWIN, wloc = win % NWIN;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's DMA (and stores) landed
+    __syncthreads();                                       // every wave's DMA visible; P3 done
+    // ---------------- P1: LayerNorm of Xn in place ----------------
+    {
+      const float4 g0 = *reinterpret_cast<const float4*>(&sP[lc * 8]), g1 = *reinterpret_cast<const float4*>(&sP[lc * 8 + 4]);
+      const float4 b0 = *reinterpret_cast<const float4*>(&sP[C + lc * 8]), b1 = *reinterpret_cast<const float4*>(&sP[C + lc * 8 + 4]);
+      const float lg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float lb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int s = 0; s < LNS; ++s) {
+        const int i = min(s * 32 + lrow0, L - 1);
+        const uint4 raw = *reinterpret_cast<const uint4*>(&Xn[cs<L>(lc, i)]);
+        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+        float v[8], sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[j] = bf2f(e[j]); sum += v[j]; }
+        sum = row16_sum(sum);
+        const float mean = sum * (1.f / C);
+        float qs = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[j] -= mean; qs += v[j] * v[j]; }
+        qs = row16_sum(qs);
+        const float rstd = __builtin_amdgcn_rsqf(qs * (1.f / C) + p.eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] * rstd * lg[j] + lb[j];
+        if (s * 32 + 4 * NW <= L || s * 32 + lrow0 < L)
+          st16(&Xn[cs<L>(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
+      }
+    }
+    __syncthreads();
+    // ---------------- P2: q / k / v of head h for row tiles sub, sub + 2, ... ----------------
+    if constexpr (SWM) {   // region one-hot of the keys (P3 of the previous window has retired its reads)
+      if (gridDim.x % NWIN != 0 || win == (int)blockIdx.x) {
+        for (int key = tid; key < L; key += NT) {
+          const int reg = region3(wloc, key, p.shift);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            unsigned w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int e0 = c * 8 + 2 * j;
+              w4[j] = (e0 == reg ? 0x3F80u : 0u) | (e0 + 1 == reg ? 0x3F800000u : 0u);
+            }
+            st16(&Oh[(c * L + key) * 8], make_uint4(w4[0], w4[1], w4[2], w4[3]));
+          }
+        }
+      }
+    }
+    s16x8 qf[MYT];
+#pragma unroll
+    for (int j = 0; j < MYT; ++j) {
+      const int t = sub + 2 * j;
+      if (t < NTILE) {
+        const int rb = 16 * t;
+        s16x8 xb[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(( (ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
+        const int grow = (int)rowmap(p.gmap, win_row3(slice, wloc, rb + r16, p.shift));
+        const bf16* gp = p.g + (int64_t)grow * p.ld_g + h * D + 4 * g;
+        f32x4 dq[2], dk[2], dv[2];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          // accumulators start at bias + guidance (q, k: features 16dt + 4g + r of token r16) / bias (v)
+          dq[dt] = *reinterpret_cast<const f32x4*>(&sP[2 * C + h * D + dt * 16 + 4 * g]) +
+                   unpack4(*reinterpret_cast<const uint2*>(gp + dt * 16));
+          dk[dt] = *reinterpret_cast<const f32x4*>(&sP[3 * C + h * D + dt * 16 + 4 * g]) +
+                   unpack4(*reinterpret_cast<const uint2*>(gp + C + dt * 16));
+          const float bvv = sP[4 * C + h * D + dt * 16 + r16];
+          dv[dt] = f32x4{bvv, bvv, bvv, bvv};
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            dq[dt] = mfma_bf16(wf[0][dt][ks], xb[ks], dq[dt]);
+            dk[dt] = mfma_bf16(wf[1][dt][ks], xb[ks], dk[dt]);
+            dv[dt] = mfma_bf16(xb[ks], *reinterpret_cast<const s16x8*>(&sWv[cs<C>(ks * 4 + g, h * D + dt * 16 + r16)]),
+                               dv[dt]);                   // D[token 4g + r][feature 16dt + r16]
+          }
+        qf[j] = pk8(dq[0], dq[1]);              // q features {4g..4g+3, 16+4g..16+4g+3} of token r16
+        st16(&Ks[h][(g * L + rb + r16) * 8], __builtin_bit_cast(uint4, pk8(dk[0], dk[1])));
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          *reinterpret_cast<uint2*>(&Vt[h][(dt * 16 + r16) * VP + rb + 4 * g]) =
+              make_uint2(f2bf2(dv[dt][0], dv[dt][1]), f2bf2(dv[dt][2], dv[dt][3]));
+      }
+      __builtin_amdgcn_sched_barrier(0);        // no cross-tile hoisting (register pressure)
+    }
+    __syncthreads();
+    // ---------------- P3: attention of head h for the same row tiles ----------------
+    if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);   // Xn is free: P2 is done everywhere
+    const bool masked = SWM && wloc != 0;       // window location 0 holds a single region
+#pragma unroll
+    for (int j = 0; j < MYT; ++j) {
+      const int t = sub + 2 * j;
+      if (t >= NTILE) break;
+      const int rb = 16 * t;
+      s16x8 qmask;
+      if (masked) {
+        const int qreg = region3(wloc, rb + r16, p.shift);
+        const short neg = (short)f2bf(-100.f / p.scale);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int dim = 8 * g + e;
+          qmask[e] = dim < 9 && dim != qreg ? neg : (short)0;
+        }
+      }
+      f32x4 st[NTILE + 1];
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt) {
+        f32x4 a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[h][(g * L + kt * 16 + r16) * 8]), qf[j],
+                            f32x4{0.f, 0.f, 0.f, 0.f});
+        if (masked) a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Oh[(g * L + kt * 16 + r16) * 8]), qmask, a);
+        st[kt] = a;
+      }
+      float mx = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
+#pragma unroll
+      for (int kt = 1; kt < NTILE; ++kt) mx = fmaxf(mx, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+      mx = xrow4_max(mx);
+      const float nb = -mx * sl2;
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+      st[NTILE] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < KBV / 32; ++u) {
+        const s16x8 pb = pk8(st[2 * u], st[2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16* vr = &Vt[h][(dt * 16 + r16) * VP + 32 * u + 4 * g];
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          o[dt] = mfma_bf16(__builtin_bit_cast(s16x8, make_uint4(lo.x, lo.y, hi.x, hi.y)), pb, o[dt]);
+        }
+        osum = mfma_bf16(ones, pb, osum);
+      }
+      const float inv = 1.f / osum[0];
+      bf16* O = p.out + (int64_t)win_row3(slice, wloc, rb + r16, p.shift) * p.ld_out + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
+            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+}  // namespace
+
+// launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st) {
+  Swin3P p;
+  p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
+  p.ln_g = a->ln_g; p.ln_b = a->ln_b; p.eps = a->eps;
+  p.w = (const bf16*)a->w_qkv; p.bias = a->b_qkv;
+  p.g = (const bf16*)a->gqk; p.ld_g = a->ld_g;
+  p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
+  p.out = (bf16*)a->out; p.ld_out = a->ld_out;
+  p.shift = a->shift; p.scale = a->scale;
+  const int nwin_total = (int)(a->S * NWIN);
+  const dim3 grid((unsigned)std::min(nwin_total, n_cu));
+  if (a->shift > 0) hipLaunchKernelGGL(swin_win3_kernel<true>, grid, dim3(NT), 0, st, p, nwin_total);
+  else hipLaunchKernelGGL(swin_win3_kernel<false>, grid, dim3(NT), 0, st, p, nwin_total);
+  return 0;
+}

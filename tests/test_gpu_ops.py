@@ -912,11 +912,14 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
     close(out, ref, atol=1e-6, what="resize")
 
 
-@pytest.mark.parametrize("shift", [0, 6])
-def test_swin_window_attention_fused_vs_unfused(shift):
+@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("shift", [0, 6, 3])
+def test_swin_window_attention_fused_vs_unfused(shift, variant):
     """catseg_swin_window_attention == catseg_rows_gemm(LN1 + q/k/v + guidance) followed by
-    catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry."""
-    B, T, HW, D = 2, 3, 576, 128
+    catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry.
+    variant 0 = the head-per-SIMD kernel (default, swin_window.hip), 2 = the row-tile-wave kernel;
+    S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
+    B, T, HW, D = 1, 7, 576, 128
     S = B * T
     R = S * HW
     dt = torch.bfloat16
@@ -932,8 +935,12 @@ def test_swin_window_attention_fused_vs_unfused(shift):
     ops.attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], ref, n_seq=S * 4, seq_len=144, n_heads=4,
                   head_dim=32, scale=32 ** -0.5, mode=1, img_hw=(24, 24), window=12, shift=shift)
     out = torch.empty(R, D, device=dev, dtype=dt)
-    ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, out, S=S, img_hw=(24, 24), window=12, shift=shift,
-                              n_heads=4, head_dim=32, scale=32 ** -0.5)
+    try:
+        L.tune("swin_variant", variant)
+        ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, out, S=S, img_hw=(24, 24), window=12, shift=shift,
+                                  n_heads=4, head_dim=32, scale=32 ** -0.5)
+    finally:
+        L.tune("swin_variant", 0)
     err = (out.float() - ref.float()).abs()
     # both are bf16 pipelines over the same math (q/k/v rounded to bf16 in both): equal to bf16 noise
     assert err.max().item() < 3e-2 and err.mean().item() < 2e-3, (err.max().item(), err.mean().item())
