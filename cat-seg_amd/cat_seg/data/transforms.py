@@ -147,7 +147,10 @@ class RandomCropCategoryArea:
         h, w = image.shape[:2]
         if self.max_area >= 1.0 or sem_seg is None:
             ch, cw = self.crop_size_for(h, w)
-            return CropTransform(np.random.randint(w - cw + 1), np.random.randint(h - ch + 1), cw, ch)
+            # detectron2 RandomCrop.get_transform draws h0 first, then w0
+            y0 = np.random.randint(h - ch + 1)
+            x0 = np.random.randint(w - cw + 1)
+            return CropTransform(x0, y0, cw, ch)
         for _ in range(10):
             ch, cw = self.crop_size_for(h, w)
             y0, x0 = np.random.randint(h - ch + 1), np.random.randint(w - cw + 1)

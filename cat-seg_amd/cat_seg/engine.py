@@ -538,7 +538,8 @@ class CatSegEngine:
         fused_swin = (self.fused_swin and dt == torch.bfloat16 and (H_, W_, ws) == (24, 24, 12)
                       and a.nheads == 4 and D == 128)
         gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)     # (b, t, p) -> (b, p)
-        fused_class = self.fused_class and dt == torch.bfloat16 and a.nheads == 4 and D == 128
+        # the fused class attention holds one pixel's T <= 256 class rows on chip (pad_len bounds T)
+        fused_class = self.fused_class and dt == torch.bfloat16 and a.nheads == 4 and D == 128 and T <= 256
         n_pad = a.pad_len - T if a.pad_len > 0 and T < a.pad_len else 0
         for l, lay in enumerate(w.layers):
             ops.layernorm(G3, lay.gnw, lay.gnb, gn)           # guidance_norm, once per image

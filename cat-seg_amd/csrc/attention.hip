@@ -335,8 +335,10 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
       qf[ks] = *reinterpret_cast<s16x8*>(&u);
     }
   }
-  // staging: chunk c < CH is K (key c/8, d 8*(c%8)), CH <= c < 2CH the same for V
+  // staging: chunk c < CH is K (key c/8, d 8*(c%8)), CH <= c < 2CH the same for V.  The source
+  // pointer advances by one block of rows per block; rows past L re-read row L-1 (no branch)
   const bf16* src[NC];
+  const bf16* last[NC];
   int dst[NC], skey[NC];
   bool sok[NC];
 #pragma unroll
@@ -345,21 +347,22 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
     sok[i] = c < 2 * CH;
     const int cc = sok[i] ? c : 0, which = cc / CH, kk = (cc % CH) / 8, d0 = (cc % 8) * 8;
     skey[i] = kk;
-    src[i] = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + d0;
-    dst[i] = which * KB * KP + kk * KP + d0;
+    const bf16* base = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + d0;
+    src[i] = base + (int64_t)kk * p.ld;
+    last[i] = base + (int64_t)(L - 1) * p.ld;
+    dst[i] = (which * KB * KP + kk * KP + d0) * 2;      // bytes
   }
+  const int64_t bstep = (int64_t)KB * p.ld;
   uint4 stg[NC];
   auto gload = [&](int blk) {
 #pragma unroll
-    for (int i = 0; i < NC; ++i) {
-      const int key = min(blk * KB + skey[i], L - 1);
-      if (sok[i]) stg[i] = ld16(src[i] + (int64_t)key * p.ld);
-    }
+    for (int i = 0; i < NC; ++i)
+      if (sok[i]) stg[i] = ld16(blk * KB + skey[i] < L ? src[i] + blk * bstep : last[i]);
   };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NC; ++i)
-      if (sok[i]) st16(&smem[buf * BUF + dst[i]], stg[i]);
+      if (sok[i]) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(smem) + buf * BUF * 2 + dst[i]) = stg[i];
   };
 
   f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
@@ -369,71 +372,80 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
   s16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
+  // per-lane LDS bases: K fragment row col / chunk g, V^T transposed-read row 4g + col/4
+  const int kbase = (col * KP + 8 * g) * 2;
+  const int vbase = (KB * KP + (4 * g + (col >> 2)) * KP + 4 * (col & 3)) * 2;
+
+  // one 64-key block from LDS buffer `buf`; TAIL: keys k0 .. k0 + 63 may pass L (masked)
+  auto block = [&](int blk, int buf, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    const char* Kb = reinterpret_cast<const char*>(smem) + buf * BUF * 2 + kbase;
+    const char* Vb = reinterpret_cast<const char*>(smem) + buf * BUF * 2 + vbase;
+    const int k0 = blk * KB;
+    f32x4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      if (!TAIL || k0 + kt * 16 < L) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          a = mfma_bf16(*reinterpret_cast<const s16x8*>(Kb + (kt * 16 * KP + ks * 32) * 2), qf[ks], a);
+      }
+      st[kt] = a;
+    }
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
+    }
+    float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
+#pragma unroll
+    for (int kt = 1; kt < 4; ++kt)
+      lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+    if (__any((lm - m_run) * sl2 > THR)) {               // rare after the first block
+      const float m_new = fmaxf(m_run, xrow4_max(lm));
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] *= alpha;
+      osum *= alpha;
+    }
+    const float nb = -m_run * sl2;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (TAIL && k0 + 32 * u >= L) continue;            // P = 0 on all 32 keys
+      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        // V^T fragment (d = 16 dt + col over keys 32u + 4g + r and + 16): transposed reads
+        const char* vr = Vb + (32 * u * KP + dt * 16) * 2;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * KP * 2));
+        o[dt] = mfma_bf16(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, pb, o[dt]);
+      }
+      osum = mfma_bf16(ones, pb, osum);
+    }
+  };
 
   const int nblk = (L + KB - 1) / KB;
+  const int nfull = L / KB;                              // blocks with every key < L
   gload(0);
   sstore(0);
   __syncthreads();
   for (int blk = 0; blk < nblk; ++blk) {
     const int buf = blk & 1;
     if (blk + 1 < nblk) gload(blk + 1);
-    const bf16* Ks = smem + buf * BUF;
-    const bf16* Vs = Ks + KB * KP;
-    const int k0 = blk * KB;
-    const bool tail = k0 + KB > L;                       // block-uniform
     if (live) {
-      f32x4 st[4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f};
-        if (!tail || k0 + kt * 16 < L) {
-          const int kr = kt * 16 + col;
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[kr * KP + ks * 32 + 8 * g]), qf[ks], a);
-        }
-        st[kt] = a;
-      }
-      if (tail) {
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
-      }
-      float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
-#pragma unroll
-      for (int kt = 1; kt < 4; ++kt)
-        lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
-      if (__any((lm - m_run) * sl2 > THR)) {             // rare after the first block
-        const float m_new = fmaxf(m_run, xrow4_max(lm));
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
-        m_run = m_new;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] *= alpha;
-        osum *= alpha;
-      }
-      const float nb = -m_run * sl2;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (tail && k0 + 32 * u >= L) continue;          // P = 0 on all 32 keys
-        uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
-                              f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
-        const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          // V^T fragment (d = 16 dt + col over keys 32u + 4g + r and + 16): transposed reads
-          const bf16* vr = &Vs[(32 * u + 4 * g + (col >> 2)) * KP + dt * 16 + 4 * (col & 3)];
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * KP));
-          o[dt] = mfma_bf16(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, pb, o[dt]);
-        }
-        osum = mfma_bf16(ones, pb, osum);
-      }
+      if (blk < nfull) block(blk, buf, std::false_type{});
+      else block(blk, buf, std::true_type{});
     }
     if (blk + 1 < nblk) sstore(buf ^ 1);
     __syncthreads();

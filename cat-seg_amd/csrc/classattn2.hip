@@ -1,6 +1,5 @@
 // Class attention, register-resident form (bf16): one pixel per 4-wave workgroup at a time,
-// one wave per head, two workgroups per CU.  Same contract as classattn_fused.hip
-// (catseg_class_attention): norm1 + [q|k|v] projection (+ the per-class text-guidance half
+// one wave per head, two workgroups per CU (catseg_class_attention): norm1 + [q|k|v] projection (+ the per-class text-guidance half
 // of q, k) + linear attention over the T classes of a pixel + the attention residual.
 // Reference: ClassTransformerLayer.forward model.py:387-413, AttentionLayer.forward
 // model.py:338-354, LinearAttention.forward model.py:256-286 (phi = elu + 1, V / S, KV, Z, * S).
@@ -328,12 +327,21 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 
 }  // namespace
 
-int g_classattn_variant = 0;   // 0 = register-resident kernel (this file), 1 = classattn_fused.hip
+int g_classattn_variant = 0;   // 2 = 16 LayerNorm row steps per batch (A/B); >= 16: diagnostics (dbg = v - 16)
 CATSEG_KNOB(g_classattn_variant, "classattn_variant");
 
-// launched by catseg_class_attention (classattn_fused.hip) after its argument checks
-int classattn2_launch(const CatsegClassAttnArgs* a, hipStream_t st) {
-  if ((g_classattn_variant == 1 || (g_classattn_variant > 2 && g_classattn_variant < 16)) || a->T > TMAX || !a->tgk_t) return 1;
+extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->x && a->w_qkv && a->b_qkv && a->ln_g && a->ln_b && a->tg && a->y && a->tgk_t,
+               "class_attention: null pointer");
+  CATSEG_CHECK(a->dtype == CATSEG_BF16, "class_attention: bf16 only");
+  CATSEG_CHECK(a->n_heads == NH && a->head_dim == D, "class_attention: needs 4 heads x 32");
+  CATSEG_CHECK(a->B > 0 && a->T > 0 && a->HW > 0, "class_attention: empty shape");
+  CATSEG_CHECK(a->T <= TMAX, "class_attention: T must be <= 256 (the class padding length)");
+  CATSEG_CHECK(a->n_pad >= 0 && (a->n_pad == 0 || (a->k_pad && a->v_pad)), "class_attention: padding projections missing");
+  CATSEG_CHECK(a->ld_x % 8 == 0 && a->ld_y % 8 == 0 && a->ld_tg % 8 == 0 && a->ld_x >= C && a->ld_y >= C &&
+               a->ld_tg >= 2 * C, "class_attention: row strides must be multiples of 8 elements");
+  CATSEG_CHECK(a->tg_bstride >= 0, "class_attention: bad guidance image stride");
+  CATSEG_CHECK(a->x != a->y, "class_attention: y must not alias x");
   CATSEG_CHECK(a->B * a->T * (int64_t)a->HW * std::max(a->ld_x, a->ld_y) < (1LL << 31) &&
                (int64_t)a->T * a->ld_tg < (1LL << 31), "class_attention: element offsets must fit 31 bits");
   CATSEG_CHECK(a->ld_tgk_t >= (a->T + 15) / 16 * 16 && a->ld_tgk_t % 4 == 0 && ((uintptr_t)a->tgk_t % 8) == 0,
@@ -357,7 +365,8 @@ int classattn2_launch(const CatsegClassAttnArgs* a, hipStream_t st) {
   }
   const int64_t npix = a->B * a->HW;
   const unsigned grid = (unsigned)std::min<int64_t>(npix, 2LL * cus);
+  hipStream_t st = (hipStream_t)stream;
   if (g_classattn_variant == 2) hipLaunchKernelGGL(classattn2_kernel<16>, dim3(grid), dim3(NT), 0, st, p);
   else hipLaunchKernelGGL(classattn2_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
-  return 0;
+  return catseg_launch_status("class_attention");
 }

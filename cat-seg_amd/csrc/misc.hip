@@ -586,25 +586,26 @@ __global__ __launch_bounds__(256) void post_band_kernel(const float* lg, int h, 
   }
 }
 
-// The same band with a compile-time output width WC (336 / 384: the CAT-Seg eval outputs):
-// thread t owns the 4-column group (t mod WC/4) for rows t / (WC/4), +G, ... of the band, so the
-// column taps (lin_idx of x, the LDS column offsets, lx) are derived once per thread instead of
-// once per store, and no integer division is left in the store loop.  Same taps, same fma order
-// as post_band_kernel: bit-identical.
-template <bool SIG, int WC>
-__global__ __launch_bounds__(256) void post_band_col_kernel(const float* lg, int h, int w, int ch, int cw, float* out,
-                                                            int H) {
-  constexpr int W4 = WC / 4, G = 256 / W4;
-  static_assert(WC % 4 == 0 && G >= 1, "output width");
-  extern __shared__ float sgm[];
+// Separable band kernel (default for W % 4 == 0): the band's source rows are sigmoid'ed into LDS,
+// then interpolated HORIZONTALLY once per source row into full output-width rows (LDS, float4
+// writes), and every output row is one vertical lerp of two of them: 2 conflict-free 16-byte LDS
+// reads + 4 fma pairs per 16-byte store (post_band_kernel: 16 scalar reads with bank conflicts per
+// store).  The horizontal value is exactly post_band_kernel's `top` / `bot` (same taps, same fma),
+// and the vertical step its last fma: bit-identical.
+template <bool SIG>
+__global__ __launch_bounds__(256) void post_sep_kernel(const float* lg, int h, int w, int ch, int cw, float* out,
+                                                        int H, int W) {
+  extern __shared__ float smem[];          // [nrows][cw] sigmoid | [nrows][W] horizontal rows
   const int64_t pl = blockIdx.y;
   const int oy0 = blockIdx.x * POST_ROWS, oy1 = min(H, oy0 + POST_ROWS);
-  const float sy = (float)ch / (float)H, sx = (float)cw / (float)WC;
+  const float sy = (float)ch / (float)H, sx = (float)cw / (float)W;
   int ya, yb, yt;
   float lt;
   lin_idx(oy0, ch, sy, ya, yt, lt);
   lin_idx(oy1 - 1, ch, sy, yt, yb, lt);
   const int nrows = yb - ya + 1;
+  float* sgm = smem;
+  float* hr = smem + ((nrows * cw + 3) & ~3);
   const float* src = lg + pl * (int64_t)h * w;
   for (int i = threadIdx.x; i < nrows * cw; i += 256) {
     const int r = i / cw, c = i - r * cw;
@@ -612,29 +613,32 @@ __global__ __launch_bounds__(256) void post_band_col_kernel(const float* lg, int
     sgm[i] = SIG ? 1.f / (1.f + __expf(-v)) : v;
   }
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t >= G * W4) return;                 // no barrier below
-  const int x4 = (t % W4) * 4;
-  int x0[4], x1[4];
-  float lx[4];
+  const int W4 = W >> 2;
+  for (int i = threadIdx.x; i < nrows * W4; i += 256) {
+    const int r = i / W4, x4 = (i - r * W4) * 4;
+    const float* rs = sgm + r * cw;
+    float v[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) lin_idx(x4 + k, cw, sx, x0[k], x1[k], lx[k]);
-  float* o = out + pl * (int64_t)H * WC + x4;
-  for (int ry = t / W4; ry < oy1 - oy0; ry += G) {
+    for (int k = 0; k < 4; ++k) {
+      int x0, x1;
+      float lx;
+      lin_idx(x4 + k, cw, sx, x0, x1, lx);
+      v[k] = fmaf(lx, rs[x1] - rs[x0], rs[x0]);
+    }
+    *reinterpret_cast<float4*>(hr + r * W + x4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  float* o = out + pl * (int64_t)H * W;
+  for (int idx = threadIdx.x; idx < (oy1 - oy0) * W4; idx += 256) {
+    const int ry = idx / W4, x4 = (idx - ry * W4) * 4;
     const int y = oy0 + ry;
     int y0, y1;
     float ly;
     lin_idx(y, ch, sy, y0, y1, ly);
-    const float* r0 = sgm + (y0 - ya) * cw;
-    const float* r1 = sgm + (y1 - ya) * cw;
-    float v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float top = fmaf(lx[k], r0[x1[k]] - r0[x0[k]], r0[x0[k]]);
-      const float bot = fmaf(lx[k], r1[x1[k]] - r1[x0[k]], r1[x0[k]]);
-      v[k] = fmaf(ly, bot - top, top);
-    }
-    *reinterpret_cast<float4*>(o + (int64_t)y * WC) = make_float4(v[0], v[1], v[2], v[3]);
+    const float4 t = *reinterpret_cast<const float4*>(hr + (y0 - ya) * W + x4);
+    const float4 b = *reinterpret_cast<const float4*>(hr + (y1 - ya) * W + x4);
+    *reinterpret_cast<float4*>(o + (int64_t)y * W + x4) =
+        make_float4(fmaf(ly, b.x - t.x, t.x), fmaf(ly, b.y - t.y, t.y), fmaf(ly, b.z - t.z, t.z), fmaf(ly, b.w - t.w, t.w));
   }
 }
 
@@ -802,31 +806,25 @@ extern "C" int catseg_bicubic_resize(const float* in, int S_in, int D, float* ou
 }
 
 namespace {
-int g_post_variant = 0;   // 0 = compile-time-width band kernel at W = 336 / 384, 1 = runtime-width band kernel (A/B)
+int g_post_variant = 0;   // 0 = separable band kernel, 1 = the direct band kernel (A/B; bit-identical)
 template <bool SIG>
 int launch_post(const char* what, const float* logits, int64_t B, int T, int h, int w, int crop_h, int crop_w,
                 float* out, int H, int W, void* stream) {
   CATSEG_CHECK(logits && out && B > 0 && T > 0 && H > 0 && W > 0, "postprocess/resize: bad args");
   CATSEG_CHECK(crop_h > 0 && crop_h <= h && crop_w > 0 && crop_w <= w, "postprocess/resize: bad crop");
   const int64_t total = B * T * (int64_t)H * W;
-  // banded kernel: source rows of one band (<= POST_ROWS * ch / H + 2) fit LDS
+  // banded kernels: source rows of one band (<= POST_ROWS * ch / H + 2) fit LDS
   const int64_t band_src_rows = (int64_t)POST_ROWS * crop_h / H + 3;
+  const dim3 grid((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T));
+  const int64_t sep_bytes = (((band_src_rows * crop_w + 3) & ~3LL) + band_src_rows * W) * 4;
+  if (W % 4 == 0 && g_post_variant == 0 && sep_bytes <= 64 * 1024) {
+    hipLaunchKernelGGL(post_sep_kernel<SIG>, grid, dim3(256), (size_t)sep_bytes, (hipStream_t)stream, logits, h, w,
+                       crop_h, crop_w, out, H, W);
+    return catseg_launch_status(what);
+  }
   if (W % 4 == 0 && band_src_rows * crop_w * 4 <= 64 * 1024) {
-    const dim3 grid((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T));
-    const size_t shb = (size_t)(band_src_rows * crop_w * 4);
-    if (g_post_variant == 0 && W == 336) {
-      hipLaunchKernelGGL((post_band_col_kernel<SIG, 336>), grid, dim3(256), shb, (hipStream_t)stream, logits, h, w,
-                         crop_h, crop_w, out, H);
-      return catseg_launch_status(what);
-    }
-    if (g_post_variant == 0 && W == 384) {
-      hipLaunchKernelGGL((post_band_col_kernel<SIG, 384>), grid, dim3(256), shb, (hipStream_t)stream, logits, h, w,
-                         crop_h, crop_w, out, H);
-      return catseg_launch_status(what);
-    }
-    hipLaunchKernelGGL(post_band_kernel<SIG>, dim3((unsigned)((H + POST_ROWS - 1) / POST_ROWS), (unsigned)(B * T)),
-                       dim3(256), (size_t)(band_src_rows * crop_w * 4), (hipStream_t)stream, logits, h, w, crop_h,
-                       crop_w, out, H, W);
+    hipLaunchKernelGGL(post_band_kernel<SIG>, grid, dim3(256), (size_t)(band_src_rows * crop_w * 4), (hipStream_t)stream,
+                       logits, h, w, crop_h, crop_w, out, H, W);
     return catseg_launch_status(what);
   }
   hipLaunchKernelGGL(post_kernel<SIG>, dim3(grid_for(total, 65536)), dim3(256), 0, (hipStream_t)stream, logits,

@@ -1,3 +1,5 @@
+// catseg_swin_window_attention: argument checks and dispatch (the default kernel is the
+// head-per-SIMD form in swin_window.hip) plus the row-tile-wave kernel kept as its A/B reference.
 // Fused Swin window attention for the CAT-Seg spatial aggregation (bf16):
 //   LayerNorm(norm1) + [q|k|v] projection (+ the per-image guidance half of q, k)
 //   + shifted-window multi-head attention, one workgroup per (slice, window).
@@ -84,183 +86,7 @@ DEV void put_onehot(bf16* Ks, int wloc, int shift, int tid, int nt) {
   }
 }
 
-template <bool SWM>
-__global__ __launch_bounds__(NT) void swin_fused_kernel(SwinP p, int nwin_total) {
-  __shared__ __attribute__((aligned(16))) bf16 sW[3 * C * C];      // all of W_qkv, staged once
-  __shared__ __attribute__((aligned(16))) bf16 Ks[L * KC * 8];
-  __shared__ __attribute__((aligned(16))) bf16 Vt[D * VP];
-  __shared__ __attribute__((aligned(16))) bf16 Qs[L * D];
-  // LN gamma | beta | qkv bias, read from LDS inside the window loop (as loop-invariant
-  // global loads the compiler hoisted ~100 of them into VGPRs and spilled)
-  __shared__ __attribute__((aligned(16))) float sP[2 * C + 3 * C];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r16 = lane & 15, g = lane >> 4;
-  const int qi = wave * 16 + r16;                           // this lane's row / query in a window
-  for (int i = tid; i < 5 * C; i += NT) sP[i] = i < C ? p.ln_g[i] : i < 2 * C ? p.ln_b[i - C] : p.bias[i - 2 * C];
-
-  for (int c = tid; c < 3 * C * 16; c += NT) {
-    const int lr = c >> 4, ch = c & 15;
-    st16(&sW[cslot<3 * C>(ch, lr)], ld16(p.w + (int64_t)lr * C + ch * 8));
-  }
-  for (int i = tid; i < D * (KB - L); i += NT) Vt[(i / (KB - L)) * VP + L + i % (KB - L)] = 0;
-  __syncthreads();
-  s16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
-  const float sl2 = p.scale * 1.4426950408889634f;
-
-  // rows of the next window are prefetched into registers while this one computes:
-  // lane (r16, g) holds chunks g, 4+g, 8+g, 12+g of its row = its MFMA B fragments
-  uint4 nx[4];
-  auto fetch = [&](int win) {
-    const int64_t row = win_row(win / NWIN, win % NWIN, qi, p.shift);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) nx[ks] = ld16(p.x + row * p.ld_x + ks * 32 + 8 * g);
-  };
-  int win = blockIdx.x;
-  if (win < nwin_total) fetch(win);
-  for (; win < nwin_total; win += gridDim.x) {
-    const int slice = win / NWIN, wloc = win % NWIN;
-    const int64_t qrow = win_row(slice, wloc, qi, p.shift);
-    // ---- LayerNorm of this lane's row into MFMA B fragments ----
-    s16x8 hf[4];
-    {
-      float v[4][8], s = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16* e = reinterpret_cast<const bf16*>(&nx[ks]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { v[ks][j] = bf2f(e[j]); s += v[ks][j]; }
-      }
-      s = xrow4_sum(s);
-      const float mean = s * (1.f / C);
-      float q = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { v[ks][j] -= mean; q += v[ks][j] * v[ks][j]; }
-      q = xrow4_sum(q);
-      const float rstd = rsqrtf(q * (1.f / C) + p.eps);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int c0 = ks * 32 + 8 * g;
-        float o8[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o8[j] = v[ks][j] * rstd * sP[c0 + j] + sP[C + c0 + j];
-        uint4 u = make_uint4(f2bf2(o8[0], o8[1]), f2bf2(o8[2], o8[3]), f2bf2(o8[4], o8[5]), f2bf2(o8[6], o8[7]));
-        hf[ks] = *reinterpret_cast<s16x8*>(&u);
-      }
-    }
-    if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
-    // region one-hot of every key of this window (the previous window's last barrier retired its
-    // reads); once per workgroup when every window it walks has the same location
-    if constexpr (SWM) {
-      if (gridDim.x % NWIN != 0 || win == (int)blockIdx.x) put_onehot(Ks, wloc, p.shift, tid, NT);
-    }
-    s16x8 qmask;
-    if constexpr (SWM) {    // -100/scale on the dims of every other region (raw-score units)
-      const int qreg = region(wloc, qi, p.shift);
-      const float neg = -100.f / p.scale;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int dim = 8 * g + j;
-        qmask[j] = (short)f2bf(dim < 9 && dim != qreg ? neg : 0.f);
-      }
-    }
-    const bf16* grow_p = p.g + rowmap(p.gmap, qrow) * p.ld_g;  // guidance row of this lane's row
-
-#pragma unroll 1
-    for (int h = 0; h < NH; ++h) {
-      // lane ids made opaque per head: the LDS addresses below are recomputed each head
-      // (a few VALU) instead of being hoisted as ~30 loop-invariant VGPRs and spilled
-      int r16 = lane & 15, g = lane >> 4;
-      asm volatile("" : "+v"(r16), "+v"(g));
-      // ---- q, k, v of head h for this wave's rows: D^T = W_h . H^T (4 consecutive d per lane) ----
-#pragma unroll 1
-      for (int part = 0; part < 3; ++part) {          // 0 = q, 1 = k, 2 = v (rolled: bounds VGPRs)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int n0 = part * C + h * D + dt * 16;  // weight row block
-          f32x4 a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            a = mfma_bf16(*reinterpret_cast<const s16x8*>(&sW[cslot16<3 * C>(ks * 4 + g, n0, r16)]), hf[ks], a);
-          const int n = n0 + 4 * g;                   // this lane's 4 output features
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = a[r] + sP[2 * C + n + r];
-          if (part < 2) {                             // + W_g . LN(guidance) (per image, per pixel)
-            float gv[4];
-            load4<bf16>(grow_p + n, gv);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += gv[r];
-          }
-          const int d = dt * 16 + 4 * g;
-          if (part == 0) {
-            *reinterpret_cast<uint2*>(&Qs[cslot16<L>(d >> 3, wave * 16, r16) + (d & 7)]) =
-                make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
-          } else if (part == 1) {
-            *reinterpret_cast<uint2*>(&Ks[cslot16<L>(d >> 3, wave * 16, r16) + (d & 7)]) =
-                make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Vt[(d + r) * VP + qi] = f2bf(v[r]);
-          }
-        }
-      }
-      __syncthreads();
-
-      // ---- attention of this wave's 16 queries over the 144 keys (one block) ----
-      const s16x8 qf = *reinterpret_cast<const s16x8*>(&Qs[cslot16<L>(g, wave * 16, r16)]);
-      f32x4 st[KTV + 1];
-#pragma unroll
-      for (int kt = 0; kt < KTV; ++kt) {
-          f32x4 a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[cslot16<L>(g, kt * 16, r16)]), qf,
-                            f32x4{0.f, 0.f, 0.f, 0.f});
-        if constexpr (SWM) a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Ks[cslot16<L>(4 + g, kt * 16, r16)]), qmask, a);
-        st[kt] = a;
-      }
-      float mx = -1e30f;
-#pragma unroll
-      for (int kt = 0; kt < KTV; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[kt][r]);
-      mx = xrow4_max(mx);
-      const float nb = -mx * sl2;
-#pragma unroll
-      for (int kt = 0; kt < KTV; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
-      st[KTV] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < KB / 32; ++u) {
-        uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
-                              f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
-        const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16* vr = &Vt[(dt * 16 + r16) * VP + 32 * u + 4 * g];
-          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-          uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          o[dt] = mfma_bf16(*reinterpret_cast<s16x8*>(&va), pb, o[dt]);
-        }
-        osum = mfma_bf16(ones, pb, osum);
-      }
-      const float inv = 1.f / osum[0];
-      bf16* O = p.out + qrow * p.ld_out + h * D;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-        *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
-            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
-      __syncthreads();    // Ks / Vt / Qs are rewritten for the next head / window
-    }
-  }
-}
-
-// ---- pipelined form (default): head h+1's q/k/v projection runs in the same barrier interval
+// ---- pipelined row-tile-wave form (A/B reference of swin_window.hip): head h+1's q/k/v projection runs in the same barrier interval
 // as head h's attention.  K and V^T are double-buffered in LDS (Q stays in registers: the
 // projection leaves lane (row, g) holding q[row][4g..4g+3 | 16+4g..16+4g+3], which is exactly a
 // B fragment when the K rows use the same permuted d order inside each 16-byte chunk, so K is
@@ -452,8 +278,7 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
   }
 }
 
-int g_swin_variant = 0;   // 0 = head-per-SIMD (swin_window.hip), 2 = pipelined row-tile waves (swin_fused2_kernel),
-                          // 1 = two barriers per head (swin_fused_kernel)
+int g_swin_variant = 0;   // 0 = head-per-SIMD (swin_window.hip), else the row-tile-wave kernel (swin_fused2_kernel)
 
 }  // namespace
 
@@ -490,11 +315,6 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
   if (g_swin_variant == 0) {
     swin_win3_launch(a, n_cu, (hipStream_t)stream);
-  } else if (g_swin_variant == 1) {
-    if (a->shift > 0)
-      hipLaunchKernelGGL(swin_fused_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);
-    else
-      hipLaunchKernelGGL(swin_fused_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);
   } else {
     if (a->shift > 0)
       hipLaunchKernelGGL(swin_fused2_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);

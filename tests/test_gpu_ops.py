@@ -675,9 +675,9 @@ def test_bicubic_postprocess():
 
 @pytest.mark.parametrize("HW,crop", [(336, None), (384, None), (336, (90, 77))])
 def test_postprocess_compile_time_width(HW, crop):
-    """The band kernel with a compile-time output width (tuning knob post_variant 0, W = 336 / 384, the
+    """The separable band kernel (tuning knob post_variant 0, default; W = 336 / 384, the
     CAT-Seg eval outputs) vs torch (sigmoid -> bilinear, align_corners=False, sem_seg_postprocess crop)
-    and bit for bit vs the runtime-width band kernel (variant 1)."""
+    and bit for bit vs the direct band kernel (variant 1)."""
     lib = L.load()
     lg = (rnd(2, 5, 96, 96, seed=36) * 4).to(dev)
     outs = []
