@@ -460,6 +460,181 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// ViT MHA, LDS-DMA ring form: the K / V blocks arrive by global_load_lds (no staging VGPRs,
+// no staging VALU) into a 4-slot ring with two blocks in flight beyond the one being read, so
+// the load latency is covered by two blocks of compute; one raw barrier per block (each wave
+// retires its own pieces with a counted vmcnt first).  The LDS images are unpadded 128-byte
+// rows with the 16-byte chunk XOR-swizzled by row & 7 (applied to the per-lane DMA source, so
+// the lane-linear DMA destination lands the swizzled image): K fragment reads (ds_read_b128)
+// and V^T transposed reads (ds_read_b64_tr_b16) are conflict-free.  Softmax, row sums and the
+// output are vit_attn_kernel's.
+// ------------------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(AttnP p) {   // two workgroups per CU
+  constexpr int D = 64, KB = 64, NBUF = 4, AHEAD = 2;
+  constexpr int BLK = 2 * KB * D;                       // elements of one ring slot (K rows, then V rows)
+  constexpr float THR = 16.f;                           // defer-max threshold (log2 units)
+  static_assert(NW >= 8, "16 DMA pieces per block, two per wave");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BLK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int s = blockIdx.y / p.H, h = blockIdx.y % p.H;
+  const int g = lane >> 4, col = lane & 15;
+  const int L = p.L;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const int q0 = (blockIdx.x * NW + wave) * 16;
+  const bool live = q0 < L;                             // wave-uniform
+  const int qi = q0 + col;
+  const bool q_ok = qi < L;
+  const int64_t row0 = (int64_t)s * L;
+
+  s16x8 qf[2];
+  {
+    const bf16* Q = reinterpret_cast<const bf16*>(p.q) + (row0 + (q_ok ? qi : 0)) * p.ld + h * D;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[ks] = *reinterpret_cast<s16x8*>(&u);
+    }
+  }
+  // DMA pieces: piece j = 8 key rows (j % 8) * 8 .. +7 of K (j < 8) or V; lane l lands in slot l
+  // of the piece = row r = (j % 8) * 8 + l / 8, swizzled chunk l % 8 = chunk c ^ (r & 7)
+  const bf16* psrc[2];
+  int prow[2], pdst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = (wave * 2 + i) % 16, which = j >> 3;
+    const int r = (j & 7) * 8 + (lane >> 3), c = (lane & 7) ^ (r & 7);
+    prow[i] = r;
+    psrc[i] = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + c * 8;
+    pdst[i] = which * KB * D + (j & 7) * 8 * D;          // element offset of the piece in a slot
+  }
+  auto issue = [&](int blk) {
+    bf16* slot = smem + (blk % NBUF) * BLK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = min(blk * KB + prow[i], L - 1);    // rows past L re-read row L-1 (masked)
+      dma16(psrc[i] + (int64_t)key * p.ld, slot + pdst[i]);
+    }
+  };
+
+  f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f;
+  s16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
+  // per-lane byte offsets in a slot: K fragment rows kt*16 + col, chunks ks*4 + g (swizzle col & 7);
+  // V^T transposed reads rows 32u + 4g + col/4 (+16), chunk 2dt + ((col & 3) >> 1), half col & 1
+  const int kswz = col & 7;
+  const int koff0 = col * 128 + ((g ^ kswz) << 4), koff1 = col * 128 + (((4 + g) ^ kswz) << 4);
+  const int vrow = 4 * g + (col >> 2), vswz = vrow & 7;
+  int voff[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    voff[dt] = KB * D * 2 + vrow * 128 + (((2 * dt + ((col & 3) >> 1)) ^ vswz) << 4) + (col & 1) * 8;
+
+  auto block = [&](int blk, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    const char* S0 = reinterpret_cast<const char*>(smem + (blk % NBUF) * BLK);
+    const int k0 = blk * KB;
+    f32x4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      if (!TAIL || k0 + kt * 16 < L) {
+        a = mfma_bf16(*reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff0), qf[0], a);
+        a = mfma_bf16(*reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff1), qf[1], a);
+      }
+      st[kt] = a;
+    }
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
+    }
+    float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
+#pragma unroll
+    for (int kt = 1; kt < 4; ++kt)
+      lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+    if (__any((lm - m_run) * sl2 > THR)) {               // rare after the first block
+      const float m_new = fmaxf(m_run, xrow4_max(lm));
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] *= alpha;
+      osum *= alpha;
+    }
+    const float nb = -m_run * sl2;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (TAIL && k0 + 32 * u >= L) continue;            // P = 0 on all 32 keys
+      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
+                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
+      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
+      // the transposed reads go through inline asm: hipcc treats the ds_read_tr builtin as
+      // aliasing the in-flight LDS-DMA and would drain every block in flight (vmcnt(0)) first;
+      // their completion is waited for here explicitly (lgkmcnt(0), MFMAs fenced behind it)
+      s16x4 lo[4], hi[4];
+      const unsigned vb = (unsigned)(uintptr_t)(S0 + 32 * u * 128);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[dt]) : "v"(vb + voff[dt]));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi[dt]) : "v"(vb + voff[dt]));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = mfma_bf16(s16x8{lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]},
+                          pb, o[dt]);
+      osum = mfma_bf16(ones, pb, osum);
+    }
+  };
+
+  const int nblk = (L + KB - 1) / KB;
+  const int nfull = L / KB;                              // blocks with every key < L
+#pragma unroll
+  for (int b = 0; b <= AHEAD; ++b)
+    if (b < nblk) issue(b);
+  for (int blk = 0; blk < nblk; ++blk) {
+    // this wave's pieces of blocks blk+1 .. min(blk+AHEAD, nblk-1) may stay in flight
+    const int after = min(AHEAD, nblk - 1 - blk);
+    if (after >= 2) wait_vmcnt<4>();
+    else if (after == 1) wait_vmcnt<2>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();                         // every wave's pieces of block blk landed;
+    __builtin_amdgcn_sched_barrier(0);                    // every wave is done with block blk - 1
+    if (blk + AHEAD + 1 < nblk) issue(blk + AHEAD + 1);   // into block blk - 1's slot
+    if (live) {
+      if (blk < nfull) block(blk, std::false_type{});
+      else block(blk, std::true_type{});
+    }
+  }
+  if (!q_ok) return;
+  const float inv = 1.f / osum[0];
+  bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
+    store4<bf16>(O + dt * 16 + 4 * g, v);
+  }
+}
+
+template <int NW>
+void launch_vit3(const AttnP& p, hipStream_t st) {
+  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
+  hipLaunchKernelGGL((vit_attn3_kernel<NW>), grid, dim3(NW * 64), 0, st, p);
+}
+
 template <int NW>
 void launch_vit(const AttnP& p, hipStream_t st) {
   dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
@@ -492,12 +667,13 @@ void launch_dense(const AttnP& p, hipStream_t st) {
     // the ViT MHA kernel; 10 waves x 16 queries when that needs fewer query blocks than 8 x 16
     // (L = 577: 4 blocks of 160, 512 workgroups, two per CU)
     if (g_attn_variant == 0) {
-      if ((p.L + 159) / 160 < (p.L + 127) / 128) launch_vit<10>(p, st);
-      else launch_vit<8>(p, st);
+      if ((p.L + 159) / 160 < (p.L + 127) / 128) launch_vit3<10>(p, st);
+      else launch_vit3<8>(p, st);
       return;
     }
-    if (g_attn_variant == 8) { launch_vit<8>(p, st); return; }
-    if (g_attn_variant == 9) { launch_vit<4>(p, st); return; }
+    if (g_attn_variant == 8) { launch_vit<10>(p, st); return; }
+    if (g_attn_variant == 9) { launch_vit3<8>(p, st); return; }
+    if (g_attn_variant == 10) { launch_vit3<12>(p, st); return; }
   }
   switch (g_attn_variant) {
     case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;

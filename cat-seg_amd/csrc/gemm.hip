@@ -408,15 +408,6 @@ __global__ __launch_bounds__(NT) void gemm2_kernel(const bf16* __restrict__ A, i
 // sub-tile of D = W . A^T (4 consecutive output columns per lane).  Needs K % BK == 0 and
 // N % BN == 0 (host-checked); rows >= M read row M-1 and are masked in the epilogue.
 // ------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void gbl_void_t;
-
-template <int N>
-DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  // gfx9 s_waitcnt encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
