@@ -470,12 +470,12 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
 // and V^T transposed reads (ds_read_b64_tr_b16) are conflict-free.  Softmax, row sums and the
 // output are vit_attn_kernel's.
 // ------------------------------------------------------------------------------------
-template <int NW>
+template <int NW, int QT>
 __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(AttnP p) {   // two workgroups per CU
   constexpr int D = 64, KB = 64, NBUF = 4, AHEAD = 2;
   constexpr int BLK = 2 * KB * D;                       // elements of one ring slot (K rows, then V rows)
+  constexpr int NI = (16 + NW - 1) / NW;                // DMA pieces (1 KiB) per wave per block
   constexpr float THR = 16.f;                           // defer-max threshold (log2 units)
-  static_assert(NW >= 8, "16 DMA pieces per block, two per wave");
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BLK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -483,28 +483,31 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   const int g = lane >> 4, col = lane & 15;
   const int L = p.L;
   const float sl2 = p.scale * 1.4426950408889634f;
-  const int q0 = (blockIdx.x * NW + wave) * 16;
+  const int q0 = (blockIdx.x * NW + wave) * 16 * QT;
   const bool live = q0 < L;                             // wave-uniform
-  const int qi = q0 + col;
-  const bool q_ok = qi < L;
   const int64_t row0 = (int64_t)s * L;
 
-  s16x8 qf[2];
-  {
-    const bf16* Q = reinterpret_cast<const bf16*>(p.q) + (row0 + (q_ok ? qi : 0)) * p.ld + h * D;
+  // QT query tiles of 16 per wave: every K fragment / V^T read feeds QT MFMAs
+  s16x8 qf[QT][2];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int qi = q0 + 16 * t + col;
+    const bf16* Q = reinterpret_cast<const bf16*>(p.q) + (row0 + (qi < L ? qi : 0)) * p.ld + h * D;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
-      qf[ks] = *reinterpret_cast<s16x8*>(&u);
+      uint4 u = qi < L ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[t][ks] = *reinterpret_cast<s16x8*>(&u);
     }
   }
   // DMA pieces: piece j = 8 key rows (j % 8) * 8 .. +7 of K (j < 8) or V; lane l lands in slot l
-  // of the piece = row r = (j % 8) * 8 + l / 8, swizzled chunk l % 8 = chunk c ^ (r & 7)
-  const bf16* psrc[2];
-  int prow[2], pdst[2];
+  // of the piece = row r = (j % 8) * 8 + l / 8, swizzled chunk l % 8 = chunk c ^ (r & 7).
+  // Every wave issues NI pieces (wave-uniform counted vmcnt); surplus waves repeat pieces (benign
+  // duplicate writes of identical bytes)
+  const bf16* psrc[NI];
+  int prow[NI], pdst[NI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int j = (wave * 2 + i) % 16, which = j >> 3;
+  for (int i = 0; i < NI; ++i) {
+    const int j = (wave * NI + i) % 16, which = j >> 3;
     const int r = (j & 7) * 8 + (lane >> 3), c = (lane & 7) ^ (r & 7);
     prow[i] = r;
     psrc[i] = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + c * 8;
@@ -513,16 +516,21 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   auto issue = [&](int blk) {
     bf16* slot = smem + (blk % NBUF) * BLK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int key = min(blk * KB + prow[i], L - 1);    // rows past L re-read row L-1 (masked)
       dma16(psrc[i] + (int64_t)key * p.ld, slot + pdst[i]);
     }
   };
 
-  f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
+  f32x4 o[QT][4], osum[QT];
+  float m_run[QT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f;
+  for (int t = 0; t < QT; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    osum[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run[t] = -1e30f;
+  }
   s16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
@@ -540,46 +548,58 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
     constexpr bool TAIL = decltype(tail_tag)::value;
     const char* S0 = reinterpret_cast<const char*>(smem + (blk % NBUF) * BLK);
     const int k0 = blk * KB;
-    f32x4 st[4];
+    f32x4 st[QT][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < QT; ++t) st[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (!TAIL || k0 + kt * 16 < L) {
-        a = mfma_bf16(*reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff0), qf[0], a);
-        a = mfma_bf16(*reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff1), qf[1], a);
+        const s16x8 k0f = *reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff0);
+        const s16x8 k1f = *reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff1);
+#pragma unroll
+        for (int t = 0; t < QT; ++t) st[t][kt] = mfma_bf16(k1f, qf[t][1], mfma_bf16(k0f, qf[t][0], st[t][kt]));
       }
-      st[kt] = a;
     }
     if constexpr (TAIL) {
 #pragma unroll
+      for (int t = 0; t < QT; ++t)
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + kt * 16 + 4 * g + r >= L) st[t][kt][r] = -INFINITY;
+    }
+    s16x8 pb[QT][2];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      float lm = fmaxf(fmaxf(st[t][0][0], st[t][0][1]), fmaxf(st[t][0][2], st[t][0][3]));
+#pragma unroll
+      for (int kt = 1; kt < 4; ++kt)
+        lm = fmaxf(lm, fmaxf(fmaxf(st[t][kt][0], st[t][kt][1]), fmaxf(st[t][kt][2], st[t][kt][3])));
+      if (__any((lm - m_run[t]) * sl2 > THR)) {          // rare after the first block
+        const float m_new = fmaxf(m_run[t], xrow4_max(lm));
+        const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * sl2);
+        m_run[t] = m_new;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[t][i] *= alpha;
+        osum[t] *= alpha;
+      }
+      const float nb = -m_run[t] * sl2;
+#pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
+        for (int r = 0; r < 4; ++r) st[t][kt][r] = __builtin_amdgcn_exp2f(fmaf(st[t][kt][r], sl2, nb));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        uint4 pu = make_uint4(f2bf2(st[t][2 * u][0], st[t][2 * u][1]), f2bf2(st[t][2 * u][2], st[t][2 * u][3]),
+                              f2bf2(st[t][2 * u + 1][0], st[t][2 * u + 1][1]),
+                              f2bf2(st[t][2 * u + 1][2], st[t][2 * u + 1][3]));
+        pb[t][u] = *reinterpret_cast<s16x8*>(&pu);
+      }
     }
-    float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
-#pragma unroll
-    for (int kt = 1; kt < 4; ++kt)
-      lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
-    if (__any((lm - m_run) * sl2 > THR)) {               // rare after the first block
-      const float m_new = fmaxf(m_run, xrow4_max(lm));
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
-      m_run = m_new;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] *= alpha;
-      osum *= alpha;
-    }
-    const float nb = -m_run * sl2;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (TAIL && k0 + 32 * u >= L) continue;            // P = 0 on all 32 keys
-      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
-                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
-      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
       // the transposed reads go through inline asm: hipcc treats the ds_read_tr builtin as
       // aliasing the in-flight LDS-DMA and would drain every block in flight (vmcnt(0)) first;
       // their completion is waited for here explicitly (lgkmcnt(0), MFMAs fenced behind it)
@@ -593,10 +613,13 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        o[dt] = mfma_bf16(s16x8{lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]},
-                          pb, o[dt]);
-      osum = mfma_bf16(ones, pb, osum);
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x8 va = s16x8{lo[dt][0], lo[dt][1], lo[dt][2], lo[dt][3], hi[dt][0], hi[dt][1], hi[dt][2], hi[dt][3]};
+#pragma unroll
+        for (int t = 0; t < QT; ++t) o[t][dt] = mfma_bf16(va, pb[t][u], o[t][dt]);
+      }
+#pragma unroll
+      for (int t = 0; t < QT; ++t) osum[t] = mfma_bf16(ones, pb[t][u], osum[t]);
     }
   };
 
@@ -608,8 +631,8 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   for (int blk = 0; blk < nblk; ++blk) {
     // this wave's pieces of blocks blk+1 .. min(blk+AHEAD, nblk-1) may stay in flight
     const int after = min(AHEAD, nblk - 1 - blk);
-    if (after >= 2) wait_vmcnt<4>();
-    else if (after == 1) wait_vmcnt<2>();
+    if (after >= 2) wait_vmcnt<2 * NI>();
+    else if (after == 1) wait_vmcnt<NI>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();                         // every wave's pieces of block blk landed;
     __builtin_amdgcn_sched_barrier(0);                    // every wave is done with block blk - 1
@@ -619,26 +642,30 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
       else block(blk, std::true_type{});
     }
   }
-  if (!q_ok) return;
-  const float inv = 1.f / osum[0];
-  bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
-    store4<bf16>(O + dt * 16 + 4 * g, v);
+  for (int t = 0; t < QT; ++t) {
+    const int qi = q0 + 16 * t + col;
+    if (qi >= L) continue;
+    const float inv = 1.f / osum[t][0];
+    bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      float v[4] = {o[t][dt][0] * inv, o[t][dt][1] * inv, o[t][dt][2] * inv, o[t][dt][3] * inv};
+      store4<bf16>(O + dt * 16 + 4 * g, v);
+    }
   }
-}
-
-template <int NW>
-void launch_vit3(const AttnP& p, hipStream_t st) {
-  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((vit_attn3_kernel<NW>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <int NW>
 void launch_vit(const AttnP& p, hipStream_t st) {
   dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
   hipLaunchKernelGGL((vit_attn_kernel<NW>), grid, dim3(NW * 64), 0, st, p);
+}
+
+template <int NW, int QT>
+void launch_vit3(const AttnP& p, hipStream_t st) {
+  dim3 grid((unsigned)((p.L + 16 * NW * QT - 1) / (16 * NW * QT)), (unsigned)(p.n_seq * p.H));
+  hipLaunchKernelGGL((vit_attn3_kernel<NW, QT>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
@@ -664,16 +691,12 @@ void launch_dense(const AttnP& p, hipStream_t st) {
   // workgroup, 64-key blocks: 35.3 us vs 40.3 for 4 waves x 2 query tiles (more waves in
   // flight hide the per-block softmax chain)
   if constexpr (sizeof(T) == 2 && D == 64) {
-    // the ViT MHA kernel; 10 waves x 16 queries when that needs fewer query blocks than 8 x 16
-    // (L = 577: 4 blocks of 160, 512 workgroups, two per CU)
-    if (g_attn_variant == 0) {
-      if ((p.L + 159) / 160 < (p.L + 127) / 128) launch_vit3<10>(p, st);
-      else launch_vit3<8>(p, st);
-      return;
-    }
+    // the ViT MHA kernels (variants: A/B of waves per workgroup / query tiles per wave)
+    if (g_attn_variant == 0) { launch_vit3<8, 1>(p, st); return; }
     if (g_attn_variant == 8) { launch_vit<10>(p, st); return; }
-    if (g_attn_variant == 9) { launch_vit3<8>(p, st); return; }
-    if (g_attn_variant == 10) { launch_vit3<12>(p, st); return; }
+    if (g_attn_variant == 9) { launch_vit3<10, 1>(p, st); return; }
+    if (g_attn_variant == 10) { launch_vit3<5, 2>(p, st); return; }
+    if (g_attn_variant == 11) { launch_vit3<4, 2>(p, st); return; }
   }
   switch (g_attn_variant) {
     case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;
