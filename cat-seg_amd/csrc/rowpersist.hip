@@ -411,6 +411,191 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   }
 }
 
+// ---- barrier-lean form (default): the epilogue of tile t runs in the same barrier interval as
+// the first GEMM (MLP) / the projection (PROJ) of tile t+1, and the next tile's rows are put into
+// LDS beside GEMM2 of this one; the residual rows (x1 / the raw input rows, res2) wait in LDS,
+// double-buffered by tile parity, instead of registers.  Barriers per 32-row tile: 2 (MLP) /
+// 4 (PROJ) instead of 4 / 6 -- one workgroup per CU (the weights fill the registers), so every
+// barrier stalls all of the CU's waves.  Same arithmetic in the same order as pmlp_kernel
+// (PAIR order): bit-identical.
+template <int ACT, bool RES2, bool PROJ>
+__global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
+                                                      const float* ln_g, const float* ln_b, float eps,
+                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                      const bf16* __restrict__ W2, PEpi e,
+                                                      const bf16* __restrict__ Xr = nullptr, int64_t ldxr = 0,
+                                                      const bf16* __restrict__ Wp = nullptr,
+                                                      const float* __restrict__ bp = nullptr) {
+  static_assert(!(PROJ && RES2), "PROJ carries the x rows in the res2 slot");
+  constexpr int FM = BM / 16, SLD = KD + 4;
+  constexpr int NPAR = 2 * KD + HID + KD + (PROJ ? KD : 0);
+  __shared__ __attribute__((aligned(16))) bf16 sX[BM * LDX];
+  __shared__ __attribute__((aligned(16))) bf16 sH[BM * LDH];
+  __shared__ __attribute__((aligned(16))) float stA[PROJ ? BM * SLD : 4];      // projection output
+  __shared__ __attribute__((aligned(16))) float stB[BM * SLD];                 // GEMM2 output
+  __shared__ __attribute__((aligned(16))) bf16 yres[2][BM * KD];               // x1 / raw rows, by tile parity
+  __shared__ __attribute__((aligned(16))) bf16 r2res[RES2 ? 2 : 1][RES2 ? BM * KD : 8];
+  __shared__ __attribute__((aligned(16))) bf16 xres[PROJ ? BM * KD : 8];       // PROJ: the x rows
+  __shared__ __attribute__((aligned(16))) float sPar[NPAR];
+  for (int i = threadIdx.x; i < NPAR; i += NT)
+    sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
+            : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
+  const float* sb1 = sPar + 2 * KD;
+  const float* sb2 = sPar + 2 * KD + HID;
+  const float* sbp = sPar + 3 * KD + HID;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  s16x8 wpf[PROJ ? 4 : 1];
+  if constexpr (PROJ) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) wpf[ks] = __builtin_bit_cast(s16x8, ld16(Wp + (int64_t)(16 * wave + r16) * KD + ks * 32 + 8 * q));
+  }
+  s16x8 w1f[4][4], w2f[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int unit = 64 * wave + 32 * (i >> 1) + 8 * (r16 >> 2) + 4 * (i & 1) + (r16 & 3);
+      w1f[i][ks] = __builtin_bit_cast(s16x8, ld16(W1 + (int64_t)unit * KD + ks * 32 + 8 * q));
+    }
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) w2f[ks] = __builtin_bit_cast(s16x8, ld16(W2 + (int64_t)(16 * wave + r16) * HID + ks * 32 + 8 * q));
+  const int64_t ntiles = (M + BM - 1) / BM;
+  const int64_t G = gridDim.x;
+  const int er = threadIdx.x >> 4, ec = (threadIdx.x & 15) * 8;   // this thread's chunk of a tile
+  const int rofs = er * KD + ec;
+  uint4 ry = {}, rr2 = {};                        // rows of the next tile, in flight
+  auto fetch = [&](int64_t t) {
+    ry = fetch_chunk(Y, ldy, t * BM, M);
+    if constexpr (RES2) rr2 = fetch_chunk(e.res2, e.ld_res2, t * BM, M);
+    if constexpr (PROJ) rr2 = fetch_chunk(Xr, ldxr, t * BM, M);
+  };
+  auto put = [&](int par) {                       // the fetched tile -> LDS
+    if constexpr (PROJ) {
+      put_chunk(ry, nullptr, nullptr, eps, sX);   // the attention rows, as they are
+      st16(&xres[rofs], rr2);
+    } else {
+      st16(&yres[par][rofs], ry);
+      if constexpr (RES2) st16(&r2res[par][rofs], rr2);
+      put_chunk(ry, sPar, sPar + KD, eps, sX);
+    }
+  };
+  auto gemm1 = [&]() {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x4 acc1[2][FM];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float4 bv = *reinterpret_cast<const float4*>(sb1 + 64 * wave + 32 * hf + 8 * q + 4 * i);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc1[i][j] = f32x4{bv.x, bv.y, bv.z, bv.w};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s16x8 xf[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const s16x8*>(&sX[cslot<BM>(ks * 4 + q, 16 * j + r16)]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc1[i][j] = mfma_bf16(w1f[2 * hf + i][ks], xf[j], acc1[i][j]);
+      }
+      const int hh = 64 * wave + 32 * hf + 8 * q;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
+            else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
+          }
+        st16(&sH[(16 * j + r16) * LDH + hh], pack8(v));
+      }
+    }
+  };
+  auto epilogue = [&](int64_t t, int par) {
+    const int64_t m = t * BM + er;
+    float v[8];
+    *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&stB[er * SLD + ec]);
+    *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&stB[er * SLD + ec + 4]);
+    const float4 c0 = *reinterpret_cast<const float4*>(sb2 + ec), c1 = *reinterpret_cast<const float4*>(sb2 + ec + 4);
+    v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+    v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+    add8(v, *reinterpret_cast<const uint4*>(&yres[par][rofs]));
+    if constexpr (RES2) add8(v, *reinterpret_cast<const uint4*>(&r2res[par][rofs]));
+    if (m < M) st16(e.out + m * e.ldo + ec, pack8(v));
+  };
+
+  int64_t t = blockIdx.x;
+  if (t < ntiles) fetch(t);
+  __syncthreads();                                // sPar
+  if (t < ntiles) put(0);
+  if (t + G < ntiles) fetch(t + G);
+  __syncthreads();
+  int it = 0;
+  for (; t < ntiles; t += G, ++it) {
+    const int par = it & 1;
+    // [A] projection (PROJ) / GEMM1 of tile t beside the epilogue of tile t - G
+    if constexpr (PROJ) {
+      f32x4 ap[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) ap[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          ap[j] = mfma_bf16(wpf[ks], *reinterpret_cast<const s16x8*>(&sX[cslot<BM>(ks * 4 + q, 16 * j + r16)]), ap[j]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        *reinterpret_cast<f32x4*>(&stA[(16 * j + r16) * SLD + 16 * wave + 4 * q]) = ap[j];
+    } else {
+      gemm1();
+    }
+    if (it > 0) epilogue(t - G, par ^ 1);
+    __syncthreads();
+    if constexpr (PROJ) {
+      // [B] x1 = bf16(attn . Wp^T + bp + x) -> residual slot; LayerNorm(x1) -> sX
+      float v[8];
+      *reinterpret_cast<f32x4*>(&v[0]) = *reinterpret_cast<const f32x4*>(&stA[er * SLD + ec]);
+      *reinterpret_cast<f32x4*>(&v[4]) = *reinterpret_cast<const f32x4*>(&stA[er * SLD + ec + 4]);
+      const float4 p0 = *reinterpret_cast<const float4*>(sbp + ec), p1 = *reinterpret_cast<const float4*>(sbp + ec + 4);
+      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+      add8(v, *reinterpret_cast<const uint4*>(&xres[rofs]));
+      const uint4 x1 = pack8(v);
+      st16(&yres[par][rofs], x1);
+      put_chunk(x1, sPar, sPar + KD, eps, sX);
+      __syncthreads();
+      // [C] GEMM1
+      gemm1();
+      __syncthreads();
+    }
+    // [D] GEMM2 -> stB; the next tile's rows -> LDS; the one after that requested
+    f32x4 acc2[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + 8 * q]);
+        acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+      *reinterpret_cast<f32x4*>(&stB[(16 * j + r16) * SLD + 16 * wave + 4 * q]) = acc2[j];
+    if (t + G < ntiles) {
+      put(par ^ 1);
+      if (t + 2 * G < ntiles) fetch(t + 2 * G);
+    }
+    __syncthreads();
+  }
+  if (it > 0) epilogue(t - G, (it - 1) & 1);
+}
+
 // ============================ decoder ConvTranspose over 64-channel rows ================
 // out = scatter_k2(relu(GN(X)) . W^T + bias): the second Up block's ConvTranspose2d
 // (model.py:546) fused with the preceding GroupNorm+ReLU of DoubleConv (model.py:532-533).
@@ -594,12 +779,26 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
 
 int g_mlp_pair = 1;   // persistent MLP hidden-unit order: 1 = paired 16-byte hidden stores (default), 0 = 8-byte
 CATSEG_KNOB(g_mlp_pair, "mlp_pair");
+int g_mlp_variant = 0;   // 0 = barrier-lean pmlp2_kernel (default), 1 = pmlp_kernel (A/B; bit-identical)
+CATSEG_KNOB(g_mlp_variant, "mlp_variant");
 
 template <bool PAIR>
 int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
                         const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e, bool res2,
                         hipStream_t st) {
   const dim3 grid(persist_grid(M)), blk(NT);
+  if (PAIR && g_mlp_variant == 0) {
+    if (act == ACT_GELU && !res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else if (act == ACT_RELU && res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_RELU, true, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else if (act == ACT_RELU && !res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_RELU, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else if (act == ACT_GELU && res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, true, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else return 1;
+    return 0;
+  }
   if (act == ACT_GELU && !res2)
     hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
   else if (act == ACT_RELU && res2)
@@ -638,7 +837,11 @@ extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const voi
   CATSEG_CHECK(out == x ? ld_out == ld_x : true, "swin_proj_mlp: in place needs ld_out == ld_x");
   PEpi e{};
   e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
-  if (g_mlp_pair)
+  if (g_mlp_pair && g_mlp_variant == 0)
+    hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
+                       (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
+  else if (g_mlp_pair)
     hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
                        (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);

@@ -1118,3 +1118,35 @@ def test_head_conv_mfma_tap_image(H, W):
     close(outs[0], outs[1], atol=1e-4, what="head mfma vs band (same fp16 staging, fp32 sums)")
     # the band kernel with the compile-time width (W = 96) is the runtime-width one, bit for bit
     assert torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("M", [2 * 577 + 9, 300 * 32 + 17, 40])
+@pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
+def test_mlp_barrier_lean_bit_identical(act, M):
+    """The barrier-lean persistent MLP (tuning knob mlp_variant 0, the default: the epilogue of one
+    tile beside the first GEMM of the next, residual rows in LDS) equals pmlp_kernel (1) bit for
+    bit -- the Swin MLP (GELU), the class MLP (ReLU, + res2), the fused Swin proj + MLP -- on ragged
+    M with one tile per workgroup (40 rows), a few, and many (> 2 tiles per workgroup)."""
+    C, Hd = 128, 512
+    dt = torch.bfloat16
+    y = (rnd(M, C, seed=130) * 2).to(dev, dt)
+    x = rnd(M, C, seed=131).to(dev, dt)
+    g, b = (1 + rnd(C, seed=132) * 0.2).to(dev), (rnd(C, seed=133) * 0.1).to(dev)
+    w1, b1 = (rnd(Hd, C, seed=134) / 11).to(dev, dt), rnd(Hd, seed=135).to(dev)
+    w2, b2 = (rnd(C, Hd, seed=136) / 22).to(dev, dt), rnd(C, seed=137).to(dev)
+    wp, bp = (rnd(C, C, seed=138) / 11).to(dev, dt), rnd(C, seed=139).to(dev)
+    outs = {}
+    try:
+        for v in (0, 1):
+            L.tune("mlp_variant", v)
+            o1 = torch.empty_like(y)
+            ops.rows_mlp(y, w1, b1, w2, o1, ln=(g, b), b2=b2, act=act, res=y,
+                         res2=x if act == L.ACT_RELU else None)
+            o2 = x.clone()
+            ops.swin_proj_mlp(y, o2, wp, bp, w1, b1, w2, b2, o2, ln=(g, b))
+            torch.cuda.synchronize()
+            outs[v] = (o1, o2)
+    finally:
+        L.tune("mlp_variant", 0)
+    assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0].float() - outs[1][0].float()).abs().max().item()
+    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1].float() - outs[1][1].float()).abs().max().item()
