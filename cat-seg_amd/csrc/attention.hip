@@ -85,8 +85,10 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) T Vt[VROWS * VP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int s = blockIdx.y / p.H;
-  const int h = blockIdx.y % p.H;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int bx = lin % gridDim.x, by = lin / gridDim.x;   // query blocks of one head on one XCD
+  const int s = by / p.H;
+  const int h = by % p.H;
   const int g = lane >> 4;
   const int L = LC ? LC : p.L;
   const T* Kg = reinterpret_cast<const T*>(p.k);
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
   float m_run[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    const int q0 = (blockIdx.x * NW * QT + wave * QT + t) * 16;
+    const int q0 = (bx * NW * QT + wave * QT + t) * 16;
     tile_live[t] = q0 < L;
     qi[t] = q0 + (lane & 15);
     q_ok[t] = qi[t] < L;
@@ -316,11 +318,14 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int s = blockIdx.y / p.H, h = blockIdx.y % p.H;
+  // all query blocks of one (sequence, head) on one XCD: its K / V are fetched into one L2
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int bx = lin % gridDim.x, by = lin / gridDim.x;
+  const int s = by / p.H, h = by % p.H;
   const int g = lane >> 4, col = lane & 15;
   const int L = p.L;
   const float sl2 = p.scale * 1.4426950408889634f;
-  const int q0 = (blockIdx.x * NW + wave) * 16;
+  const int q0 = (bx * NW + wave) * 16;
   const bool live = q0 < L;                             // wave-uniform
   const int qi = q0 + col;
   const bool q_ok = qi < L;
@@ -479,11 +484,14 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BLK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int s = blockIdx.y / p.H, h = blockIdx.y % p.H;
+  // all query blocks of one (sequence, head) on one XCD: its K / V are fetched into one L2
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int bx = lin % gridDim.x, by = lin / gridDim.x;
+  const int s = by / p.H, h = by % p.H;
   const int g = lane >> 4, col = lane & 15;
   const int L = p.L;
   const float sl2 = p.scale * 1.4426950408889634f;
-  const int q0 = (blockIdx.x * NW + wave) * 16 * QT;
+  const int q0 = (bx * NW + wave) * 16 * QT;
   const bool live = q0 < L;                             // wave-uniform
   const int64_t row0 = (int64_t)s * L;
 
@@ -687,16 +695,13 @@ int g_attn_variant = 0;   // dense-path tiling (catseg_set_attn_variant; 0 = def
 template <typename T, int D>
 void launch_dense(const AttnP& p, hipStream_t st) {
   if (p.causal) { launch<T, D, 4, 64, 2, 0, false, true>(p, st); return; }
-  // measured on the ViT-L/14 shape (tools/micro_attn.py): 8 waves x 16 queries per
-  // workgroup, 64-key blocks: 35.3 us vs 40.3 for 4 waves x 2 query tiles (more waves in
-  // flight hide the per-block softmax chain)
   if constexpr (sizeof(T) == 2 && D == 64) {
-    // the ViT MHA kernels (variants: A/B of waves per workgroup / query tiles per wave)
+    // the ViT MHA kernels, ViT-L/14 shape (tools/micro_attn.py, XCD-remapped grids): LDS-DMA
+    // ring 8 waves 28.3 us, register-staged 10 waves 29.2, generic tiling (variant 7) 28.5;
+    // measured before the remap: ring 10 waves 33.2, ring 5 waves x 2 query tiles 37.1,
+    // 4 x 2 31.6 (the shared K / V^T fragment reads did not pay for the lost occupancy)
     if (g_attn_variant == 0) { launch_vit3<8, 1>(p, st); return; }
     if (g_attn_variant == 8) { launch_vit<10>(p, st); return; }
-    if (g_attn_variant == 9) { launch_vit3<10, 1>(p, st); return; }
-    if (g_attn_variant == 10) { launch_vit3<5, 2>(p, st); return; }
-    if (g_attn_variant == 11) { launch_vit3<4, 2>(p, st); return; }
   }
   switch (g_attn_variant) {
     case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;

@@ -71,6 +71,13 @@ template <> DEV void store4<bf16>(bf16* p, const float v[4]) {
 // LDS-DMA (global_load_lds, 16 B per lane, lane-linear LDS destination) and counted vmcnt waits
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
+// Workgroups are dealt round-robin over the 8 XCDs (observed, speed only): remap the linear
+// block id so each XCD owns a contiguous range (neighbouring tiles share one L2).
+DEV int xcd_remap(int bid, int nwg) {
+  const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
 DEV void dma16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }

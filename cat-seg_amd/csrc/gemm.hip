@@ -286,11 +286,6 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
 // ------------------------------------------------------------------------------------
 constexpr int BK2 = 64;
 
-DEV int xcd_remap(int bid, int nwg) {
-  const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-}
-
 template <typename TO, int BM, int BN>
 __global__ __launch_bounds__(NT) void gemm2_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
                                                    const bf16* __restrict__ W, int64_t ldw, int64_t M, int64_t N,
