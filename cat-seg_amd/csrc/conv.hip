@@ -555,138 +555,14 @@ __global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__
   }
 }
 
-// ---------------- head conv on the MFMA (bf16 input, C = 32) ---------------------------
-// The 3x3, 32 -> 1 head (model.py:634) as a 1x1 conv to the 9 taps followed by a shift-add:
-// y[p][t] = sum_c w[t][c] z[p][c] for every staged pixel p (one v_mfma_f32_16x16x32_f16 per 16
-// pixels: A = the 9 tap rows of w padded to 16, B = 16 pixels' fp16 channels), then
-// out(y, x) = bias + sum_t y[(y+dy, x+dx)][t].  Staging (GroupNorm+ReLU in fp32 -> fp16, zero
-// halo) is head_band_kernel's; the 144 v_dot2c per output it replaces were most of its VALU.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-constexpr int HYS = 13;           // fp32 per pixel in the tap image (odd: conflict-free tap reads)
-
-template <int C>
-__global__ __launch_bounds__(256) void head_mfma_kernel(const bf16* __restrict__ x, int Tn, int H, int W,
-                                                        const float* __restrict__ w, float bias, const float* mean,
-                                                        const float* rstd, const float* gamma, const float* beta,
-                                                        int cpg, const int32_t* classes, int Tout, float* out) {
-  static_assert(C == 32, "one K=32 MFMA step per 16 pixels");
-  constexpr int CPX = C / 8, CP = C + 8;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* ssc = reinterpret_cast<float*>(smem);                          // [C]
-  float* ssh = ssc + C;                                                 // [C]
-  _Float16* tile = reinterpret_cast<_Float16*>(smem + 2 * C * 4);       // [HBR+2][W+2][CP], then the tap image
-  float* ys = reinterpret_cast<float*>(smem + 2 * C * 4);               // [pixels][HYS] (overlays the tile)
-  const int64_t s = blockIdx.y;
-  const int y0 = blockIdx.x * HBR;
-  const int rows = min(HBR, H - y0);
-  const int WP = W + 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r16 = lane & 15, q = lane >> 4;
-  const int groups = C / cpg;
-  for (int c = tid; c < C; c += 256) {
-    if (mean) {
-      const float sc = rstd[s * groups + c / cpg] * gamma[c];
-      ssc[c] = sc;
-      ssh[c] = beta[c] - mean[s * groups + c / cpg] * sc;
-    } else {
-      ssc[c] = 1.f;
-      ssh[c] = 0.f;
-    }
-  }
-  // A fragment: tap row r16 (< 9, else 0), channels 8q .. 8q+7, fp16
-  f16x8 wa;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) wa[k] = (_Float16)(r16 < 9 ? w[r16 * C + 8 * q + k] : 0.f);
-  __syncthreads();
-  const bool relu = mean != nullptr;
-  const int64_t HW = (int64_t)H * W;
-  const bf16* xs = x + s * HW * C;
-  const int npix = (rows + 2) * WP;
-  const int total = npix * CPX;
-  constexpr int NL = 16;
-  for (int i0 = 0; i0 < total; i0 += 256 * NL) {
-    uint4 u[NL];
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int i = i0 + j * 256 + tid;
-      const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
-      const int yy = y0 - 1 + r, xx = xc - 1;
-      u[j] = (i < total && yy >= 0 && yy < H && xx >= 0 && xx < W) ? ld16(xs + ((int64_t)yy * W + xx) * C + ch * 8)
-                                                                   : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int i = i0 + j * 256 + tid;
-      if (i >= total) continue;
-      const int ch = i % CPX, pos = i / CPX, r = pos / WP, xc = pos - r * WP;
-      const int yy = y0 - 1 + r, xx = xc - 1;
-      const bool inside = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      const bf16* e = reinterpret_cast<const bf16*>(&u[j]);
-      _Float16 hv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float v = fmaf(bf2f(e[k]), ssc[ch * 8 + k], ssh[ch * 8 + k]);
-        if (relu) v = fmaxf(v, 0.f);
-        hv[k] = (_Float16)(inside ? v : 0.f);
-      }
-      st16(&tile[pos * CP + ch * 8], *reinterpret_cast<uint4*>(hv));
-    }
-  }
-  __syncthreads();
-  // y[p][tap] for every staged pixel: wave w takes 16-pixel groups w, w+4, ...; results stay in
-  // registers until every wave has read the fp16 tile (the tap image overlays it)
-  constexpr int MAXG = ((HBR + 2) * (128 + 2) + 15) / 16 / 4 + 1;      // groups per wave, W <= 128
-  const int ngr = (npix + 15) / 16;
-  f32x4 yv[MAXG];
-#pragma unroll
-  for (int k = 0; k < MAXG; ++k) {
-    const int gi = wave + 4 * k;
-    yv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (gi < ngr) {
-      const int p = min(gi * 16 + r16, npix - 1);
-      const f16x8 zb = *reinterpret_cast<const f16x8*>(&tile[p * CP + 8 * q]);
-      yv[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, zb, yv[k], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < MAXG; ++k) {
-    const int gi = wave + 4 * k;
-    const int p = gi * 16 + r16;
-    if (gi < ngr && p < npix && q < 3) {             // lane holds taps 4q .. 4q+3 of pixel p
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * q + r < 9) ys[p * HYS + 4 * q + r] = yv[k][r];
-    }
-  }
-  __syncthreads();
-  const int b = (int)(s / Tn), t = (int)(s % Tn);
-  const int cls = classes ? classes[(int64_t)b * Tn + t] : t;
-  float* o = out + ((int64_t)b * Tout + cls) * HW + (int64_t)y0 * W;
-  for (int idx = tid; idx < rows * W; idx += 256) {
-    const int yy = idx / W, xx = idx - yy * W;
-    float acc = bias;
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) acc += ys[((yy + dy) * WP + xx + dx) * HYS + dy * 3 + dx];
-    o[idx] = acc;
-  }
-}
-
-// 1 = MFMA tap image (head_mfma_kernel), 0 = v_dot2c band (head_band_kernel, default): the MFMA form
-// cuts the VALU ~40 % but measured slower in the pipeline (0.315 vs 0.286 ms per step) -- the
-// kernel is bound by its staging (HBM rows + GroupNorm/ReLU/convert), and the tap image costs
-// two more barriers and an LDS pass
 int g_head_variant = 0;   // 2 = the band kernel with a runtime map width (A/B of the compile-time 96)
 
 }  // namespace
 
 extern "C" int catseg_conv_tile_rows(void) { return BM; }
 
-int catseg_conv3x3_lds(const CatsegConvArgs* a, hipStream_t st);    // conv_lds.hip
 int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st);   // conv_ring.hip
-int g_conv_mode = 2;   // 2 = row-ring kernel, 1 = LDS-tile kernel, 0 = im2col only
+int g_conv_mode = 2;   // 2 = row-ring kernel where it applies, 0 = im2col only
 CATSEG_KNOB(g_conv_mode, "conv_mode");
 CATSEG_KNOB(g_head_variant, "head_variant");
 
@@ -705,7 +581,7 @@ extern "C" int catseg_conv3x3_stats_tile(const CatsegConvArgs* a) {
     const int t = catseg_conv3x3_ring_tile(a);
     if (t) return t;
   }
-  return BM;   // the LDS-tile and im2col kernels emit 128-pixel partials
+  return BM;   // the im2col kernel emits 128-pixel partials
 }
 
 extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
@@ -733,7 +609,6 @@ extern "C" int catseg_conv3x3(const CatsegConvArgs* a, void* stream) {
   p.ksplit = 1; p.ws = nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (g_conv_mode >= 2 && catseg_conv3x3_ring(a, st) == 0) return catseg_launch_status("conv3x3_ring");
-  if (g_conv_mode >= 1 && catseg_conv3x3_lds(a, st) == 0) return catseg_launch_status("conv3x3_lds");
   const int ks = conv_ksplit(a);
   const int64_t Mtot = a->S * (int64_t)a->H * a->W;
   if (ks > 1 && a->workspace && a->workspace_bytes >= (int64_t)ks * Mtot * a->c_out * 4 && a->c_out % 4 == 0) {
@@ -776,20 +651,6 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                                       int dtype, void* stream) {
   CATSEG_CHECK(x && weight && out && C % 8 == 0 && C <= 256 && B > 0 && T > 0, "conv3x3_head: bad args");
   CATSEG_CHECK(!mean || (rstd && gamma && beta && cpg > 0 && C % cpg == 0), "conv3x3_head: bad GN args");
-  if (dtype == CATSEG_BF16 && C == 32 && W <= 128 && g_head_variant == 1) {
-    const size_t tile_b = (size_t)(HBR + 2) * (W + 2) * (C + 8) * 2, ys_b = (size_t)(HBR + 2) * (W + 2) * HYS * 4;
-    const size_t shm = 2 * C * 4 + std::max(tile_b, ys_b);
-    static bool configured_m = false;
-    if (!configured_m) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_mfma_kernel<32>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      configured_m = true;
-    }
-    hipLaunchKernelGGL(head_mfma_kernel<32>, dim3((unsigned)((H + HBR - 1) / HBR), (unsigned)(B * T)), dim3(256), shm,
-                       (hipStream_t)stream, (const bf16*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg,
-                       classes, T_out, out);
-    return catseg_launch_status("conv3x3_head");
-  }
   if (dtype == CATSEG_BF16 && C == 32 && W <= 128) {
     const size_t shb = 9 * C * 2 + 2 * C * 4 + (size_t)(HBR + 2) * (W + 2) * (C + 8) * 2;
     static bool configured = false;

@@ -253,7 +253,7 @@ int catseg_upconv3x3_stats_tile(void);
  * out[b][(y/2)*(W2/2) + x/2][((y%2)*2 + x%2)*cout + co].  bf16 g with 16 or 32 channels. */
 int catseg_upconv_addend(const void* g, int64_t B, int H2, int W2, int cin, const float* weight,
                          const float* tap_bias, int cout, float* out, int dtype, void* stream);
-/* Rows per conv tile of the im2col / LDS-tile kernels (128). */
+/* Rows per conv tile of the im2col kernel (128). */
 int catseg_conv_tile_rows(void);
 /* Pixels per GroupNorm partial ("tile") of the kernel catseg_conv3x3 picks for `args`:
  * stats is [S][H*W/tile][c_out/stats_cpg][2] (the row-ring kernel emits one partial per
