@@ -34,6 +34,7 @@ namespace {
 
 constexpr int NT = 256;          // 4 waves
 int g_ring_variant = 0;          // A/B tiling / band knobs (catseg_set_ring_variant; 0 = default)
+int g_ring_persist = 2;          // persistent workgroups over (slice, band) units: 2 = >= 4 units each (bands by that), 1 = one-unit band rule, 0 = one unit per workgroup
 
 struct RingP {
   const bf16* s1; int64_t s1_ss; int c1;
@@ -87,17 +88,15 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   const int wpx = wave % WPX, wco = wave / WPX;
   // UP with up_split > 1: workgroup `half` computes channel block half of every parity
   // (COW of the CO = COW * up_split channels per parity); the source ring is read per block
+  // Persistent over units (slice, band): workgroup g keeps channel block half = g % nsplit (its
+  // weights stay in registers) and walks units g / nsplit, + gridDim.x / nsplit, ...
   const int nsplit = UP ? p.up_split : 1;
-  const int64_t s = blockIdx.x / (p.bands * nsplit);
-  const int band = blockIdx.x % p.bands;
-  const int half = UP ? (int)((blockIdx.x / p.bands) % nsplit) : 0;
+  const int half = UP ? (int)(blockIdx.x % nsplit) : 0;
+  const int64_t nunits = p.S * p.bands, ustride = gridDim.x / nsplit;
   const int CO = COW * nsplit;                          // UP: channels per parity in the output map
   const int ch0 = wco * CO + half * COW;                // first weight row / addend channel of this wave
   const int HW = H * W;
   const int nchunks = HW / CH;
-  const int c_begin = band * p.chunks_per_band;
-  const int c_end = min(nchunks, c_begin + p.chunks_per_band);
-  if (c_begin >= c_end) return;
 
   // ---- weights of this wave's output channels, all taps, in registers ----
   // The trailing 16 channels of two taps share one K=32 step: lanes q < 2 carry tap 2p's
@@ -128,6 +127,19 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
       wt[tp][i] = *reinterpret_cast<s16x8*>(&u);
     }
   }
+  float bv[FN][4];                      // bias of this lane's output channels (0 without)
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[ch0 + 16 * i + 4 * q + r] : 0.f;
+
+  for (int64_t unit = blockIdx.x / nsplit; unit < nunits; unit += ustride) {
+  const int64_t s = unit / p.bands;
+  const int band = (int)(unit % p.bands);
+  const int c_begin = band * p.chunks_per_band;
+  const int c_end = min(nchunks, c_begin + p.chunks_per_band);
+  if (c_begin >= c_end) continue;       // uniform over the workgroup
+  // (the previous unit ended on a barrier after its last ring reads / GN-table reads)
   if (p.gmean) {
     const int ngroups = p.c1 / p.gcpg;
     for (int c = tid; c < p.c1; c += NT) {
@@ -136,11 +148,6 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
       gsh[c] = p.gbeta[c] - p.gmean[s * ngroups + c / p.gcpg] * sc;
     }
   }
-  float bv[FN][4];                      // bias of this lane's output channels (0 without)
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[ch0 + 16 * i + 4 * q + r] : 0.f;
   const bf16* s1base = p.s1 + s * p.s1_ss;
   const bf16* s2base = p.s2 ? p.s2 + (s / p.s2_div) * p.s2_ss : nullptr;
 
@@ -381,6 +388,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     loaded_to += nnew > 0 ? nnew : 0;
     __syncthreads();
   }
+  }   // units
 }
 
 template <int C>
@@ -399,22 +407,31 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   const int base = p.W >= 64 ? 6144 : 3072;
   const int per_band = (g_ring_variant == 3 ? base / 2 : g_ring_variant == 4 ? base * 2 : base) / CH;
   int bands = (nchunks + per_band - 1) / per_band;
-  while (p.S * bands < 2048 && bands * 4 <= nchunks) bands *= 2;
+  const size_t sh = ring_lds<C>(p.W, NR);
+  const int nsplit = UP ? p.up_split : 1;
+  // persistent grid: the workgroups that fit at once (OCC per CU, LDS permitting), a multiple of
+  // nsplit; g_ring_persist 0 = one unit per workgroup (A/B)
+  const int per_cu = std::max(1, std::min(OCC, (int)((160 * 1024) / std::max<size_t>(sh, 1))));
+  const int64_t cap = (int64_t)(256 * per_cu / nsplit) * nsplit;
+  // enough units for every workgroup: >= 2048 workgroups when each takes one unit, >= 4 units
+  // per workgroup when persistent (ring_persist 2; 1 keeps the one-unit band rule)
+  const int64_t want = g_ring_persist == 2 ? 4 * cap / nsplit : 2048;
+  while (p.S * bands < want && bands * 4 <= nchunks) bands *= 2;
   p.bands = bands;
   p.chunks_per_band = (nchunks + bands - 1) / bands;
-  const size_t sh = ring_lds<C>(p.W, NR);
   static size_t configured = 0;
   if (sh > configured) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
-  const int nsplit = UP ? p.up_split : 1;
   if (nsplit < 1 || nsplit > 4 || (COUT / WCO) % 16 != 0 || ((int64_t)p.H * p.W) % CH != 0 || (WFIX > 0 && p.W != WFIX)) {
     catseg_set_error("conv ring: bad channel split %d or H*W %% %d != 0", nsplit, CH);
     return -1;
   }
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>), dim3((unsigned)(p.S * bands * nsplit)),
+  int64_t grid = p.S * bands * nsplit;
+  if (g_ring_persist) grid = std::min(grid, cap);
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>), dim3((unsigned)grid),
                      dim3(NT), sh, st, p);
   return 0;
 }
@@ -645,6 +662,7 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
 }
 
 CATSEG_KNOB(g_ring_variant, "ring_variant");
+CATSEG_KNOB(g_ring_persist, "ring_persist");
 
 // ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
 // The conv over the ConvTranspose output y (2H x 2W, no nonlinearity between them) equals, per
