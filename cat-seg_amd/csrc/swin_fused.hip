@@ -278,13 +278,25 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
   }
 }
 
-int g_swin_variant = 0;   // 0 = head-per-SIMD (swin_window.hip), else the row-tile-wave kernel (swin_fused2_kernel)
+// 0 = head-per-SIMD kernel (swin_window.hip swin_win3) with the opaque (inline-asm) LDS-DMA and the
+// per-window guidance base, 1 = the same with the builtin LDS-DMA and a row map per tile,
+// 2 = the row-tile-wave kernel (swin_fused2_kernel).  (A barrier-free form with two 4-wave
+// workgroups per CU, every head wave LayerNorming its window's rows itself, measured 314 / 410 us
+// vs 259 / 271 us: the per-wave load -> LayerNorm -> MFMA chains left their latency exposed.)
+int g_swin_variant = 0;
 
 }  // namespace
 
 CATSEG_KNOB(g_swin_variant, "swin_variant");
 
-int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st);   // swin_window.hip
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin);   // swin_window.hip
+
+// the guidance row map restricted to one slice is rowmap(slice * 576) + pixel (swin_win3 then adds the pixel)
+static bool gmap_linear_in_pixel(const CatsegRowMap& m) {
+  const int64_t P = IMG * IMG;
+  return (m.d2 == 1 && m.s2 == 1 && m.m2 % P == 0 && m.d1 % P == 0) ||
+         (m.d1 == 1 && m.s1 == 1 && m.m1 % P == 0 && m.d2 % P == 0);
+}
 
 extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->x && a->ln_g && a->ln_b && a->w_qkv && a->b_qkv && a->gqk && a->out,
@@ -313,8 +325,8 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   }
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (g_swin_variant == 0) {
-    swin_win3_launch(a, n_cu, (hipStream_t)stream);
+  if (g_swin_variant <= 1) {
+    swin_win3_launch(a, n_cu, (hipStream_t)stream, g_swin_variant == 0, g_swin_variant == 0 && gmap_linear_in_pixel(a->gmap));
   } else {
     if (a->shift > 0)
       hipLaunchKernelGGL(swin_fused2_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);

@@ -50,6 +50,7 @@ struct Swin3P {
   const bf16* g; int64_t ld_g; RowMap gmap;
   bf16* out; int64_t ld_out;
   int shift; float scale;
+  int glin;     // gmap restricted to a slice is rowmap(slice * 576) + pixel
 };
 
 // 16-byte chunk c of row r of a chunk-major image with ROWS rows, row XOR swizzle in the low 4 bits
@@ -78,7 +79,15 @@ DEV f32x4 unpack4(uint2 u) {
                __uint_as_float(u.y & 0xffff0000u)};
 }
 
-template <bool SWM>
+// LDS-DMA issued from inline asm: the compiler does not see it, so it does not make every later LDS
+// read wait (s_waitcnt vmcnt(0)) for the next window's rows in flight -- with the builtin, P3's first
+// K-fragment read waited for the whole prefetch, and the window start for every P3 store.  The
+// kernel retires the DMA itself (counted vmcnt at the window start).
+DEV void dma16_opaque(const void* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
+
+template <bool SWM, bool ASMDMA>
 __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 Ks[NH][4 * L * 8];       // [head][chunk][key] (chunk-major)
@@ -126,16 +135,37 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
     for (int k = wave; k < NDMA; k += NW) {
       const int sl = k * 64 + lane, c = sl / L, i = (sl % L) ^ (c & 15);
       const bf16* src = p.x + (int64_t)win_row3(slice, wloc, i, p.shift) * p.ld_x + c * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(Xn + k * 64 * 8), 16, 0, 0);
+      if constexpr (ASMDMA)
+        dma16_opaque(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xn + k * 64 * 8)));
+      else
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Xn + k * 64 * 8), 16, 0, 0);
     }
   };
   int win = blockIdx.x;
   if (win < nwin_total) fetch(win);
   for (; win < nwin_total; win += gridDim.x) {
     const int slice = win / NWIN, wloc = win % NWIN;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's DMA (and stores) landed
+    // this wave's DMA of the window landed: after the first window only the P3 stores (2 per
+    // row tile, >= 8 per wave) were issued behind it, and those may stay in flight
+    if (!ASMDMA || win == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();                                       // every wave's DMA visible; P3 done
+    // guidance row of token rb + r16 of this window: rowmap(slice*576) + pixel when the host
+    // found the map linear in the pixel (CAT-Seg's (b, t, p) -> (b, p)), else the general map
+    const int64_t gbase = p.glin ? rowmap(p.gmap, (int64_t)slice * (IMG * IMG)) : 0;
+    auto fetch_g = [&](int t, uint2 (&gd)[2][2]) {
+      const int row = win_row3(slice, wloc, 16 * t + r16, p.shift);
+      const int64_t grow = p.glin ? gbase + (row - slice * (IMG * IMG)) : rowmap(p.gmap, row);
+      const bf16* gp = p.g + grow * p.ld_g + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        gd[0][dt] = *reinterpret_cast<const uint2*>(gp + dt * 16);
+        gd[1][dt] = *reinterpret_cast<const uint2*>(gp + C + dt * 16);
+      }
+    };
+    uint2 gc[2][2];
+    fetch_g(sub, gc);
     // ---------------- P1: LayerNorm of Xn in place ----------------
     {
       const float4 g0 = *reinterpret_cast<const float4*>(&sP[lc * 8]), g1 = *reinterpret_cast<const float4*>(&sP[lc * 8 + 4]);
@@ -183,24 +213,24 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
       }
     }
     s16x8 qf[MYT];
+    // guidance rows of row tile sub + 2j (q, k halves of head h): tile j+1's are in flight during
+    // tile j, tile 0's were requested before P1
 #pragma unroll
     for (int j = 0; j < MYT; ++j) {
       const int t = sub + 2 * j;
       if (t < NTILE) {
         const int rb = 16 * t;
+        uint2 gn[2][2];
+        if (j + 1 < MYT && t + 2 < NTILE) fetch_g(t + 2, gn);
         s16x8 xb[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(( (ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
-        const int grow = (int)rowmap(p.gmap, win_row3(slice, wloc, rb + r16, p.shift));
-        const bf16* gp = p.g + (int64_t)grow * p.ld_g + h * D + 4 * g;
         f32x4 dq[2], dk[2], dv[2];
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           // accumulators start at bias + guidance (q, k: features 16dt + 4g + r of token r16) / bias (v)
-          dq[dt] = *reinterpret_cast<const f32x4*>(&sP[2 * C + h * D + dt * 16 + 4 * g]) +
-                   unpack4(*reinterpret_cast<const uint2*>(gp + dt * 16));
-          dk[dt] = *reinterpret_cast<const f32x4*>(&sP[3 * C + h * D + dt * 16 + 4 * g]) +
-                   unpack4(*reinterpret_cast<const uint2*>(gp + C + dt * 16));
+          dq[dt] = *reinterpret_cast<const f32x4*>(&sP[2 * C + h * D + dt * 16 + 4 * g]) + unpack4(gc[0][dt]);
+          dk[dt] = *reinterpret_cast<const f32x4*>(&sP[3 * C + h * D + dt * 16 + 4 * g]) + unpack4(gc[1][dt]);
           const float bvv = sP[4 * C + h * D + dt * 16 + r16];
           dv[dt] = f32x4{bvv, bvv, bvv, bvv};
         }
@@ -219,6 +249,10 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
         for (int dt = 0; dt < 2; ++dt)
           *reinterpret_cast<uint2*>(&Vt[h][(dt * 16 + r16) * VP + rb + 4 * g]) =
               make_uint2(f2bf2(dv[dt][0], dv[dt][1]), f2bf2(dv[dt][2], dv[dt][3]));
+#pragma unroll
+        for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) gc[a2][dt] = gn[a2][dt];
       }
       __builtin_amdgcn_sched_barrier(0);        // no cross-tile hoisting (register pressure)
     }
@@ -286,8 +320,9 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
 }  // namespace
 
 // launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
-int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st) {
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin) {
   Swin3P p;
+  p.glin = glin ? 1 : 0;
   p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
   p.ln_g = a->ln_g; p.ln_b = a->ln_b; p.eps = a->eps;
   p.w = (const bf16*)a->w_qkv; p.bias = a->b_qkv;
@@ -297,7 +332,12 @@ int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st) {
   p.shift = a->shift; p.scale = a->scale;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (a->shift > 0) hipLaunchKernelGGL(swin_win3_kernel<true>, grid, dim3(NT), 0, st, p, nwin_total);
-  else hipLaunchKernelGGL(swin_win3_kernel<false>, grid, dim3(NT), 0, st, p, nwin_total);
+  if (asm_dma) {
+    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, true>), grid, dim3(NT), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win3_kernel<false, true>), grid, dim3(NT), 0, st, p, nwin_total);
+  } else {
+    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, false>), grid, dim3(NT), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win3_kernel<false, false>), grid, dim3(NT), 0, st, p, nwin_total);
+  }
   return 0;
 }
