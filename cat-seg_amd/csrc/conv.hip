@@ -555,7 +555,110 @@ __global__ __launch_bounds__(256) void head_band_kernel(const bf16* __restrict__
   }
 }
 
-int g_head_variant = 0;   // 2 = the band kernel with a runtime map width (A/B of the compile-time 96)
+// ---------------- head conv, MFMA tap products (bf16 input, C = 32, W = 96) ---------------
+// out[y][x] = bias + sum_{dy,dx} D[y+dy-1][x+dx-1][3 dy + dx],  D[p][tap] = relu(GN(x[p])) . w[tap]:
+// one v_mfma_f32_16x16x32_f16 per 16 input pixels computes all 9 tap products of every pixel
+// (A = the 16 pixels' 32 channels straight from a 16-byte load per lane, GroupNorm+ReLU applied
+// in fp32 and rounded to fp16 as the band kernel does; B = the 9 weight rows, zero columns 9-15),
+// and each input element is read ONCE per band (no per-tap re-reads, no fp16 staging image).  A
+// workgroup walks the input rows of one band (RB output rows of a slice + 2 halo rows) two rows
+// per step; the D rows go to a 6-row LDS ring [row][tap][x] (4 zero columns each side) and the
+// output rows whose three D rows are complete are summed there (9 LDS reads per output).  Loads
+// of step k+1 are in flight during step k (registers); one barrier per step.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+constexpr int HT_W = 96, HT_TPR = HT_W / 16, HT_NR = 6, HT_WP = HT_W + 8;
+constexpr int HT_TPS = 2 * HT_TPR / 4;      // 16-pixel tiles per wave per step (two rows, 4 waves)
+
+__global__ __launch_bounds__(256) void head_tap_kernel(const bf16* __restrict__ x, int Tn, int H, const float* __restrict__ w,
+                                                       float bias, const float* mean, const float* rstd,
+                                                       const float* gamma, const float* beta, int cpg,
+                                                       const int32_t* classes, int Tout, float* out, int RB,
+                                                       int ups, int nunits) {
+  constexpr int C = 32;
+  __shared__ __attribute__((aligned(16))) float ring[HT_NR][9][HT_WP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  for (int i = tid; i < HT_NR * 9 * HT_WP; i += 256) (&ring[0][0][0])[i] = 0.f;   // pad columns stay zero
+  // B operand: W[tap r16][channels 8g .. 8g+7] (taps 9..15 zero)
+  h8 wb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wb[j] = r16 < 9 ? (_Float16)w[r16 * C + 8 * g + j] : (_Float16)0.f;
+  const int groups = C / cpg;
+  const int64_t HW = (int64_t)H * HT_W;
+  __syncthreads();
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const int s = u / ups, y0 = (u - s * ups) * RB, y1 = min(H, y0 + RB);
+    const int nin = y1 - y0 + 2;                     // input rows y0 - 1 .. y1
+    const int nsteps = (nin + 1) >> 1;
+    // GroupNorm affine of this lane's channels 8g .. 8g+7 (slice s)
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * g + j;
+      if (mean) {
+        const float a = rstd[(int64_t)s * groups + c / cpg] * gamma[c];
+        sc[j] = a;
+        sh[j] = beta[c] - mean[(int64_t)s * groups + c / cpg] * a;
+      } else {
+        sc[j] = 1.f;
+        sh[j] = 0.f;
+      }
+    }
+    const bf16* xs = x + (int64_t)s * HW * C;
+    // tile j of step k: input row i = 2k + (tile / TPR), pixels 16 (tile % TPR) + r16
+    auto load = [&](int k, uint4 (&v)[HT_TPS]) {
+#pragma unroll
+      for (int j = 0; j < HT_TPS; ++j) {
+        const int tile = wave * HT_TPS + j, i = 2 * k + tile / HT_TPR, yy = y0 - 1 + i;
+        const int xx = (tile % HT_TPR) * 16 + r16;
+        const bool in = i < nin && yy >= 0 && yy < H;
+        v[j] = ld16(xs + ((int64_t)(in ? yy : 0) * HT_W + xx) * C + 8 * g);
+      }
+    };
+    uint4 cur[HT_TPS], nxt[HT_TPS];
+    load(0, cur);
+    const int b = s / Tn, t = s - b * Tn;
+    const int cls = classes ? classes[(int64_t)b * Tn + t] : t;
+    float* o = out + ((int64_t)b * Tout + cls) * HW;
+    for (int k = 0; k < nsteps; ++k) {
+      if (k + 1 < nsteps) load(k + 1, nxt);
+#pragma unroll
+      for (int j = 0; j < HT_TPS; ++j) {
+        const int tile = wave * HT_TPS + j, i = 2 * k + tile / HT_TPR, yy = y0 - 1 + i;
+        const int x0 = (tile % HT_TPR) * 16;
+        const bool in = i < nin && yy >= 0 && yy < H;       // wave-uniform
+        const bf16* e = reinterpret_cast<const bf16*>(&cur[j]);
+        h8 a;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = (_Float16)(in ? fmaxf(fmaf(bf2f(e[q]), sc[q], sh[q]), 0.f) : 0.f);
+        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, wb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // D[pixel x0 + 4g + r][tap r16]
+        if (r16 < 9) *reinterpret_cast<f32x4*>(&ring[(i % HT_NR)][r16][4 + x0 + 4 * g]) = d;
+      }
+      __syncthreads();
+      // outputs whose rows y-1, y, y+1 are in: y - y0 + 2 <= 2k + 1
+      const int ylo = max(y0, y0 + 2 * k - 2), yhi = min(y1, y0 + 2 * k);
+      for (int idx = tid; idx < (yhi - ylo) * HT_W; idx += 256) {
+        const int yy = ylo + idx / HT_W, xx = idx % HT_W, i0 = yy - y0;   // rows i0, i0+1, i0+2
+        float acc = bias;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const float* rr = &ring[(i0 + dy) % HT_NR][3 * dy][3 + xx];
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) acc += rr[dx * HT_WP + dx];
+        }
+        o[(int64_t)yy * HT_W + xx] = acc;
+      }
+#pragma unroll
+      for (int j = 0; j < HT_TPS; ++j) cur[j] = nxt[j];
+    }
+    __syncthreads();                                 // the ring is rewritten by the next unit
+  }
+}
+
+// 0 = MFMA tap-product kernel at W = 96 (head_tap_kernel), 1 = the v_dot2c band kernel with the
+// compile-time width 96, 2 = the band kernel with a runtime width
+int g_head_variant = 0;
 
 }  // namespace
 
@@ -659,7 +762,20 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       configured = true;
     }
-    if (W == 96 && g_head_variant != 2) {
+    if (W == 96 && g_head_variant == 0) {
+      static int n_cu = 0;
+      if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+          n_cu = 256;
+      }
+      const int RB = 24, ups = (H + RB - 1) / RB;
+      const int64_t nunits = B * (int64_t)T * ups;
+      CATSEG_CHECK(nunits < (1LL << 31), "conv3x3_head: too many bands");
+      const unsigned grid = (unsigned)std::min<int64_t>(nunits, 4LL * n_cu);
+      hipLaunchKernelGGL(head_tap_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, T, H, weight, bias,
+                         mean, rstd, gamma, beta, cpg, classes, T_out, out, RB, ups, (int)nunits);
+    } else if (W == 96 && g_head_variant != 2) {
       static bool configured96 = false;
       if (!configured96) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_band_kernel<32, 96>),

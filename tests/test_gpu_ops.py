@@ -1113,12 +1113,12 @@ def test_mlp_pair_order_bit_identical(act):
     assert torch.equal(outs[1][1], outs[0][1]), (outs[1][1].float() - outs[0][1].float()).abs().max().item()
 
 
-@pytest.mark.parametrize("H,W", [(96, 96), (50, 37)])
+@pytest.mark.parametrize("H,W", [(96, 96), (50, 96), (50, 37)])
 def test_head_conv_band(H, W):
-    """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load): the v_dot2c band kernel
-    (head_variant 0, the default; compile-time width at W = 96) vs fp64, with the top-k class
-    scatter; ragged band (H % 8 != 0) included; variant 2 (runtime width) equals variant 0 bit for
-    bit."""
+    """The head conv (model.py:634, 32 -> 1, 3x3, GroupNorm+ReLU on load) vs fp64, with the top-k
+    class scatter: at W = 96 the MFMA tap-product kernel (head_variant 0, the default; 24-row bands,
+    ragged last band at H = 50) and the v_dot2c band kernel with the compile-time width (variant 1),
+    which equals the runtime-width band kernel (variant 2, also the W = 37 path) bit for bit."""
     B, T, C = 2, 3, 32
     S = B * T
     lib = L.load()
@@ -1133,22 +1133,25 @@ def test_head_conv_band(H, W):
     rh = F.conv2d(y1, hw_.double(), torch.tensor([0.25]).double(), padding=1).reshape(B, T, H, W)
     xin = xb.permute(0, 2, 3, 1).contiguous().to(dev)
     cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
-    outs = []
-    for v in (0, 2):
-        L.tune("head_variant", v)
-        logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
-        ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
-                         bias=0.25, out=logits, T_out=T + 2, classes=cls,
-                         gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16))
-        outs.append(logits.cpu())
-    L.tune("head_variant", 0)
-    for bi in range(B):
-        for t in range(T):
-            # fp16 staging of relu(GN(x)): ~5e-4 per product, 288 terms
-            close(outs[0][bi, cls[bi, t]], rh[bi, t], atol=6e-3, what="head band vs fp64")
-    assert (outs[0] == -100.0).sum() == B * 2 * H * W        # the unselected class planes stay untouched
+    outs = {}
+    try:
+        for v in (0, 1, 2):
+            L.tune("head_variant", v)
+            logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
+            ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
+                             bias=0.25, out=logits, T_out=T + 2, classes=cls,
+                             gn=(mean.to(dev), rstd.to(dev), gam.to(dev), bet.to(dev), 16))
+            outs[v] = logits.cpu()
+    finally:
+        L.tune("head_variant", 0)
+    for v in (0, 1):
+        for bi in range(B):
+            for t in range(T):
+                # fp16 relu(GN(x)) operands: ~5e-4 per product, 288 terms
+                close(outs[v][bi, cls[bi, t]], rh[bi, t], atol=6e-3, what=f"head variant {v} vs fp64")
+        assert (outs[v] == -100.0).sum() == B * 2 * H * W        # the unselected class planes stay untouched
     # the band kernel with the compile-time width (W = 96) is the runtime-width one, bit for bit
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[1], outs[2])
 
 
 @pytest.mark.parametrize("M", [2 * 577 + 9, 300 * 32 + 17, 40])
