@@ -345,7 +345,138 @@ __global__ __launch_bounds__(256) void sliding_merge_stage_kernel(const float* _
   }
 }
 
-int g_merge_variant = 0;   // 0 = tile rows staged in LDS where nb <= 2 (sliding_merge_stage_kernel), 1 = band kernel
+// The staged merge with the per-row interpolation terms tabulated once per workgroup (the row-side
+// lin_src of the global map and of both tile rows is uniform over a band row: computed per output
+// by every thread it was ~25 VALU of ~70) and the band's 16 x 640 outputs split evenly over the
+// threads (columns t and t + 256 for all rows, column 512 + t % 128 for half the rows: 40 each;
+// the column-per-thread walk gave 128 threads 48 outputs and 128 threads 32).  Same taps, blend,
+// sigmoid and Fold order as sliding_merge_stage_kernel: bit-identical.  nb == 2, out_res <= 768.
+__global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __restrict__ lg, int T, int h, int w,
+                                                                int k, int stride, int out_res, int bands, int grows,
+                                                                int trows, float* __restrict__ out) {
+  extern __shared__ float smem_m[];
+  float* gsig = smem_m;                        // [grows][k]
+  float* tsl = smem_m + grows * k;             // [2 tile rows][2 tile cols][trows][w]
+  __shared__ int ti[MERGE_BY][6];              // gy0, gy1 (rel. r_lo); per tile row bi: ty0, ty1 (rel.), or -1
+  __shared__ float tf[MERGE_BY][3];            // gly, tly[0], tly[1]
+  constexpr int nb = 2, L = nb * nb + 1;
+  const int64_t nt = blockIdx.x / bands;
+  const int band = blockIdx.x % bands;
+  const int t = (int)(nt % T);
+  const int64_t n = nt / T;
+  const int Y0 = band * MERGE_BY, Y1 = min(Y0 + MERGE_BY, out_res);
+  const float sg = (float)k / (float)out_res, st_ = (float)h / (float)k;
+  int r_lo, r_hi, tmp;
+  float tl;
+  lin_src(Y0, k, sg, r_lo, tmp, tl);
+  lin_src(Y1 - 1, k, sg, tmp, r_hi, tl);
+  const int nr = r_hi - r_lo + 1;
+  const int64_t plane = (int64_t)h * w;
+  const float* gp = lg + ((n * L + L - 1) * T + t) * plane;
+  for (int idx = threadIdx.x; idx < nr * k; idx += blockDim.x) {
+    const int r = r_lo + idx / k, x = idx % k;
+    gsig[idx] = up_sig_fast(gp, h, w, k, r, x);
+  }
+  int tlo[2] = {0, 0};
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    const int ya = max(Y0, stride * bi), yb = min(Y1, stride * bi + k) - 1;
+    if (ya > yb) continue;
+    int a0, a1, b0, b1;
+    float la;
+    lin_src(ya - stride * bi, h, st_, a0, a1, la);
+    lin_src(yb - stride * bi, h, st_, b0, b1, la);
+    tlo[bi] = a0;
+    const int rows = b1 - a0 + 1;
+    for (int bj = 0; bj < nb; ++bj) {
+      const float* pl = lg + ((n * L + bi * nb + bj) * T + t) * plane + (int64_t)a0 * w;
+      float* dst = tsl + (bi * 2 + bj) * trows * w;
+      for (int i = threadIdx.x; i < rows * w; i += blockDim.x) dst[i] = pl[i];
+    }
+  }
+  if (threadIdx.x < Y1 - Y0) {
+    const int Y = Y0 + threadIdx.x;
+    int y0, y1;
+    float ly;
+    lin_src(Y, k, sg, y0, y1, ly);
+    ti[threadIdx.x][0] = (y0 - r_lo) * k;
+    ti[threadIdx.x][1] = (y1 - r_lo) * k;
+    tf[threadIdx.x][0] = ly;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) {
+      const int yy = Y - stride * bi;
+      if (yy < 0 || yy >= k) {
+        ti[threadIdx.x][2 + 2 * bi] = -1;
+        ti[threadIdx.x][3 + 2 * bi] = -1;
+        tf[threadIdx.x][1 + bi] = 0.f;
+      } else {
+        int ty0, ty1;
+        float tly;
+        lin_src(yy, h, st_, ty0, ty1, tly);
+        ti[threadIdx.x][2 + 2 * bi] = (ty0 - tlo[bi]) * w;
+        ti[threadIdx.x][3 + 2 * bi] = (ty1 - tlo[bi]) * w;
+        tf[threadIdx.x][1 + bi] = tly;
+      }
+    }
+  }
+  __syncthreads();
+  float* ob = out + nt * (int64_t)out_res * out_res;
+  // this thread's columns: X = tid + 256 c for c < C0 over every band row, then one more column
+  // of the remainder over half the rows when out_res % 256 != 0
+  const int full = out_res / 256, rem = out_res % 256;
+  const int nrow = Y1 - Y0;
+  const int ncols = full + (rem ? 1 : 0);
+  for (int c = 0; c < ncols; ++c) {
+    int X, ya, yb;
+    if (c < full) {
+      X = threadIdx.x + 256 * c; ya = 0; yb = nrow;
+    } else {
+      // rem columns x (256 / rem) row groups share the 256 threads
+      const int groups = 256 / rem, gi = threadIdx.x / rem;
+      if (gi >= groups) break;
+      X = 256 * full + threadIdx.x % rem;
+      const int per = (nrow + groups - 1) / groups;
+      ya = gi * per; yb = min(nrow, ya + per);
+    }
+    int gx0, gx1;
+    float glx;
+    lin_src(X, k, sg, gx0, gx1, glx);
+    int tx0[2], tx1[2], tbj[2];
+    float tlx[2];
+    int ncol = 0;
+#pragma unroll
+    for (int bj = 0; bj < nb; ++bj) {
+      const int xx = X - stride * bj;
+      if (xx < 0 || xx >= k) continue;
+      lin_src(xx, w, (float)w / (float)k, tx0[ncol], tx1[ncol], tlx[ncol]);
+      tbj[ncol++] = bj;
+    }
+#pragma unroll 4
+    for (int yi = ya; yi < yb; ++yi) {
+      const float* g0 = gsig + ti[yi][0];
+      const float* g1 = gsig + ti[yi][1];
+      const float glob = blend(g0[gx0], g0[gx1], g1[gx0], g1[gx1], tf[yi][0], glx);
+      float sum = 0.f, cnt = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < nb; ++bi) {
+        const int o0 = ti[yi][2 + 2 * bi];
+        if (o0 < 0) continue;
+        const int o1 = ti[yi][3 + 2 * bi];
+        const float tly = tf[yi][1 + bi];
+        for (int cc = 0; cc < ncol; ++cc) {
+          const float* pl = tsl + (bi * 2 + tbj[cc]) * trows * w;
+          sum += sigm_fast(blend(pl[o0 + tx0[cc]], pl[o0 + tx1[cc]], pl[o1 + tx0[cc]], pl[o1 + tx1[cc]], tly, tlx[cc]));
+          cnt += 1.f;
+        }
+      }
+      ob[(int64_t)(Y0 + yi) * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
+    }
+  }
+}
+
+// 0 = staged merge with tabulated row terms and balanced columns (sliding_merge_tab_kernel, nb == 2),
+// 1 = band kernel, 2 = staged merge (sliding_merge_stage_kernel)
+int g_merge_variant = 0;
 
 }  // namespace
 
@@ -406,7 +537,12 @@ extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h
     // tile-plane rows under one band: (MERGE_BY - 1) output rows span (MERGE_BY - 1) h / k source rows
     const int trows = (int)((int64_t)(MERGE_BY - 1) * h / kernel) + 3;
     const size_t sh2 = ((size_t)rows * kernel + (size_t)4 * trows * w) * sizeof(float);
-    if (g_merge_variant == 0 && nb <= 2 && sh2 <= 64 * 1024) {
+    if (g_merge_variant == 0 && nb == 2 && sh2 <= 64 * 1024 && out_res <= 768) {
+      hipLaunchKernelGGL(sliding_merge_tab_kernel, dim3((unsigned)blocks), dim3(256), sh2, (hipStream_t)stream, logits,
+                         T, h, w, kernel, stride, out_res, bands, rows, trows, out);
+      return catseg_launch_status("sliding_merge");
+    }
+    if (g_merge_variant != 1 && nb <= 2 && sh2 <= 64 * 1024) {
       hipLaunchKernelGGL(sliding_merge_stage_kernel, dim3((unsigned)blocks), dim3(256), sh2, (hipStream_t)stream, logits,
                          T, h, w, kernel, stride, nb, out_res, bands, rows, trows, out);
       return catseg_launch_status("sliding_merge");

@@ -896,16 +896,18 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
         glob = F.interpolate(o[-1:], size=[res, res], mode="bilinear", align_corners=False)
         t = fold(o[:-1].flatten(1).T) / fold(unfold(torch.ones([1, res, res])))
         close(merged[i], ((t + glob) / 2.0)[0], atol=1e-5, what=f"merge {i}")
-    # the LDS-staged merge (variant 0, default) equals the band kernel gathering from global (1)
+    # the tabulated staged merge (variant 0, default) equals the band kernel gathering from global (1)
+    # and the staged merge computing the row terms per output (2)
     lib = L.load()
-    merged1 = torch.empty_like(merged)
-    try:
-        L.tune("merge_variant", 1)
-        ops.sliding_merge(lg.to(dev), merged1, kernel=k, stride=stride, out_res=res)
-        torch.cuda.synchronize()
-    finally:
-        L.tune("merge_variant", 0)
-    assert torch.equal(merged, merged1)
+    for v in (1, 2):
+        merged1 = torch.empty_like(merged)
+        try:
+            L.tune("merge_variant", v)
+            ops.sliding_merge(lg.to(dev), merged1, kernel=k, stride=stride, out_res=res)
+            torch.cuda.synchronize()
+        finally:
+            L.tune("merge_variant", 0)
+        assert torch.equal(merged, merged1), v
     out = torch.empty(1, T, 480, 400, device=dev)
     ops.resize_bilinear(merged[:1], out, crop=(res, res))
     ref = F.interpolate(merged[:1].cpu(), size=(480, 400), mode="bilinear", align_corners=False)
