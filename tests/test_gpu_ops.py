@@ -309,7 +309,7 @@ def test_attention_dense(dt, L_, H, causal):
     close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8, 10])
 def test_attention_dense_tilings(variant):
     """Every A/B tiling of the dense path (tuning knob attn_variant) == the default tiling."""
     B, L_, H, d = 2, 577, 4, 64
