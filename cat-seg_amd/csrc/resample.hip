@@ -350,7 +350,8 @@ __global__ __launch_bounds__(256) void sliding_merge_stage_kernel(const float* _
 // by every thread it was ~25 VALU of ~70) and the band's 16 x 640 outputs split evenly over the
 // threads (columns t and t + 256 for all rows, column 512 + t % 128 for half the rows: 40 each;
 // the column-per-thread walk gave 128 threads 48 outputs and 128 threads 32).  Same taps, blend,
-// sigmoid and Fold order as sliding_merge_stage_kernel: bit-identical.  nb == 2, out_res <= 768.
+// sigmoid and Fold order as sliding_merge_stage_kernel (the blends' FMA contraction may differ by
+// an ulp).  nb == 2, out_res <= 768.
 __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __restrict__ lg, int T, int h, int w,
                                                                 int k, int stride, int out_res, int bands, int grows,
                                                                 int trows, float* __restrict__ out) {

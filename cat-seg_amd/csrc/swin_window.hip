@@ -87,7 +87,10 @@ DEV void dma16_opaque(const void* src, unsigned lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
 }
 
-template <bool SWM, bool ASMDMA>
+// STAMP (diagnostics, swin_variant 16): wave-lane-0 s_memtime stamps at the phase boundaries of the
+// first 4 windows of every wave, written PAST the last output row (the caller allocates
+// grid x 8 x 32 x 8 bytes more: tools/stamps_swin.py)
+template <bool SWM, bool ASMDMA, bool STAMP = false>
 __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 Ks[NH][4 * L * 8];       // [head][chunk][key] (chunk-major)
@@ -144,13 +147,21 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
   };
   int win = blockIdx.x;
   if (win < nwin_total) fetch(win);
-  for (; win < nwin_total; win += gridDim.x) {
+  uint64_t* stp = reinterpret_cast<uint64_t*>(p.out + (int64_t)(nwin_total / NWIN) * IMG * IMG * p.ld_out) +
+                  ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * 32;
+  int it = 0;
+  auto stamp = [&](int k) {
+    if (STAMP && (threadIdx.x & 63) == 0 && it < 4) stp[it * 8 + k] = __builtin_amdgcn_s_memtime();
+  };
+  for (; win < nwin_total; win += gridDim.x, ++it) {
     const int slice = win / NWIN, wloc = win % NWIN;
+    stamp(0);
     // this wave's DMA of the window landed: after the first window only the P3 stores (2 per
     // row tile, >= 8 per wave) were issued behind it, and those may stay in flight
     if (!ASMDMA || win == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();                                       // every wave's DMA visible; P3 done
+    stamp(1);
     // guidance row of token rb + r16 of this window: rowmap(slice*576) + pixel when the host
     // found the map linear in the pixel (CAT-Seg's (b, t, p) -> (b, p)), else the general map
     const int64_t gbase = p.glin ? rowmap(p.gmap, (int64_t)slice * (IMG * IMG)) : 0;
@@ -193,7 +204,9 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
           st16(&Xn[cs<L>(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
       }
     }
+    stamp(2);
     __syncthreads();
+    stamp(3);
     // ---------------- P2: q / k / v of head h for row tiles sub, sub + 2, ... ----------------
     if constexpr (SWM) {   // region one-hot of the keys (P3 of the previous window has retired its reads)
       if (gridDim.x % NWIN != 0 || win == (int)blockIdx.x) {
@@ -256,7 +269,9 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
       }
       __builtin_amdgcn_sched_barrier(0);        // no cross-tile hoisting (register pressure)
     }
+    stamp(4);
     __syncthreads();
+    stamp(5);
     // ---------------- P3: attention of head h for the same row tiles ----------------
     if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);   // Xn is free: P2 is done everywhere
     const bool masked = SWM && wloc != 0;       // window location 0 holds a single region
@@ -314,13 +329,14 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
             make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
       __builtin_amdgcn_sched_barrier(0);
     }
+    stamp(6);
   }
 }
 
 }  // namespace
 
 // launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
-int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin) {
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin, bool stamps) {
   Swin3P p;
   p.glin = glin ? 1 : 0;
   p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
@@ -332,7 +348,10 @@ int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   p.shift = a->shift; p.scale = a->scale;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (asm_dma) {
+  if (stamps) {
+    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, true, true>), grid, dim3(NT), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win3_kernel<false, true, true>), grid, dim3(NT), 0, st, p, nwin_total);
+  } else if (asm_dma) {
     if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, true>), grid, dim3(NT), 0, st, p, nwin_total);
     else hipLaunchKernelGGL((swin_win3_kernel<false, true>), grid, dim3(NT), 0, st, p, nwin_total);
   } else {

