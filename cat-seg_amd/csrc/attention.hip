@@ -701,7 +701,6 @@ void launch_dense(const AttnP& p, hipStream_t st) {
     // measured before the remap: ring 10 waves 33.2, ring 5 waves x 2 query tiles 37.1,
     // 4 x 2 31.6 (the shared K / V^T fragment reads did not pay for the lost occupancy)
     if (g_attn_variant == 0) { launch_vit3<8, 1>(p, st); return; }
-    if (g_attn_variant == 10) { launch_vit3<10, 1>(p, st); return; }
     if (g_attn_variant == 8) { launch_vit<10>(p, st); return; }
   }
   switch (g_attn_variant) {

@@ -52,9 +52,12 @@ DEV s16x8 pack8(const f32x4& a, const f32x4& b) {
 DEV float ushort_f(const bf16* p) { return bf2f(*p); }
 
 // LNB: LayerNorm row steps (16 rows each) loaded per batch
-template <int LNB>
+// SB: the q / k / v biases read from LDS where used instead of held in 12 VGPRs (the kernel sits at
+// 256 VGPRs; its spill reloads, counted in vmcnt, drained the in-flight prefetches)
+template <int LNB, bool SB = true>
 __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
   __shared__ __attribute__((aligned(16))) bf16 xn[TMAX * C];
+  __shared__ __attribute__((aligned(16))) float sbias[SB ? 3 * C : 4];   // q | k | v bias
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
 
@@ -73,11 +76,15 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
   // prefetches issued before it); LayerNorm affine and padding projections are read where used
   float bk[2], bv[2];
   f32x4 bq[2];
+  if constexpr (SB) {
+    for (int i = tid; i < 3 * C; i += NT) sbias[i] = a.bias[i];   // first read after the LN barrier
+  } else {
 #pragma unroll
-  for (int ib = 0; ib < 2; ++ib) {
-    bk[ib] = a.bias[C + h * D + ib * 16 + r16];
-    bv[ib] = a.bias[2 * C + h * D + ib * 16 + r16];
-    bq[ib] = *reinterpret_cast<const f32x4*>(a.bias + h * D + ib * 16 + 4 * q);
+    for (int ib = 0; ib < 2; ++ib) {
+      bk[ib] = a.bias[C + h * D + ib * 16 + r16];
+      bv[ib] = a.bias[2 * C + h * D + ib * 16 + r16];
+      bq[ib] = *reinterpret_cast<const f32x4*>(a.bias + h * D + ib * 16 + 4 * q);
+    }
   }
   const float S = (float)(a.T + a.n_pad), invS = 1.f / S;
 
@@ -164,9 +171,11 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
       for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-          dk[tt][ib] = f32x4{__uint_as_float(g[ib][tt].x << 16) + bk[ib], __uint_as_float(g[ib][tt].x & 0xffff0000u) + bk[ib],
-                             __uint_as_float(g[ib][tt].y << 16) + bk[ib], __uint_as_float(g[ib][tt].y & 0xffff0000u) + bk[ib]};
-          dv[tt][ib] = f32x4{bv[ib], bv[ib], bv[ib], bv[ib]};
+          const float bkk = SB ? sbias[C + h * D + ib * 16 + r16] : bk[ib];
+          const float bvv = SB ? sbias[2 * C + h * D + ib * 16 + r16] : bv[ib];
+          dk[tt][ib] = f32x4{__uint_as_float(g[ib][tt].x << 16) + bkk, __uint_as_float(g[ib][tt].x & 0xffff0000u) + bkk,
+                             __uint_as_float(g[ib][tt].y << 16) + bkk, __uint_as_float(g[ib][tt].y & 0xffff0000u) + bkk};
+          dv[tt][ib] = f32x4{bvv, bvv, bvv, bvv};
         }
 #pragma unroll
       for (int kq = 0; kq < 4; ++kq) {
@@ -273,7 +282,8 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
         dq[ib] = f32x4{__uint_as_float(gq[ib].x << 16), __uint_as_float(gq[ib].x & 0xffff0000u),
-                       __uint_as_float(gq[ib].y << 16), __uint_as_float(gq[ib].y & 0xffff0000u)} + bq[ib];
+                       __uint_as_float(gq[ib].y << 16), __uint_as_float(gq[ib].y & 0xffff0000u)} +
+                (SB ? *reinterpret_cast<const f32x4*>(&sbias[h * D + ib * 16 + 4 * q]) : bq[ib]);
 #pragma unroll
       for (int kq = 0; kq < 4; ++kq) {
         const s16x8 xb = *reinterpret_cast<const s16x8*>(&xn[xoff(t, kq * 4 + q)]);
@@ -327,7 +337,8 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 
 }  // namespace
 
-int g_classattn_variant = 0;   // 2 = 16 LayerNorm row steps per batch (A/B); >= 16: diagnostics (dbg = v - 16)
+// 2 = 16 LayerNorm row steps per batch, 3 = biases in registers (A/B); >= 16: diagnostics (dbg = v - 16)
+int g_classattn_variant = 0;
 CATSEG_KNOB(g_classattn_variant, "classattn_variant");
 
 extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream) {
@@ -367,6 +378,7 @@ extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream
   const unsigned grid = (unsigned)std::min<int64_t>(npix, 2LL * cus);
   hipStream_t st = (hipStream_t)stream;
   if (g_classattn_variant == 2) hipLaunchKernelGGL(classattn2_kernel<16>, dim3(grid), dim3(NT), 0, st, p);
+  else if (g_classattn_variant == 3) hipLaunchKernelGGL((classattn2_kernel<8, false>), dim3(grid), dim3(NT), 0, st, p);
   else hipLaunchKernelGGL(classattn2_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
   return catseg_launch_status("class_attention");
 }
