@@ -281,7 +281,8 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
 // 0 = head-per-SIMD kernel (swin_window.hip swin_win3) with the opaque (inline-asm) LDS-DMA and the
 // per-window guidance base, 1 = the same with the builtin LDS-DMA and a row map per tile,
 // 2 = the row-tile-wave kernel (swin_fused2_kernel), 16 = variant 0 with phase stamps (diagnostics,
-// tools/stamps_swin.py).  (A barrier-free form with two 4-wave workgroups per CU, every head wave
+// tools/stamps_swin.py), 3 = the register-resident form (swin_win5: two 4-wave workgroups per CU,
+// q / k / v^T of a head held in its wave's registers).  (A barrier-free form with two 4-wave workgroups per CU, every head wave
 // LayerNorming its window's rows itself, measured 314 / 410 us vs 259 / 271 us: the per-wave
 // load -> LayerNorm -> MFMA chains left their latency exposed.)
 int g_swin_variant = 0;
@@ -291,6 +292,7 @@ int g_swin_variant = 0;
 CATSEG_KNOB(g_swin_variant, "swin_variant");
 
 int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin, bool stamps);   // swin_window.hip
+int swin_win5_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool glin);
 
 // the guidance row map restricted to one slice is rowmap(slice * 576) + pixel (swin_win3 then adds the pixel)
 static bool gmap_linear_in_pixel(const CatsegRowMap& m) {
@@ -326,7 +328,9 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   }
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (g_swin_variant <= 1 || g_swin_variant == 16) {
+  if (g_swin_variant == 3) {
+    swin_win5_launch(a, n_cu, (hipStream_t)stream, gmap_linear_in_pixel(a->gmap));
+  } else if (g_swin_variant <= 1 || g_swin_variant == 16) {
     const bool v0 = g_swin_variant != 1;
     swin_win3_launch(a, n_cu, (hipStream_t)stream, v0, v0 && gmap_linear_in_pixel(a->gmap), g_swin_variant == 16);
   } else {

@@ -333,6 +333,250 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-resident form (win5): 4-wave workgroups, TWO per CU (75 KB of LDS each), wave h owns
+// head h of the workgroup's window for all 9 row tiles.  The projection leaves every operand the
+// attention needs in the lane that needs it: an MFMA output k^T tile (lane: features 16dt + 4g + r
+// of token r16) is already the A fragment of S^T = K Q^T for that key tile, q^T the B fragment, and
+// v (lane: tokens 4g + r, feature 16dt + r16) is the V^T A fragment of O^T = V^T P^T when two key
+// tiles are paired.  So K, V^T and Q stay in registers (108 VGPRs), no K / V image goes through LDS,
+// and there is no barrier between projection and attention.  The LayerNorm'd rows (Xn, filled by
+// LDS-DMA and normalised by the 4 waves together) and W_v stay in LDS; W_q / W_k are re-read (L2) at
+// each window start so they are dead during the attention.  The two workgroups of a CU run different
+// windows, so one's projection MFMAs sit beside the other's softmax VALU on every SIMD.
+constexpr int NW5 = 4, NT5 = NW5 * 64;
+constexpr int LNS5 = (L + 4 * NW5 - 1) / (4 * NW5);          // LayerNorm steps (4 rows per wave each)
+
+DEV int local_region5(int wloc, int i, int shift) {   // region3 renumbered within the window: 0..3
+  const int wy = wloc >> 1, wx = wloc & 1;
+  const int Y = wy * WS + i / WS, X = wx * WS + i % WS;
+  const int lh = wy ? (Y < IMG - shift ? 0 : 1) : 0;
+  const int lw = wx ? (X < IMG - shift ? 0 : 1) : 0;
+  return lh * 2 + lw;
+}
+
+template <bool SWM, bool GLIN>
+__global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_total) {
+  __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
+  __shared__ __attribute__((aligned(16))) bf16 sWv[C * C];              // W_v (every head), chunk-major
+  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? L * 16 : 16];   // local region one-hot per key (k 0..3 of 16)
+  __shared__ __attribute__((aligned(16))) float sP[5 * C];              // LN gamma | beta | qkv bias
+
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int wloc = (int)(blockIdx.x % NWIN);                 // the grid is a multiple of 4 (host)
+  for (int i = tid; i < 5 * C; i += NT5) sP[i] = i < C ? p.ln_g[i] : i < 2 * C ? p.ln_b[i - C] : p.bias[i - 2 * C];
+  for (int c = tid; c < C * 16; c += NT5) {
+    const int lr = c >> 4, ch = c & 15;
+    st16(&sWv[cs<C>(ch, lr)], ld16(p.w + (int64_t)(2 * C + lr) * C + ch * 8));
+  }
+  if constexpr (SWM) {
+    for (int key = tid; key < L; key += NT5) {
+      const int reg = local_region5(wloc, key, p.shift);
+      st16(&Oh[key * 16], make_uint4(reg == 0 ? 0x3F80u : reg == 1 ? 0x3F800000u : 0u,
+                                     reg == 2 ? 0x3F80u : reg == 3 ? 0x3F800000u : 0u, 0u, 0u));
+      st16(&Oh[key * 16 + 8], make_uint4(0u, 0u, 0u, 0u));
+    }
+  }
+  s16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  const bool masked = SWM && wloc != 0;                      // window location 0 holds a single region
+  const short neg = (short)f2bf(-100.f / p.scale);
+  constexpr int NDMA = L * 16 / 64;                          // 36 wave-instructions per window
+  auto fetch = [&](int win) {
+    const int slice = win / NWIN;
+    for (int k = h; k < NDMA; k += NW5) {
+      const int sl = k * 64 + lane, c = sl / L, i = (sl % L) ^ (c & 15);
+      const bf16* src = p.x + (int64_t)win_row3(slice, wloc, i, p.shift) * p.ld_x + c * 8;
+      dma16_opaque(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xn + k * 64 * 8)));
+    }
+  };
+  int win = blockIdx.x;
+  if (win < nwin_total) fetch(win);
+  __syncthreads();
+  for (; win < nwin_total; win += gridDim.x) {
+    const int slice = win / NWIN;
+    // lane-derived offsets recomputed per window from an opaque copy: hoisted out of the window loop
+    // they would hold ~100 VGPRs for the whole kernel
+    int lane_w = lane;
+    asm volatile("" : "+v"(lane_w));
+    const int r16 = lane_w & 15, g = lane_w >> 4, lc = lane_w & 15, lrow0 = 4 * h + (lane_w >> 4);
+    // this wave's DMA of the window landed (only the previous window's >= 18 output stores were
+    // issued behind it and may stay in flight)
+    if (win == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    __syncthreads();
+    // W_q / W_k of head h (A fragments: rows 16dt + r16 of the head, k = 32ks + 8g ..), L2-resident
+    s16x8 wf[2][2][4];
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          wf[part][dt][ks] = __builtin_bit_cast(
+              s16x8, ld16(p.w + (int64_t)(part * C + h * D + dt * 16 + r16) * C + ks * 32 + 8 * g));
+    const int64_t gbase = GLIN ? rowmap(p.gmap, (int64_t)slice * (IMG * IMG)) : 0;
+    auto fetch_g = [&](int t, int part, uint2 (&gd)[2]) {     // guidance of the q (0) or k (1) half
+      const int row = win_row3(slice, wloc, 16 * t + r16, p.shift);
+      const int64_t grow = GLIN ? gbase + (row - slice * (IMG * IMG)) : rowmap(p.gmap, row);
+      const bf16* gp = p.g + grow * p.ld_g + part * C + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) gd[dt] = *reinterpret_cast<const uint2*>(gp + dt * 16);
+    };
+    uint2 gc[2];
+    fetch_g(0, 1, gc);
+    // ---------------- P1: LayerNorm of Xn in place, the 4 waves together ----------------
+    {
+      const float4 g0 = *reinterpret_cast<const float4*>(&sP[lc * 8]), g1 = *reinterpret_cast<const float4*>(&sP[lc * 8 + 4]);
+      const float4 b0 = *reinterpret_cast<const float4*>(&sP[C + lc * 8]), b1 = *reinterpret_cast<const float4*>(&sP[C + lc * 8 + 4]);
+      const float lg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float lb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int st_ = 0; st_ < LNS5; ++st_) {
+        const int i = min(st_ * 16 + lrow0, L - 1);
+        const uint4 raw = *reinterpret_cast<const uint4*>(&Xn[cs<L>(lc, i)]);
+        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+        float v[8], sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[j] = bf2f(e[j]); sum += v[j]; }
+        sum = row16_sum(sum);
+        const float mean = sum * (1.f / C);
+        float qs = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[j] -= mean; qs += v[j] * v[j]; }
+        qs = row16_sum(qs);
+        const float rstd = __builtin_amdgcn_rsqf(qs * (1.f / C) + p.eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] * rstd * lg[j] + lb[j];
+        if (st_ * 16 + 4 * NW5 <= L || st_ * 16 + lrow0 < L)
+          st16(&Xn[cs<L>(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
+      }
+    }
+    __syncthreads();
+    // ---------------- P2: k / v of head h for all 9 row tiles, then q, kept in registers ----------------
+    // (two passes over Xn so that W_k is dead before q's pass and q's guidance is not held during k's)
+    s16x8 qf[NTILE], kf[NTILE];
+    uint2 vv[NTILE][2];                       // v of tokens 16t + 4g + r, feature 16dt + r16 (bf16 x 4)
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      uint2 gn[2];
+      fetch_g(t + 1 < NTILE ? t + 1 : 0, t + 1 < NTILE ? 1 : 0, gn);   // the last prefetches q's tile 0
+      __builtin_amdgcn_sched_barrier(0);      // keep the prefetch at the tile start
+      asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
+      const int rb = 16 * t;
+      s16x8 xb[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(((ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
+      f32x4 dk[2], dv[2];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        dk[dt] = *reinterpret_cast<const f32x4*>(&sP[3 * C + h * D + dt * 16 + 4 * g]) + unpack4(gc[dt]);
+        const float bvv = sP[4 * C + h * D + dt * 16 + r16];
+        dv[dt] = f32x4{bvv, bvv, bvv, bvv};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dk[dt] = mfma_bf16(wf[1][dt][ks], xb[ks], dk[dt]);
+          dv[dt] = mfma_bf16(xb[ks], *reinterpret_cast<const s16x8*>(&sWv[cs<C>(ks * 4 + g, h * D + dt * 16 + r16)]),
+                             dv[dt]);
+        }
+      kf[t] = pk8(dk[0], dk[1]);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) vv[t][dt] = make_uint2(f2bf2(dv[dt][0], dv[dt][1]), f2bf2(dv[dt][2], dv[dt][3]));
+      // pin the packed bf16 forms: left alone the conversions sink to the use in P3 and the f32
+      // accumulators (twice the registers) stay live across the tiles
+      asm volatile("" : "+v"(kf[t]), "+v"(vv[t][0]), "+v"(vv[t][1]));
+      gc[0] = gn[0]; gc[1] = gn[1];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      uint2 gn[2];
+      if (t + 1 < NTILE) fetch_g(t + 1, 0, gn);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
+      const int rb = 16 * t;
+      s16x8 xb[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(((ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
+      f32x4 dq[2];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        dq[dt] = *reinterpret_cast<const f32x4*>(&sP[2 * C + h * D + dt * 16 + 4 * g]) + unpack4(gc[dt]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma_bf16(wf[0][dt][ks], xb[ks], dq[dt]);
+      qf[t] = pk8(dq[0], dq[1]);
+      asm volatile("" : "+v"(qf[t]));
+      if (t + 1 < NTILE) { gc[0] = gn[0]; gc[1] = gn[1]; }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();                          // every wave is done with Xn
+    if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
+    // ---------------- P3: attention of head h, 9 query tiles, K / V^T / Q from registers ----------------
+#pragma unroll
+    for (int j = 0; j < NTILE; ++j) {
+      const int rb = 16 * j;
+      asm volatile("" ::: "memory");          // the region one-hots are re-read per query tile
+      // an opaque window location per tile: otherwise the output rows are CSE'd with P2's guidance rows
+      // and carried (spilled) across P2, and the per-tile masks are hoisted out of the loop
+      int wl = wloc;
+      asm volatile("" : "+s"(wl));
+      s16x4 qmask;                            // B of the 16x16x16 mask product: -100/scale off the query's region
+      if (masked) {
+        const int qreg = local_region5(wl, rb + r16, p.shift);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qmask[e] = g == 0 && e != qreg ? neg : (short)0;
+      }
+      f32x4 st[NTILE + 1];
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt) {
+        f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+        if (masked)
+          a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(kt * 16 + r16) * 16 + 4 * g]),
+                                                        qmask, a, 0, 0, 0);
+        st[kt] = a;
+      }
+      float mx = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
+#pragma unroll
+      for (int kt = 1; kt < NTILE; ++kt) mx = fmaxf(mx, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+      mx = xrow4_max(mx);
+      const float nb = -mx * sl2;
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
+      st[NTILE] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < KBV / 32; ++u) {
+        const s16x8 pb = pk8(st[2 * u], st[2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          // V^T fragment: keys 32u + 4g .. +3 (tile 2u) and 32u + 16 + 4g .. +3 (tile 2u + 1), feature 16dt + r16
+          const uint2 lo = vv[2 * u][dt];
+          const uint2 hi = 2 * u + 1 < NTILE ? vv[2 * u + 1][dt] : make_uint2(0u, 0u);
+          o[dt] = mfma_bf16(__builtin_bit_cast(s16x8, make_uint4(lo.x, lo.y, hi.x, hi.y)), pb, o[dt]);
+        }
+        osum = mfma_bf16(ones, pb, osum);
+      }
+      const float inv = 1.f / osum[0];
+      bf16* O = p.out + (int64_t)win_row3(slice, wl, rb + r16, p.shift) * p.ld_out + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
+            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 }  // namespace
 
 // launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
@@ -357,6 +601,31 @@ int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   } else {
     if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, false>), grid, dim3(NT), 0, st, p, nwin_total);
     else hipLaunchKernelGGL((swin_win3_kernel<false, false>), grid, dim3(NT), 0, st, p, nwin_total);
+  }
+  return 0;
+}
+
+// two 4-wave workgroups per CU, the grid a multiple of the 4 window locations
+int swin_win5_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool glin) {
+  Swin3P p;
+  p.glin = glin ? 1 : 0;
+  p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
+  p.ln_g = a->ln_g; p.ln_b = a->ln_b; p.eps = a->eps;
+  p.w = (const bf16*)a->w_qkv; p.bias = a->b_qkv;
+  p.g = (const bf16*)a->gqk; p.ld_g = a->ld_g;
+  p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
+  p.out = (bf16*)a->out; p.ld_out = a->ld_out;
+  p.shift = a->shift; p.scale = a->scale;
+  const int nwin_total = (int)(a->S * NWIN);
+  const dim3 grid((unsigned)std::min(nwin_total, (2 * n_cu) / NWIN * NWIN));
+  // the guidance rows of a slice are one base + the pixel (GLIN) in every engine call; a general row
+  // map takes the per-tile rowmap form
+  if (a->shift > 0) {
+    if (glin) hipLaunchKernelGGL((swin_win5_kernel<true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win5_kernel<true, false>), grid, dim3(NT5), 0, st, p, nwin_total);
+  } else {
+    if (glin) hipLaunchKernelGGL((swin_win5_kernel<false, true>), grid, dim3(NT5), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win5_kernel<false, false>), grid, dim3(NT5), 0, st, p, nwin_total);
   }
   return 0;
 }
