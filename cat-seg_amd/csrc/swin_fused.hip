@@ -278,11 +278,12 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
   }
 }
 
-// 0 = head-per-SIMD kernel (swin_window.hip swin_win3) with the opaque (inline-asm) LDS-DMA and the
-// per-window guidance base, 1 = the same with the builtin LDS-DMA and a row map per tile,
-// 2 = the row-tile-wave kernel (swin_fused2_kernel), 16 = variant 0 with phase stamps (diagnostics,
-// tools/stamps_swin.py), 3 = the register-resident form (swin_win5: two 4-wave workgroups per CU,
-// q / k / v^T of a head held in its wave's registers).  (A barrier-free form with two 4-wave workgroups per CU, every head wave
+// 0 = the register-resident kernel (swin_window.hip swin_win5: two 4-wave workgroups per CU, wave h
+// holding head h's k / v^T / q in registers after the projection), 1 = the head-per-SIMD kernel
+// (swin_win3) with the builtin LDS-DMA and a row map per tile, 2 = the row-tile-wave kernel
+// (swin_fused2_kernel), 3 = swin_win3 with the opaque (inline-asm) LDS-DMA and the per-window guidance
+// base (the default until round 3), 16 = variant 3 with phase stamps (diagnostics,
+// tools/stamps_swin.py).  (A barrier-free form with two 4-wave workgroups per CU, every head wave
 // LayerNorming its window's rows itself, measured 314 / 410 us vs 259 / 271 us: the per-wave
 // load -> LayerNorm -> MFMA chains left their latency exposed.)
 int g_swin_variant = 0;
@@ -328,11 +329,11 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   }
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (g_swin_variant == 3) {
+  if (g_swin_variant == 0) {
     swin_win5_launch(a, n_cu, (hipStream_t)stream, gmap_linear_in_pixel(a->gmap));
-  } else if (g_swin_variant <= 1 || g_swin_variant == 16) {
-    const bool v0 = g_swin_variant != 1;
-    swin_win3_launch(a, n_cu, (hipStream_t)stream, v0, v0 && gmap_linear_in_pixel(a->gmap), g_swin_variant == 16);
+  } else if (g_swin_variant == 1 || g_swin_variant == 3 || g_swin_variant == 16) {
+    const bool v3 = g_swin_variant != 1;
+    swin_win3_launch(a, n_cu, (hipStream_t)stream, v3, v3 && gmap_linear_in_pixel(a->gmap), g_swin_variant == 16);
   } else {
     if (a->shift > 0)
       hipLaunchKernelGGL(swin_fused2_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);

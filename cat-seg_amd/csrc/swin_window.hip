@@ -30,6 +30,7 @@
 // HBM traffic per window: the 144 input rows, the 144 output rows, the guidance rows (shared by
 // every class of an image: L2-resident).
 #include "common.h"
+#include <type_traits>
 #include "capi.h"
 
 namespace {
@@ -520,6 +521,11 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
     __syncthreads();                          // every wave is done with Xn
     if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
     // ---------------- P3: attention of head h, 9 query tiles, K / V^T / Q from registers ----------------
+    // (one instance per kernel; the masked / unmasked choice stays a uniform branch per key tile: a
+    // hoisted per-window choice between two instances produced wrong shifted-window outputs on the
+    // box and was not kept)
+    auto attend = [&](auto mk) {
+    constexpr bool MK = decltype(mk)::value;
 #pragma unroll
     for (int j = 0; j < NTILE; ++j) {
       const int rb = 16 * j;
@@ -529,7 +535,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       int wl = wloc;
       asm volatile("" : "+s"(wl));
       s16x4 qmask;                            // B of the 16x16x16 mask product: -100/scale off the query's region
-      if (masked) {
+      if (MK && masked) {
         const int qreg = local_region5(wl, rb + r16, p.shift);
 #pragma unroll
         for (int e = 0; e < 4; ++e) qmask[e] = g == 0 && e != qreg ? neg : (short)0;
@@ -538,7 +544,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
 #pragma unroll
       for (int kt = 0; kt < NTILE; ++kt) {
         f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
-        if (masked)
+        if (MK && masked)
           a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(kt * 16 + r16) * 16 + 4 * g]),
                                                         qmask, a, 0, 0, 0);
         st[kt] = a;
@@ -574,6 +580,8 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
             make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
       __builtin_amdgcn_sched_barrier(0);
     }
+    };
+    attend(std::integral_constant<bool, SWM>{});
   }
 }
 

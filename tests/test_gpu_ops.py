@@ -933,9 +933,9 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
 def test_swin_window_attention_fused_vs_unfused(shift, variant):
     """catseg_swin_window_attention == catseg_rows_gemm(LN1 + q/k/v + guidance) followed by
     catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry.
-    variant 0 = the head-per-SIMD kernel with the opaque LDS-DMA (default, swin_window.hip), 1 = the
-    same with the builtin LDS-DMA and a row map per tile, 2 = the row-tile-wave kernel, 3 = the
-    register-resident kernel (two 4-wave workgroups per CU); S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
+    variant 0 = the register-resident kernel (default, swin_window.hip swin_win5: two 4-wave
+    workgroups per CU), 1 = the head-per-SIMD kernel with the builtin LDS-DMA and a row map per tile,
+    2 = the row-tile-wave kernel, 3 = the head-per-SIMD kernel with the opaque LDS-DMA; S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
     B, T, HW, D = 1, 7, 576, 128
     S = B * T
     R = S * HW
@@ -989,10 +989,10 @@ def test_swin_window_attention_fused_vs_unfused(shift, variant):
 @pytest.mark.parametrize("shift", [0, 6])
 def test_swin_window_attention_persistent_variants_agree(shift, glin):
     """Persistent grid over several windows per workgroup (S = 200 slices = 800 windows > the
-    256-workgroup grid, guidance map of 2 images): the opaque-DMA kernel (variant 0, whose counted
+    grid, guidance map of 2 images): the head-per-SIMD opaque-DMA kernel (variant 3, whose counted
     window-start wait lets the previous window's stores stay in flight, guidance rows from a per-window
     base) equals the builtin-DMA / per-tile row-map kernel (variant 1) bit for bit, and so does the
-    register-resident kernel (variant 3: same LayerNorm, projection and softmax arithmetic, its
+    register-resident default (variant 0: same LayerNorm, projection and softmax arithmetic, its
     one-hot mask product on the 16x16x16 MFMA).  glin=False stores the guidance pixel-major
     (row = pixel * B + image), which no slice maps to one base + pixel: the per-tile row-map path."""
     B, T, HW, D = 2, 100, 576, 128
@@ -1007,7 +1007,7 @@ def test_swin_window_attention_persistent_variants_agree(shift, glin):
     gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1) if glin else rowmap(d1=T * HW, s1=1, d2=1, m2=HW, s2=B)
     outs = []
     try:
-        for variant in (1, 0, 3):
+        for variant in (1, 3, 0):
             L.tune("swin_variant", variant)
             o = torch.full((R, D), float("nan"), device=dev, dtype=dt)
             ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, o, S=S, img_hw=(24, 24), window=12,
