@@ -1,16 +1,19 @@
-// Swin window attention, head-per-SIMD form (bf16) -- the default kernel behind
-// catseg_swin_window_attention (swin_fused.hip holds the argument checks and the older forms).
+// Swin window attention (bf16): the kernels behind catseg_swin_window_attention (swin_fused.hip
+// holds the argument checks, the variant switch and the older row-tile-wave form).
 // Reference: SwinTransformerBlock.forward model.py:191-199 (norm1, concat guidance, roll,
 // window_partition) and WindowAttention.forward model.py:86-114 up to the output projection;
 // the -100 region mask of model.py:161-183.
 //
-// A window is 144 tokens = 9 row tiles of 16.  With one wave per row tile (swin_fused2_kernel)
-// the 9 waves sit 3 / 2 / 2 / 2 on the CU's four SIMDs and the 3-wave SIMD paces every window.
-// Here the work is cut by HEAD instead: 8 waves, wave w computes head h = w % 4 (waves w and
-// w + 4 share a SIMD -- a workgroup's waves are dealt to the SIMDs cyclically), so every SIMD
-// does exactly one head's q/k/v projection and attention for all 144 tokens.
+// A window is 144 tokens = 9 row tiles of 16, 4 heads of 32.  Two forms cut the work by HEAD:
 //
-// Per window (persistent workgroup per CU, windows strided by the grid):
+// swin_win5 (default, swin_variant 0; below): two 4-wave workgroups per CU, wave h = head h of its
+// workgroup's window for all 9 tiles.  LayerNorm by the 4 waves into Xn (LDS), then the projection
+// leaves k^T / q^T / v of the head in the wave's own registers in exactly the MFMA operand layouts the
+// attention needs (108 VGPRs), so no K / V image goes through LDS and there is no barrier between
+// projection and attention; the two workgroups of a CU interleave their MFMA and softmax phases.
+//
+// swin_win3 (swin_variant 3 / 1 / 16): one 8-wave workgroup per CU, waves w and w + 4 share head
+// w % 4 (every SIMD does one head), K and V^T of each head staged in LDS:
 //   P1  LayerNorm(norm1) of the 144 rows in place in Xn (bf16, chunk-major XOR-swizzled), 16
 //       lanes per row.  The raw rows were brought in by LDS-DMA during the previous window's P3.
 //   --  barrier
@@ -26,7 +29,7 @@
 //       the 144 keys of the window in registers, O^T = V^T P^T and the row sums on the MFMA,
 //       8-byte stores of the head's 32 output channels.  The next window's rows are requested
 //       (LDS-DMA into Xn, free once P2 is done everywhere).
-//   --  vmcnt(0) + barrier (the DMA is visible; every wave is past P3)
+//   --  counted vmcnt + barrier (the DMA is visible; every wave is past P3)
 // HBM traffic per window: the 144 input rows, the 144 output rows, the guidance rows (shared by
 // every class of an image: L2-resident).
 #include "common.h"
@@ -465,7 +468,9 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
     for (int t = 0; t < NTILE; ++t) {
       uint2 gn[2];
       fetch_g(t + 1 < NTILE ? t + 1 : 0, t + 1 < NTILE ? 1 : 0, gn);   // the last prefetches q's tile 0
+#ifndef W5_NOSB2K
       __builtin_amdgcn_sched_barrier(0);      // keep the prefetch at the tile start
+#endif
       asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
       const int rb = 16 * t;
       s16x8 xb[4];
@@ -493,13 +498,17 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       // accumulators (twice the registers) stay live across the tiles
       asm volatile("" : "+v"(kf[t]), "+v"(vv[t][0]), "+v"(vv[t][1]));
       gc[0] = gn[0]; gc[1] = gn[1];
+#ifndef W5_NOSB2K
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       uint2 gn[2];
       if (t + 1 < NTILE) fetch_g(t + 1, 0, gn);
+#ifndef W5_NOSB2Q
       __builtin_amdgcn_sched_barrier(0);
+#endif
       asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
       const int rb = 16 * t;
       s16x8 xb[4];
@@ -516,7 +525,9 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       qf[t] = pk8(dq[0], dq[1]);
       asm volatile("" : "+v"(qf[t]));
       if (t + 1 < NTILE) { gc[0] = gn[0]; gc[1] = gn[1]; }
+#ifndef W5_NOSB2Q
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     __syncthreads();                          // every wave is done with Xn
     if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
@@ -535,16 +546,28 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       int wl = wloc;
       asm volatile("" : "+s"(wl));
       s16x4 qmask;                            // B of the 16x16x16 mask product: -100/scale off the query's region
+#ifdef W5_NOBR
+      if constexpr (MK) {
+        const int qreg = local_region5(wl, rb + r16, p.shift);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qmask[e] = masked && g == 0 && e != qreg ? neg : (short)0;
+      }
+#else
       if (MK && masked) {
         const int qreg = local_region5(wl, rb + r16, p.shift);
 #pragma unroll
         for (int e = 0; e < 4; ++e) qmask[e] = g == 0 && e != qreg ? neg : (short)0;
       }
+#endif
       f32x4 st[NTILE + 1];
 #pragma unroll
       for (int kt = 0; kt < NTILE; ++kt) {
         f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+#ifdef W5_NOBR
+        if constexpr (MK)
+#else
         if (MK && masked)
+#endif
           a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(kt * 16 + r16) * 16 + 4 * g]),
                                                         qmask, a, 0, 0, 0);
         st[kt] = a;
@@ -578,7 +601,9 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       for (int dt = 0; dt < 2; ++dt)
         *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
             make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+#ifndef W5_NOSB3
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     };
     attend(std::integral_constant<bool, SWM>{});
