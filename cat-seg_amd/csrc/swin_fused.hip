@@ -329,11 +329,13 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   }
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (g_swin_variant == 0) {
-    swin_win5_launch(a, n_cu, (hipStream_t)stream, gmap_linear_in_pixel(a->gmap));
-  } else if (g_swin_variant == 1 || g_swin_variant == 3 || g_swin_variant == 16) {
-    const bool v3 = g_swin_variant != 1;
-    swin_win3_launch(a, n_cu, (hipStream_t)stream, v3, v3 && gmap_linear_in_pixel(a->gmap), g_swin_variant == 16);
+  const bool glin = gmap_linear_in_pixel(a->gmap);
+  if (g_swin_variant == 0 && glin) {
+    swin_win5_launch(a, n_cu, (hipStream_t)stream, true);
+  } else if (g_swin_variant <= 1 || g_swin_variant == 3 || g_swin_variant == 16) {
+    // (variant 0 with a row map that is not base + pixel per slice runs swin_win3's row-map form)
+    const bool v3 = g_swin_variant == 3 || g_swin_variant == 16;
+    swin_win3_launch(a, n_cu, (hipStream_t)stream, v3, v3 && glin, g_swin_variant == 16);
   } else {
     if (a->shift > 0)
       hipLaunchKernelGGL(swin_fused2_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, p, nwin_total);

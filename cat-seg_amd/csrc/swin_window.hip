@@ -468,9 +468,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
     for (int t = 0; t < NTILE; ++t) {
       uint2 gn[2];
       fetch_g(t + 1 < NTILE ? t + 1 : 0, t + 1 < NTILE ? 1 : 0, gn);   // the last prefetches q's tile 0
-#ifndef W5_NOSB2K
       __builtin_amdgcn_sched_barrier(0);      // keep the prefetch at the tile start
-#endif
       asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
       const int rb = 16 * t;
       s16x8 xb[4];
@@ -498,17 +496,13 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       // accumulators (twice the registers) stay live across the tiles
       asm volatile("" : "+v"(kf[t]), "+v"(vv[t][0]), "+v"(vv[t][1]));
       gc[0] = gn[0]; gc[1] = gn[1];
-#ifndef W5_NOSB2K
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       uint2 gn[2];
       if (t + 1 < NTILE) fetch_g(t + 1, 0, gn);
-#ifndef W5_NOSB2Q
       __builtin_amdgcn_sched_barrier(0);
-#endif
       asm volatile("" ::: "memory");          // W_v / bias fragments re-read per tile, not held across tiles
       const int rb = 16 * t;
       s16x8 xb[4];
@@ -525,16 +519,13 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       qf[t] = pk8(dq[0], dq[1]);
       asm volatile("" : "+v"(qf[t]));
       if (t + 1 < NTILE) { gc[0] = gn[0]; gc[1] = gn[1]; }
-#ifndef W5_NOSB2Q
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     __syncthreads();                          // every wave is done with Xn
     if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);
     // ---------------- P3: attention of head h, 9 query tiles, K / V^T / Q from registers ----------------
-    // (one instance per kernel; the masked / unmasked choice stays a uniform branch per key tile: a
-    // hoisted per-window choice between two instances produced wrong shifted-window outputs on the
-    // box and was not kept)
+    // (one instance per kernel: a hoisted per-window choice between a masked and an unmasked instance
+    // produced wrong shifted-window outputs on the box and was not kept)
     auto attend = [&](auto mk) {
     constexpr bool MK = decltype(mk)::value;
 #pragma unroll
@@ -546,28 +537,18 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       int wl = wloc;
       asm volatile("" : "+s"(wl));
       s16x4 qmask;                            // B of the 16x16x16 mask product: -100/scale off the query's region
-#ifdef W5_NOBR
+      // window location 0 holds one region: its mask operand is zero (S + 0 is exact), which keeps
+      // the tile free of a branch per key tile (branches split the MFMA / softmax schedule)
       if constexpr (MK) {
         const int qreg = local_region5(wl, rb + r16, p.shift);
 #pragma unroll
         for (int e = 0; e < 4; ++e) qmask[e] = masked && g == 0 && e != qreg ? neg : (short)0;
       }
-#else
-      if (MK && masked) {
-        const int qreg = local_region5(wl, rb + r16, p.shift);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) qmask[e] = g == 0 && e != qreg ? neg : (short)0;
-      }
-#endif
       f32x4 st[NTILE + 1];
 #pragma unroll
       for (int kt = 0; kt < NTILE; ++kt) {
         f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
-#ifdef W5_NOBR
         if constexpr (MK)
-#else
-        if (MK && masked)
-#endif
           a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(kt * 16 + r16) * 16 + 4 * g]),
                                                         qmask, a, 0, 0, 0);
         st[kt] = a;
@@ -601,9 +582,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       for (int dt = 0; dt < 2; ++dt)
         *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
             make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
-#ifndef W5_NOSB3
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     };
     attend(std::integral_constant<bool, SWM>{});
@@ -651,14 +630,11 @@ int swin_win5_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   p.shift = a->shift; p.scale = a->scale;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, (2 * n_cu) / NWIN * NWIN));
-  // the guidance rows of a slice are one base + the pixel (GLIN) in every engine call; a general row
-  // map takes the per-tile rowmap form
-  if (a->shift > 0) {
-    if (glin) hipLaunchKernelGGL((swin_win5_kernel<true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
-    else hipLaunchKernelGGL((swin_win5_kernel<true, false>), grid, dim3(NT5), 0, st, p, nwin_total);
-  } else {
-    if (glin) hipLaunchKernelGGL((swin_win5_kernel<false, true>), grid, dim3(NT5), 0, st, p, nwin_total);
-    else hipLaunchKernelGGL((swin_win5_kernel<false, false>), grid, dim3(NT5), 0, st, p, nwin_total);
-  }
+  // only for guidance rows that are one base + the pixel per slice (every engine call; the caller
+  // sends other row maps to swin_win3).  The general-row-map instance spilled 19-23 VGPRs and gave
+  // wrong shifted-window outputs on the box, so it is not instantiated.
+  if (!glin) return -1;
+  if (a->shift > 0) hipLaunchKernelGGL((swin_win5_kernel<true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
+  else hipLaunchKernelGGL((swin_win5_kernel<false, true>), grid, dim3(NT5), 0, st, p, nwin_total);
   return 0;
 }

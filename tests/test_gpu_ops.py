@@ -994,7 +994,8 @@ def test_swin_window_attention_persistent_variants_agree(shift, glin):
     base) equals the builtin-DMA / per-tile row-map kernel (variant 1) bit for bit, and so does the
     register-resident default (variant 0: same LayerNorm, projection and softmax arithmetic, its
     one-hot mask product on the 16x16x16 MFMA).  glin=False stores the guidance pixel-major
-    (row = pixel * B + image), which no slice maps to one base + pixel: the per-tile row-map path."""
+    (row = pixel * B + image), which no slice maps to one base + pixel: variants 3 and 0 then run
+    swin_win3's per-tile row-map path."""
     B, T, HW, D = 2, 100, 576, 128
     S = B * T
     R = S * HW
