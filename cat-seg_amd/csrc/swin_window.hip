@@ -363,7 +363,9 @@ template <bool SWM, bool GLIN>
 __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 sWv[C * C];              // W_v (every head), chunk-major
-  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? L * 16 : 16];   // local region one-hot per key (k 0..3 of 16)
+  // local region one-hot per key as the 16x16x16 A operand, k-group-major: [g][key][4] (g > 0 zero),
+  // so the 64 lanes' 8-byte reads of a key tile hit distinct banks
+  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? 4 * L * 4 : 16];
   __shared__ __attribute__((aligned(16))) float sP[5 * C];              // LN gamma | beta | qkv bias
 
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
@@ -377,9 +379,10 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
   if constexpr (SWM) {
     for (int key = tid; key < L; key += NT5) {
       const int reg = local_region5(wloc, key, p.shift);
-      st16(&Oh[key * 16], make_uint4(reg == 0 ? 0x3F80u : reg == 1 ? 0x3F800000u : 0u,
-                                     reg == 2 ? 0x3F80u : reg == 3 ? 0x3F800000u : 0u, 0u, 0u));
-      st16(&Oh[key * 16 + 8], make_uint4(0u, 0u, 0u, 0u));
+      *reinterpret_cast<uint2*>(&Oh[key * 4]) = make_uint2(reg == 0 ? 0x3F80u : reg == 1 ? 0x3F800000u : 0u,
+                                                           reg == 2 ? 0x3F80u : reg == 3 ? 0x3F800000u : 0u);
+#pragma unroll
+      for (int gg = 1; gg < 4; ++gg) *reinterpret_cast<uint2*>(&Oh[(gg * L + key) * 4]) = make_uint2(0u, 0u);
     }
   }
   s16x8 ones;
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       for (int kt = 0; kt < NTILE; ++kt) {
         f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
         if constexpr (MK)
-          a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(kt * 16 + r16) * 16 + 4 * g]),
+          a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(g * L + kt * 16 + r16) * 4]),
                                                         qmask, a, 0, 0, 0);
         st[kt] = a;
       }

@@ -1,0 +1,54 @@
+"""Where swin_variant 4 (swin_win5 for every block; the runs are listed as variant 0) differs from variant 3 (S = 200, shift 6, linear guidance map): rows that differ,
+by window location / slice / token, and whether variant 0 is deterministic run to run."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
+import torch
+from cat_seg import ops
+from cat_seg import _lib as L
+from cat_seg._lib import rowmap
+L.load()
+B, T, HW, D = 2, 100, 576, 128
+S, R = B * T, B * T * HW
+dev, dt = "cuda", torch.bfloat16
+def rnd(*shape, seed=0, scale=1.0):     # tests/test_gpu_ops.py's inputs
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+X = rnd(R, D, seed=61, scale=2.0).to(dev, dt)
+g1, b1 = (1 + rnd(D, seed=62, scale=0.2)).to(dev), rnd(D, seed=63, scale=0.2).to(dev)
+W = (rnd(3 * D, D, seed=64) / D ** 0.5).to(dev, dt)
+bias = rnd(3 * D, seed=65, scale=0.1).to(dev)
+gqk = rnd(B * HW, 2 * D, seed=66, scale=0.5).to(dev, dt)
+gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)
+shift = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+order = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "3,0,0,0,0,0").split(",")]
+outs = {}
+for v in order:
+    L.tune("swin_variant", 4 if v == 0 else v)
+    o = torch.full((R, D), float("nan"), device=dev, dtype=dt)
+    ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, o, S=S, img_hw=(24, 24), window=12, shift=shift,
+                              n_heads=4, head_dim=32, scale=32 ** -0.5)
+    torch.cuda.synchronize()
+    outs.setdefault(v, []).append(o.float().cpu())
+L.tune("swin_variant", 0)
+a = outs[3][0] if 3 in outs else outs[0][-1]
+n_bad = sum(not torch.equal(x, a) for x in outs[0])
+print("launches of variant 0:", len(outs[0]), "differing from variant 3:", n_bad)
+b = [x for x in outs[0] if not torch.equal(x, a)]
+b = b[0] if b else outs[0][0]
+print("order", order, "variant 0 runs equal to the reference:", [torch.equal(x, a) for x in outs[0]],
+      "max", [(x - a).abs().max().item() for x in outs[0]])
+d = (a - b).abs().reshape(S, 24, 24, D)
+print("max diff", d.max().item(), "rows differing", (d.amax(-1) > 0).sum().item(), "of", S * 576)
+# undo the roll: pixel (y, x) of the rolled map is (y + shift) % 24
+rows = (d.amax(-1) > 0).nonzero()
+if len(rows):
+    ys = (rows[:, 1] - shift) % 24
+    xs = (rows[:, 2] - shift) % 24
+    wl = (ys // 12) * 2 + (xs // 12)
+    print("window locations:", torch.bincount(wl, minlength=4).tolist())
+    print("slices (first 20):", sorted(set(rows[:, 0].tolist()))[:20], "n slices", len(set(rows[:, 0].tolist())))
+    tok = (ys % 12) * 12 + xs % 12
+    print("tokens (first 40):", sorted(set(tok.tolist()))[:40])
+    ch = (d.reshape(-1, D)[(d.reshape(-1, D).amax(-1) > 0)] > 0).float().sum(0)
+    print("channels hit:", ch.nonzero().flatten().tolist()[:40])
