@@ -279,14 +279,11 @@ __global__ __launch_bounds__(NT) void swin_fused2_kernel(SwinP p, int nwin_total
 }
 
 // 0 (default) = the register-resident kernel (swin_window.hip swin_win5: two 4-wave workgroups per
-// CU, wave h holding head h's k / v^T / q in registers after the projection) for the unshifted blocks
-// and swin_win3 (variant 3) for the shifted ones, 1 = the head-per-SIMD kernel (swin_win3) with the
-// builtin LDS-DMA and a row map per tile, 2 = the row-tile-wave kernel (swin_fused2_kernel), 3 =
-// swin_win3 with the opaque (inline-asm) LDS-DMA and the per-window guidance base (the default until
-// round 3), 4 = swin_win5 for every block, 16 = variant 3 with phase stamps (diagnostics,
-// tools/stamps_swin.py).  swin_win5's masked (shifted) instance returns one wave's query tile 0 wrong
-// in ~1 of 5 launches (16 rows x 32 channels of one window; tools/debug_swin_diff.py); the unshifted
-// instance has not differed from swin_win3 in any launch, so only it is on the default path.
+// CU, wave h holding head h's k / v^T / q in registers after the projection), 1 = the head-per-SIMD
+// kernel (swin_win3) with the builtin LDS-DMA and a row map per tile, 2 = the row-tile-wave kernel
+// (swin_fused2_kernel), 3 = swin_win3 with the opaque (inline-asm) LDS-DMA and the per-window
+// guidance base (the default until round 3), 16 = variant 3 with phase stamps (diagnostics,
+// tools/stamps_swin.py).  Row maps that are not base + pixel per slice run swin_win3.
 // (A barrier-free form with two 4-wave workgroups per CU, every head wave LayerNorming its window's
 // rows itself, measured 314 / 410 us vs 259 / 271 us: the per-wave load -> LayerNorm -> MFMA chains
 // left their latency exposed.)
@@ -334,10 +331,10 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
   const bool glin = gmap_linear_in_pixel(a->gmap);
-  if (glin && (g_swin_variant == 4 || (g_swin_variant == 0 && a->shift == 0))) {
+  if (glin && g_swin_variant == 0) {
     swin_win5_launch(a, n_cu, (hipStream_t)stream, true);
   } else if (g_swin_variant != 2) {
-    // variant 0's shifted blocks, and any row map that is not base + pixel per slice, run swin_win3
+    // (variant 0 with a row map that is not base + pixel per slice runs swin_win3's row-map form)
     const bool v3 = g_swin_variant != 1;
     swin_win3_launch(a, n_cu, (hipStream_t)stream, v3, v3 && glin, g_swin_variant == 16);
   } else {

@@ -363,9 +363,9 @@ template <bool SWM, bool GLIN>
 __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 sWv[C * C];              // W_v (every head), chunk-major
-  // local region one-hot per key as the 16x16x16 A operand, k-group-major: [g][key][4] (g > 0 zero),
-  // so the 64 lanes' 8-byte reads of a key tile hit distinct banks
-  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? 4 * L * 4 : 16];
+  // local region one-hot per key (regions 0..3 of 8 bf16): the A operand of the 16x16x32 mask product
+  // for every k group -- the B operand (qmask) is zero outside k 0..3, so lanes g > 0 may read it too
+  __shared__ __attribute__((aligned(16))) bf16 Oh[SWM ? L * 8 : 8];
   __shared__ __attribute__((aligned(16))) float sP[5 * C];              // LN gamma | beta | qkv bias
 
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
@@ -379,10 +379,8 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
   if constexpr (SWM) {
     for (int key = tid; key < L; key += NT5) {
       const int reg = local_region5(wloc, key, p.shift);
-      *reinterpret_cast<uint2*>(&Oh[key * 4]) = make_uint2(reg == 0 ? 0x3F80u : reg == 1 ? 0x3F800000u : 0u,
-                                                           reg == 2 ? 0x3F80u : reg == 3 ? 0x3F800000u : 0u);
-#pragma unroll
-      for (int gg = 1; gg < 4; ++gg) *reinterpret_cast<uint2*>(&Oh[(gg * L + key) * 4]) = make_uint2(0u, 0u);
+      st16(&Oh[key * 8], make_uint4(reg == 0 ? 0x3F80u : reg == 1 ? 0x3F800000u : 0u,
+                                    reg == 2 ? 0x3F80u : reg == 3 ? 0x3F800000u : 0u, 0u, 0u));
     }
   }
   s16x8 ones;
@@ -539,21 +537,24 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       // and carried (spilled) across P2, and the per-tile masks are hoisted out of the loop
       int wl = wloc;
       asm volatile("" : "+s"(wl));
-      s16x4 qmask;                            // B of the 16x16x16 mask product: -100/scale off the query's region
+      // B of the mask product: -100/scale at the regions other than the query's (k 0..3, lanes g = 0).
+      // (The 16x16x16 form with 2-VGPR operands was intermittently wrong: its LDS operand reload for
+      // the next key tile could land in registers an in-flight mask MFMA still had to read as SrcC --
+      // 1 launch in 5 when LDS was idle; tools/debug_swin_diff.py.)
+      s16x8 qmask;
       // window location 0 holds one region: its mask operand is zero (S + 0 is exact), which keeps
       // the tile free of a branch per key tile (branches split the MFMA / softmax schedule)
       if constexpr (MK) {
         const int qreg = local_region5(wl, rb + r16, p.shift);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) qmask[e] = masked && g == 0 && e != qreg ? neg : (short)0;
+        for (int e = 0; e < 8; ++e) qmask[e] = masked && g == 0 && e < 4 && e != qreg ? neg : (short)0;
       }
       f32x4 st[NTILE + 1];
 #pragma unroll
       for (int kt = 0; kt < NTILE; ++kt) {
         f32x4 a = mfma_bf16(kf[kt], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
         if constexpr (MK)
-          a = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*reinterpret_cast<const s16x4*>(&Oh[(g * L + kt * 16 + r16) * 4]),
-                                                        qmask, a, 0, 0, 0);
+          a = mfma_bf16(*reinterpret_cast<const s16x8*>(&Oh[(kt * 16 + r16) * 8]), qmask, a);
         st[kt] = a;
       }
       float mx = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));

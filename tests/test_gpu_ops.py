@@ -933,8 +933,8 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
 def test_swin_window_attention_fused_vs_unfused(shift, variant):
     """catseg_swin_window_attention == catseg_rows_gemm(LN1 + q/k/v + guidance) followed by
     catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry.
-    variant 0 = the default (the register-resident swin_win5 for unshifted blocks, swin_win3 for
-    shifted ones), 1 = the head-per-SIMD kernel with the builtin LDS-DMA and a row map per tile,
+    variant 0 = the register-resident kernel (default, swin_window.hip swin_win5: two 4-wave
+    workgroups per CU), 1 = the head-per-SIMD kernel with the builtin LDS-DMA and a row map per tile,
     2 = the row-tile-wave kernel, 3 = the head-per-SIMD kernel with the opaque LDS-DMA; S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
     B, T, HW, D = 1, 7, 576, 128
     S = B * T
@@ -992,8 +992,8 @@ def test_swin_window_attention_persistent_variants_agree(shift, glin):
     grid, guidance map of 2 images): the head-per-SIMD opaque-DMA kernel (variant 3, whose counted
     window-start wait lets the previous window's stores stay in flight, guidance rows from a per-window
     base) equals the builtin-DMA / per-tile row-map kernel (variant 1) bit for bit, and so does the
-    default (variant 0: for shift 0 the register-resident swin_win5 -- same LayerNorm, projection
-    and softmax arithmetic).  glin=False stores the guidance pixel-major
+    register-resident default (variant 0, swin_win5: same LayerNorm, projection, mask and softmax
+    arithmetic).  glin=False stores the guidance pixel-major
     (row = pixel * B + image), which no slice maps to one base + pixel: variants 3 and 0 then run
     swin_win3's per-tile row-map path."""
     B, T, HW, D = 2, 100, 576, 128

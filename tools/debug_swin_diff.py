@@ -1,4 +1,4 @@
-"""Where swin_variant 4 (swin_win5 for every block; the runs are listed as variant 0) differs from variant 3 (S = 200, shift 6, linear guidance map): rows that differ,
+"""Where swin_variant 0 (swin_win5) differs from variant 3 (swin_win3) (S = 200, shift 6, linear guidance map): rows that differ,
 by window location / slice / token, and whether variant 0 is deterministic run to run."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -24,7 +24,7 @@ shift = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 order = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "3,0,0,0,0,0").split(",")]
 outs = {}
 for v in order:
-    L.tune("swin_variant", 4 if v == 0 else v)
+    L.tune("swin_variant", v)
     o = torch.full((R, D), float("nan"), device=dev, dtype=dt)
     ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, o, S=S, img_hw=(24, 24), window=12, shift=shift,
                               n_heads=4, head_dim=32, scale=32 ** -0.5)
