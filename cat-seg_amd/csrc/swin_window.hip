@@ -538,9 +538,9 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       int wl = wloc;
       asm volatile("" : "+s"(wl));
       // B of the mask product: -100/scale at the regions other than the query's (k 0..3, lanes g = 0).
-      // (The 16x16x16 form with 2-VGPR operands was intermittently wrong: its LDS operand reload for
-      // the next key tile could land in registers an in-flight mask MFMA still had to read as SrcC --
-      // 1 launch in 5 when LDS was idle; tools/debug_swin_diff.py.)
+      // (The 16x16x16 form with 2-VGPR operands was intermittently wrong -- one wave's tile in ~1
+      // launch of 5, tools/debug_swin_diff.py; hipcc allocated its destination over its A operand,
+      // the K=16 bf16 MFMA defect DESIGN.md section 8 records for the ring conv.)
       s16x8 qmask;
       // window location 0 holds one region: its mask operand is zero (S + 0 is exact), which keeps
       // the tile free of a branch per key tile (branches split the MFMA / softmax schedule)
