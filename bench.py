@@ -41,7 +41,7 @@ sys.path.insert(0, ROOT)
 
 from cat_seg import ops  # noqa: E402
 from cat_seg import _lib as L  # noqa: E402
-from cat_seg.distributed import gather_logits  # noqa: E402
+from cat_seg.distributed import gather_logits, gather_logits_async  # noqa: E402
 from cat_seg.arch import VIT_B16, VIT_L14_336  # noqa: E402
 from cat_seg.engine import CatSegEngine  # noqa: E402
 from cat_seg.weights import synthesize_state_dict  # noqa: E402
@@ -168,7 +168,6 @@ def main():
     sizes = torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev)
     out = None if cfg5 else torch.empty(B, T, R, R, device=dev)
     gsize = eng.SLIDE_OUT if cfg5 else 4 * arch.grid
-    gathered = torch.empty(world * B, T, gsize, gsize, device=dev) if world > 1 else None
 
     def step():
         if cfg5:      # crops + head + Fold merge -> 640² probabilities at the image size (sem_seg_postprocess)
@@ -177,67 +176,85 @@ def main():
         ops.postprocess(logits, out, crop=(min(logits.shape[-2], R), min(logits.shape[-1], R)))
         return logits
 
+    # One compute stream carries the whole step (input copies, graph replays, eager launches).  With
+    # N > 1 the forward is captured twice (two graphs, each with its own logits buffer) and step i
+    # replays graph i % 2; over RCCL the logits all-gather of step i runs on the collective's own
+    # stream, after that replay and overlapped with step i+1's forward, and the replay of step i+2
+    # waits for gather i (which reads the buffer it rewrites).  gloo stages through the host and
+    # gathers synchronously after each step (same buffer ring, no overlap).
     stream = torch.cuda.Stream(device=dev)
-    graph = None
+    overlap = world > 1 and backend == "nccl"
+    nbuf = 2 if world > 1 else 1
+    graphs, g_logits = [], []
+    gathered = ([torch.empty(world * B, T, gsize, gsize, device=dev) for _ in range(nbuf)]
+                if world > 1 else None)
+    works = [None] * nbuf
     torch.cuda.synchronize()
-    with torch.no_grad():
+    with torch.no_grad(), torch.cuda.stream(stream):
         if not args.no_graph:
-            with torch.cuda.stream(stream):
-                step()            # allocate / warm the caching allocator outside capture
+            step()                # allocate / warm the caching allocator outside capture
             torch.cuda.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                g_logits = step()
+            for _ in range(nbuf):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream):
+                    g_logits.append(step())
+                graphs.append(g)
 
-        def forward_once():
-            if graph is not None:
-                graph.replay()
-                return g_logits
-            with torch.cuda.stream(stream):
-                return step()
+        def forward_once(i=0):
+            """Step i's forward on `stream` (the current stream inside run / the parity gate)."""
+            if graphs:
+                graphs[i % nbuf].replay()
+                return g_logits[i % nbuf]
+            return step()
 
-        def run():
-            lg = forward_once()
+        def run(i):
+            k = i % nbuf
+            if works[k] is not None:
+                works[k].wait()                    # gather i-2 has read the buffer this replay rewrites
+                works[k] = None
+            lg = forward_once(i)
             if world > 1:
-                with torch.cuda.stream(stream):
-                    gather_logits(lg, world * B, out=gathered)     # RCCL all-gather over xGMI
+                works[k] = gather_logits_async(lg, gathered[k])   # RCCL all-gather over xGMI
             return lg
 
-        for _ in range(args.warmup):
-            run()
+        for i in range(args.warmup):
+            run(i)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            run()
+        for i in range(args.steps):
+            run(args.warmup + i)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        last = (args.warmup + args.steps - 1) % nbuf
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64)
             t = t.to(dev) if backend == "nccl" else t
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = t.item()
         # multi-GPU parity gate: rank 0 recomputes every rank's seeded batch on its own GPU and
-        # compares with that rank's slice of the gathered logits, bit for bit
+        # compares with that rank's slice of the last step's gathered logits, bit for bit
         gather_ok = None
         if world > 1:
             ok = True
             if rank == 0:
+                ref = gathered[last].clone()
                 for r in range(world):
                     raw.copy_(synthetic_batch(r, B, S, dev))
-                    lg = forward_once()
+                    lg = forward_once(last)
                     torch.cuda.synchronize()
-                    ok = ok and torch.equal(gathered[r * B:(r + 1) * B], lg)
+                    ok = ok and torch.equal(ref[r * B:(r + 1) * B], lg)
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
             flag = flag.to(dev) if backend == "nccl" else flag
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             gather_ok = bool(flag.item())
             raw.copy_(synthetic_batch(rank, B, S, dev))
+            torch.cuda.synchronize()
     images = world * B * args.steps
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -271,11 +288,14 @@ def main():
                        "bench_config": args.config,
                        "global_batch": world * B, "classes": T, "resolution": R,
                        "parallelism": f"batch-shard x{world} + {backend} all-gather of logits" if world > 1 else "1 GPU",
-                       "hipgraph": graph is not None},
+                       "hipgraph": bool(graphs),
+                       "gather_overlap": overlap if world > 1 else None},
             "roofline": roofline,
-            "path_roofline": {"bound": "mfma", "achieved": round(path_tflops, 2), "peak": path_peak,
-                              "unit": "TFLOP/s", "gf_per_image": cfg["gf"],
-                              "frac": round(path_tflops / path_peak, 4)},
+            # the whole path's fraction of the dtype's dense peak; None with fp8 ViT GEMMs (a mix of
+            # fp8 and bf16 work has no single roof)
+            "path_roofline": None if vit_fp8 else {
+                "bound": "mfma", "achieved": round(path_tflops, 2), "peak": path_peak,
+                "unit": "TFLOP/s", "gf_per_image": cfg["gf"], "frac": round(path_tflops / path_peak, 4)},
             "cpu_baseline": cpu,
             "kernels": kernels,
         }

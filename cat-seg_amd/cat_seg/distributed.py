@@ -78,6 +78,26 @@ def gather_logits(local: torch.Tensor, n_total: int, group=None, out: Optional[t
     return out
 
 
+def gather_logits_async(local: torch.Tensor, out: torch.Tensor, group=None):
+    """Start the all-gather of equal-size per-rank logits into `out` (world * b rows, rank order)
+    and return its work handle, or None when it completed synchronously.
+
+    On a device backend (RCCL) the collective runs on its own stream: it starts after the work
+    already queued on the caller's current stream (which produces `local`), and `work.wait()` makes
+    the caller's current stream wait for it (before anything rewrites `local` or reads `out`).
+    gloo has no device all-gather: the host-staged gather_logits runs synchronously instead."""
+    rank, world = _world(group)
+    if out.shape[0] != world * local.shape[0] or out.shape[1:] != local.shape[1:]:
+        raise ValueError(f"gather_logits_async: out {tuple(out.shape)} is not world={world} x {tuple(local.shape)}")
+    if world == 1:
+        out.copy_(local)
+        return None
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        gather_logits(local, out.shape[0], group=group, out=out)
+        return None
+    return dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+
+
 def run_sharded(forward: Callable[[Sequence], torch.Tensor], items: Sequence, group=None) -> torch.Tensor:
     """Run `forward` on this rank's slice of `items` and all-gather the results.
 

@@ -6,6 +6,10 @@
 
 void catseg_set_error(const char* fmt, ...);
 
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount, cached per device):
+// persistent grids are sized from it, never from a literal 256 (partitioned parts expose fewer)
+int catseg_device_cus();
+
 // A/B knob registration (tuning.hip, include/catseg_hip_tuning.h): a process-wide int read at
 // launch, settable by name through catseg_tuning_set; not part of the product ABI.
 struct CatsegKnobReg { CatsegKnobReg(const char* name, int* value); };

@@ -367,13 +367,7 @@ extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream
   p.y = (bf16*)a->y; p.ld_y = a->ld_y;
   p.B = a->B; p.T = a->T; p.HW = a->HW;
   p.dbg = g_classattn_variant >= 16 ? g_classattn_variant - 16 : 0;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
+  const int cus = catseg_device_cus();
   const int64_t npix = a->B * a->HW;
   const unsigned grid = (unsigned)std::min<int64_t>(npix, 2LL * cus);
   hipStream_t st = (hipStream_t)stream;

@@ -763,12 +763,7 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
       configured = true;
     }
     if (W == 96 && g_head_variant == 0) {
-      static int n_cu = 0;
-      if (n_cu == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-          n_cu = 256;
-      }
+      const int n_cu = catseg_device_cus();
       const int RB = 24, ups = (H + RB - 1) / RB;
       const int64_t nunits = B * (int64_t)T * ups;
       CATSEG_CHECK(nunits < (1LL << 31), "conv3x3_head: too many bands");

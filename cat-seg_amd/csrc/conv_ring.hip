@@ -412,7 +412,7 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   // persistent grid: the workgroups that fit at once (OCC per CU, LDS permitting), a multiple of
   // nsplit; g_ring_persist 0 = one unit per workgroup (A/B)
   const int per_cu = std::max(1, std::min(OCC, (int)((160 * 1024) / std::max<size_t>(sh, 1))));
-  const int64_t cap = (int64_t)(256 * per_cu / nsplit) * nsplit;
+  const int64_t cap = (int64_t)(catseg_device_cus() * per_cu / nsplit) * nsplit;
   // enough units for every workgroup: >= 2048 workgroups when each takes one unit, >= 4 units
   // per workgroup when persistent (ring_persist 2; 1 keeps the one-unit band rule)
   const int64_t want = g_ring_persist == 2 ? 4 * cap / nsplit : 2048;

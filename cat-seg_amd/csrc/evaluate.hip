@@ -28,8 +28,11 @@ __global__ __launch_bounds__(256) void confusion_kernel(const float* __restrict_
   int arg = 0;
   for (int64_t t = 1; t < T; ++t) {
     const float v = probs[t * HW + p];
-    // strict >: the first maximum wins; NaN ranks above every number (torch.argmax)
-    if (best == best && (v > best || v != v)) {
+    // strict >: the first maximum wins; NaN ranks above every number (torch.argmax).  NaN is
+    // tested on the bits, so the rule holds whatever float mode the file is built with
+    const bool best_nan = (__float_as_uint(best) & 0x7fffffffu) > 0x7f800000u;
+    const bool v_nan = (__float_as_uint(v) & 0x7fffffffu) > 0x7f800000u;
+    if (!best_nan && (v_nan || v > best)) {
       best = v;
       arg = (int)t;
     }

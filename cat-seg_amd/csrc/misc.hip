@@ -15,6 +15,18 @@ void catseg_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* catseg_last_error(void) { return g_err; }
+
+int catseg_device_cus() {
+  static int cached[64];   // per device ordinal; 0 = not yet queried
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
 extern "C" int catseg_abi_version(void) { return 1; }
 
 namespace {
@@ -698,13 +710,7 @@ extern "C" int catseg_corr_embed(const float* corr, int64_t corr_t_stride, int64
   CATSEG_CHECK(sh <= 64 * 1024, "corr_embed: slice too large for LDS");
   const unsigned grid = (unsigned)(B * T);
   if (dtype == CATSEG_BF16 && hidden == 128 && (H + 6) * (W + 6) <= 1024 && H * W <= 768 && g_corr_mfma) {
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
-    }
+    const int cus = catseg_device_cus();
     const unsigned pgrid = (unsigned)std::min<int64_t>(B * T, (int64_t)cus * 2);
     hipLaunchKernelGGL(corr_embed_mfma_kernel, dim3(pgrid), dim3(256), 0, (hipStream_t)stream, corr, corr_t_stride,
                        corr_b_stride, classes, B * (int64_t)T, T, H, W, weight, bias, (bf16*)out, g_corr_mfma != 2 ? 1 : 0);

@@ -724,13 +724,7 @@ PEpi make_pepi(const CatsegRowsEpi* p) {
 }
 
 unsigned persist_grid(int64_t M, int per_cu = 1) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
+  const int cus = catseg_device_cus();
   const int64_t tiles = (M + BM - 1) / BM;
   return (unsigned)std::min<int64_t>(tiles, (int64_t)cus * per_cu);
 }

@@ -322,12 +322,7 @@ extern "C" int catseg_swin_window_attention(const CatsegSwinAttnArgs* a, void* s
   p.out = (bf16*)a->out; p.ld_out = a->ld_out;
   p.shift = a->shift; p.scale = a->scale;
   // persistent: one workgroup per CU (W_qkv staged once per CU), windows strided over them
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
+  const int n_cu = catseg_device_cus();
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
   const bool glin = gmap_linear_in_pixel(a->gmap);

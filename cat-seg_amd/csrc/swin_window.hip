@@ -151,6 +151,9 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
   };
   int win = blockIdx.x;
   if (win < nwin_total) fetch(win);
+  // the first window's rows: retired here, outside the window loop, so that the counted wait at
+  // the loop top is only ever reached from the previous window's P3 (tools/isa_lint.py R3)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint64_t* stp = reinterpret_cast<uint64_t*>(p.out + (int64_t)(nwin_total / NWIN) * IMG * IMG * p.ld_out) +
                   ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * 32;
   int it = 0;
@@ -160,9 +163,10 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
   for (; win < nwin_total; win += gridDim.x, ++it) {
     const int slice = win / NWIN, wloc = win % NWIN;
     stamp(0);
-    // this wave's DMA of the window landed: after the first window only the P3 stores (2 per
-    // row tile, >= 8 per wave) were issued behind it, and those may stay in flight
-    if (!ASMDMA || win == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's DMA of the window landed: only the previous window's P3 stores (2 per row tile,
+    // >= 8 per wave) were issued behind it, and those may stay in flight (the first window's DMA
+    // was retired before the loop)
+    if (!ASMDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();                                       // every wave's DMA visible; P3 done
     stamp(1);
@@ -400,6 +404,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
   };
   int win = blockIdx.x;
   if (win < nwin_total) fetch(win);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first window's rows, retired outside the loop
   __syncthreads();
   for (; win < nwin_total; win += gridDim.x) {
     const int slice = win / NWIN;
@@ -408,10 +413,10 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
     int lane_w = lane;
     asm volatile("" : "+v"(lane_w));
     const int r16 = lane_w & 15, g = lane_w >> 4, lc = lane_w & 15, lrow0 = 4 * h + (lane_w >> 4);
-    // this wave's DMA of the window landed (only the previous window's >= 18 output stores were
-    // issued behind it and may stay in flight)
-    if (win == (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    // this wave's DMA of the window landed: only the previous window's 18 output stores were
+    // issued behind it and may stay in flight (the first window's DMA was retired before the loop;
+    // tools/isa_lint.py R3 checks the count on every path of the shipped code object)
+    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
     __syncthreads();
     // W_q / W_k of head h (A fragments: rows 16dt + r16 of the head, k = 32ks + 8g ..), L2-resident
     s16x8 wf[2][2][4];

@@ -91,6 +91,47 @@ def test_gloo_world2_gather_is_exact_copy(n_items):
         assert torch.equal(g, want)
 
 
+def _ring_worker(rank, world, port, out_dir):
+    """bench.py's N > 1 loop shape on gloo/CPU: a two-buffer ring of per-step logits, each step's
+    gather started with gather_logits_async and waited for two steps later (before its buffer is
+    rewritten); every gathered block must equal that step's per-rank logits."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = 3
+        bufs = [torch.empty(b, 5, 4, 4) for _ in range(2)]
+        gathered = [torch.empty(world * b, 5, 4, 4) for _ in range(2)]
+        works = [None, None]
+        seen = []
+        for i in range(5):
+            k = i % 2
+            if works[k] is not None:
+                works[k].wait()
+                seen.append(gathered[k].clone())      # step i-2's gather, complete
+            bufs[k].copy_(torch.arange(b * 80, dtype=torch.float32).view(b, 5, 4, 4) + 1000 * rank + 10 * i)
+            works[k] = D.gather_logits_async(bufs[k], gathered[k])
+        for k in (1, 0):                               # steps 3, 4
+            if works[k] is not None:
+                works[k].wait()
+            seen.append(gathered[k].clone())
+        torch.save(torch.stack(seen), os.path.join(out_dir, f"ring{rank}.pt"))
+        with pytest.raises(ValueError):
+            D.gather_logits_async(bufs[0], torch.empty(world * b + 1, 5, 4, 4))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_async_gather_ring():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ring_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        got = [torch.load(os.path.join(d, f"ring{r}.pt"), weights_only=True) for r in range(world)]
+    base = torch.arange(3 * 80, dtype=torch.float32).view(3, 5, 4, 4)
+    want = torch.stack([torch.cat([base + 1000 * r + 10 * i for r in range(world)]) for i in range(5)])
+    for g in got:
+        assert torch.equal(g, want)
+
+
 def test_world1_is_identity():
     x = torch.randn(3, 4)
     assert D.gather_logits(x, 3) is x

@@ -28,12 +28,15 @@ def _bench(*args, timeout=400):
 
 @pytest.mark.timeout(500)
 def test_bench_two_ranks_gloo_on_one_gpu():
-    line = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-images", "0", "--no-roofline",
+    # 3 timed steps after 1 warm-up: both graphs of the two-buffer ring replay, and the gate checks
+    # the last step's gathered logits (ring slot 1)
+    line = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--cpu-images", "0", "--no-roofline",
                   "--backend", "gloo")
     assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["backend"] == "gloo"
     assert line["gather_matches_1gpu"] is True
+    assert line["config"]["hipgraph"] is True and line["config"]["gather_overlap"] is False
     assert line["config"]["global_batch"] == 16
-    assert line["value"] > 0 and line["steps"] == 2
+    assert line["value"] > 0 and line["steps"] == 3
 
 
 @pytest.mark.timeout(400)

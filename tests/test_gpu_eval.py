@@ -44,6 +44,25 @@ def test_confusion_kernel_bit_exact(T, H, W, clamp):
     assert np.array_equal(conf.cpu().numpy().reshape(n1, n1), ref)
 
 
+def test_confusion_kernel_nan_ranks_highest():
+    """torch.argmax / numpy argmax rank NaN above every number (the first NaN wins); the kernel
+    tests NaN on the bits, whatever float mode evaluate.hip is built with."""
+    probs, gt = _case(9, 16, 20, seed=7)
+    probs[3, 0, :5] = float("nan")         # NaN at a class index > 0
+    probs[5, 1, :] = float("nan")
+    probs[2, 1, ::2] = float("nan")        # two NaNs: the first (class 2) wins
+    probs[0, 2, :3] = float("nan")         # NaN at class 0
+    probs[7, 3, 4] = float("inf")
+    probs[8, 3, 4] = float("nan")
+    conf = torch.zeros(100, dtype=torch.int64, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ops.semseg_confusion(probs.cuda(), gt.cuda(), conf, bad, num_classes=9, ignore_label=255)
+    ref = OE.confusion_update(np.zeros((10, 10), np.int64), probs.numpy(), gt.numpy(), 9, 255)
+    pred = probs.argmax(0)
+    assert int(pred[0, 0]) == 3 and int(pred[1, 0]) == 2 and int(pred[1, 1]) == 5 and int(pred[3, 4]) == 8
+    assert np.array_equal(conf.cpu().numpy().reshape(10, 10), ref)
+
+
 def test_confusion_kernel_counts_invalid_labels():
     probs, gt = _case(5, 8, 8, seed=3)
     gt[0, 0] = 7          # not a class, not ignore
