@@ -91,9 +91,17 @@ class CatSegEngine:
         ops.quant_fp8_rows(wf, q, sc)
         return q, sc
 
-    def _block(self, sd, p, dense=False, fp8=False):
+    def _block(self, sd, p, dense=False, fp8=False, heads=0):
+        """One ResidualAttentionBlock's weights.  heads > 0 (bf16 ViT image blocks): the q rows of the
+        in-projection (weight and bias) are multiplied by head_dim^-0.5 * log2(e) in fp32 before the
+        bf16 / e4m3 rounding, for catseg_attention mode 2 (the scores come out of q.k in log2 units)."""
         width = sd[p + "attn.q_proj_weight"].shape[0]
         b = sd[p + "attn.in_proj_bias"]
+        wq = sd[p + "attn.q_proj_weight"]
+        if heads and not dense:
+            c = (width // heads) ** -0.5 * 1.4426950408889634
+            wq = wq.float() * c
+            b = torch.cat([b[:width].float() * c, b[width:].float()])
         blk = _NS(
             ln1w=self._F(sd[p + "ln_1.weight"]), ln1b=self._F(sd[p + "ln_1.bias"]),
             wo=self._W(sd[p + "attn.out_proj.weight"]), bo=self._F(sd[p + "attn.out_proj.bias"]),
@@ -101,11 +109,13 @@ class CatSegEngine:
             wfc=self._W(sd[p + "mlp.c_fc.weight"]), bfc=self._F(sd[p + "mlp.c_fc.bias"]),
             wpr=self._W(sd[p + "mlp.c_proj.weight"]), bpr=self._F(sd[p + "mlp.c_proj.bias"]),
         )
+        wqkv = None if dense else torch.cat([wq.float(), sd[p + "attn.k_proj_weight"].float(),
+                                             sd[p + "attn.v_proj_weight"].float()], 0)
         if dense:   # forward_dense: v path only (model_vpt.py:219-240)
             blk["wv"] = self._W(sd[p + "attn.v_proj_weight"])
             blk["bv"] = self._F(b[2 * width:])
         else:
-            blk["wqkv"] = self._W(torch.cat([sd[p + f"attn.{x}_proj_weight"] for x in "qkv"], 0))
+            blk["wqkv"] = self._W(wqkv)
             blk["bqkv"] = self._F(b)
         if fp8:
             g = self.vit_fp8_gemms
@@ -118,7 +128,7 @@ class CatSegEngine:
             if "wqkv" in g and dense:
                 blk["q8_wv"] = self._Q8(sd[p + "attn.v_proj_weight"])
             elif "wqkv" in g:
-                blk["q8_wqkv"] = self._Q8(torch.cat([sd[p + f"attn.{x}_proj_weight"] for x in "qkv"], 0))
+                blk["q8_wqkv"] = self._Q8(wqkv)
         return blk
 
     @staticmethod
@@ -174,8 +184,11 @@ class CatSegEngine:
             pos = torch.cat([pos[:1], out], 0).contiguous()
         w.pos = pos
         w.ln_pre = (self._F(sd[p + "ln_pre.weight"]), self._F(sd[p + "ln_pre.bias"]))
+        # bf16: the image blocks' q projection carries the softmax scale in log2 units (attention mode 2)
+        self.vit_l2s = self.dt == torch.bfloat16 and W // a.vision_heads == 64
         w.vblocks = [self._block(sd, f"{p}transformer.resblocks.{i}.", dense=(i == a.vision_layers - 1),
-                                 fp8=self.vit_fp8) for i in range(a.vision_layers)]
+                                 fp8=self.vit_fp8, heads=a.vision_heads if self.vit_l2s else 0)
+                     for i in range(a.vision_layers)]
         w.ln_post = (self._F(sd[p + "ln_post.weight"]), self._F(sd[p + "ln_post.bias"]))
         w.proj_t = self._W(sd[p + "proj"].t())
         # ---------------- CLIP text ----------------
@@ -301,8 +314,9 @@ class CatSegEngine:
             return fp8_lin(a, blk["q8_" + name], out, **kw)
         return ops.gemm(a, blk[name], out, **kw)
 
-    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None, fp8=False):
-        """ResidualAttentionBlock.forward over a stack (model_vpt.py:208-217, 256-266)."""
+    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None, fp8=False, l2s=False):
+        """ResidualAttentionBlock.forward over a stack (model_vpt.py:208-217, 256-266).  l2s: the blocks'
+        q projections carry scale * log2(e) (_block heads > 0): attention mode 2."""
         M, width = x.shape
         dt, dev = self.dt, self.device
         h = torch.empty(M, width, device=dev, dtype=dt)
@@ -315,7 +329,7 @@ class CatSegEngine:
             self._ln_linear(f8, x, blk.ln1w, blk.ln1b, h, blk, "wqkv", qkv, bias=blk.bqkv)
             ops.attention(qkv[:, :width], qkv[:, width:2 * width], qkv[:, 2 * width:], o,
                           n_seq=n_seq, seq_len=seq_len, n_heads=n_heads, head_dim=width // n_heads,
-                          scale=(width // n_heads) ** -0.5, causal=causal)
+                          scale=(width // n_heads) ** -0.5, causal=causal, mode=2 if l2s else 0)
             x_new = torch.empty_like(x) if fresh else x
             self._linear(f8, o, blk, "wo", x_new, bias=blk.bo, res=x)
             x = x_new
@@ -396,7 +410,7 @@ class CatSegEngine:
         ops.vit_embed(patches, w.cls, w.pos, *w.ln_pre, x, B=B, G2=G2, width=W)
         hooks: List[torch.Tensor] = []
         x = self._resblocks(x, w.vblocks[:-1], B, Lt, a.vision_heads, False,
-                            hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8)
+                            hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8, l2s=self.vit_l2s)
         if a.vision_layers - 1 in a.hook_layers:
             raise NotImplementedError("hook on the dense block")
         # forward_dense (model_vpt.py:219-240)

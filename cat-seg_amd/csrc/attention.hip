@@ -298,184 +298,26 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
 
 // ------------------------------------------------------------------------------------
 // CLIP ViT MHA (bf16, head_dim 64, dense, non-causal; model_vpt.py:202-206), one wave per
-// 16 queries of one (image, head), NW waves sharing 64-key K/V blocks in LDS.
-//   * K/V staging is register-double-buffered: block b+1's global loads are issued before
-//     block b's MFMAs and written to the other LDS buffer after them, one barrier per block.
-//     Rows past L read the clamped row L-1 (no per-element branch); their scores are masked.
+// 16 queries of one (image, head), NW waves sharing 64-key K/V blocks.  LDS-DMA ring: the K / V
+// blocks arrive by global_load_lds (no staging VGPRs, no staging VALU) into a 4-slot ring with two
+// blocks in flight beyond the one being read, so the load latency is covered by two blocks of
+// compute; one raw barrier per block (each wave retires its own pieces with a counted vmcnt
+// first).  The LDS images are unpadded 128-byte rows with the 16-byte chunk XOR-swizzled by
+// row & 7 (applied to the per-lane DMA source, so the lane-linear DMA destination lands the
+// swizzled image): K fragment reads (ds_read_b128) and V^T transposed reads (ds_read_b64_tr_b16)
+// are conflict-free.
 //   * Defer-max online softmax (cdna_hip_programming.md T13): the running max m of a query
 //     moves only when a block's scores exceed it by more than 2^THR in exp2 units, so the
 //     common block costs one max chain per lane and one wave vote -- no cross-lane reduction,
 //     no rescale of O.  The softmax is invariant to the subtracted constant; p <= 2^THR.
 //   * Row sums l from the MFMA (all-ones A fragment times P^T), as attn_kernel.
+//   * Rows past L read the clamped row L-1 (no per-element branch); their scores are masked.
 // ------------------------------------------------------------------------------------
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void vit_attn_kernel(AttnP p) {
-  constexpr int D = 64, KB = 64, KP = D + 16, NT = NW * 64;
-  constexpr int CH = KB * D / 8;                        // 16-byte chunks per K (or V) block
-  constexpr int BUF = 2 * KB * KP;                      // K then V of one block
-  constexpr int NC = (2 * CH + NT - 1) / NT;            // chunks staged per thread
-  constexpr float THR = 16.f;                           // defer-max threshold (log2 units)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // all query blocks of one (sequence, head) on one XCD: its K / V are fetched into one L2
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-  const int bx = lin % gridDim.x, by = lin / gridDim.x;
-  const int s = by / p.H, h = by % p.H;
-  const int g = lane >> 4, col = lane & 15;
-  const int L = p.L;
-  const float sl2 = p.scale * 1.4426950408889634f;
-  const int q0 = (bx * NW + wave) * 16;
-  const bool live = q0 < L;                             // wave-uniform
-  const int qi = q0 + col;
-  const bool q_ok = qi < L;
-  const int64_t row0 = (int64_t)s * L;
-
-  s16x8 qf[2];
-  {
-    const bf16* Q = reinterpret_cast<const bf16*>(p.q) + (row0 + (q_ok ? qi : 0)) * p.ld + h * D;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint4 u = q_ok ? ld16(Q + ks * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
-      qf[ks] = *reinterpret_cast<s16x8*>(&u);
-    }
-  }
-  // staging: chunk c < CH is K (key c/8, d 8*(c%8)), CH <= c < 2CH the same for V.  The source
-  // pointer advances by one block of rows per block; rows past L re-read row L-1 (no branch)
-  const bf16* src[NC];
-  const bf16* last[NC];
-  int dst[NC], skey[NC];
-  bool sok[NC];
-#pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = tid + i * NT;
-    sok[i] = c < 2 * CH;
-    const int cc = sok[i] ? c : 0, which = cc / CH, kk = (cc % CH) / 8, d0 = (cc % 8) * 8;
-    skey[i] = kk;
-    const bf16* base = reinterpret_cast<const bf16*>(which ? p.v : p.k) + row0 * p.ld + h * D + d0;
-    src[i] = base + (int64_t)kk * p.ld;
-    last[i] = base + (int64_t)(L - 1) * p.ld;
-    dst[i] = (which * KB * KP + kk * KP + d0) * 2;      // bytes
-  }
-  const int64_t bstep = (int64_t)KB * p.ld;
-  uint4 stg[NC];
-  auto gload = [&](int blk) {
-#pragma unroll
-    for (int i = 0; i < NC; ++i)
-      if (sok[i]) stg[i] = ld16(blk * KB + skey[i] < L ? src[i] + blk * bstep : last[i]);
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NC; ++i)
-      if (sok[i]) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(smem) + buf * BUF * 2 + dst[i]) = stg[i];
-  };
-
-  f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f;
-  s16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;   // bf16 1.0
-  // per-lane LDS bases: K fragment row col / chunk g, V^T transposed-read row 4g + col/4
-  const int kbase = (col * KP + 8 * g) * 2;
-  const int vbase = (KB * KP + (4 * g + (col >> 2)) * KP + 4 * (col & 3)) * 2;
-
-  // one 64-key block from LDS buffer `buf`; TAIL: keys k0 .. k0 + 63 may pass L (masked)
-  auto block = [&](int blk, int buf, auto tail_tag) {
-    constexpr bool TAIL = decltype(tail_tag)::value;
-    const char* Kb = reinterpret_cast<const char*>(smem) + buf * BUF * 2 + kbase;
-    const char* Vb = reinterpret_cast<const char*>(smem) + buf * BUF * 2 + vbase;
-    const int k0 = blk * KB;
-    f32x4 st[4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      if (!TAIL || k0 + kt * 16 < L) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          a = mfma_bf16(*reinterpret_cast<const s16x8*>(Kb + (kt * 16 * KP + ks * 32) * 2), qf[ks], a);
-      }
-      st[kt] = a;
-    }
-    if constexpr (TAIL) {
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (k0 + kt * 16 + 4 * g + r >= L) st[kt][r] = -INFINITY;
-    }
-    float lm = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
-#pragma unroll
-    for (int kt = 1; kt < 4; ++kt)
-      lm = fmaxf(lm, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
-    if (__any((lm - m_run) * sl2 > THR)) {               // rare after the first block
-      const float m_new = fmaxf(m_run, xrow4_max(lm));
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
-      m_run = m_new;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] *= alpha;
-      osum *= alpha;
-    }
-    const float nb = -m_run * sl2;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sl2, nb));
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (TAIL && k0 + 32 * u >= L) continue;            // P = 0 on all 32 keys
-      uint4 pu = make_uint4(f2bf2(st[2 * u][0], st[2 * u][1]), f2bf2(st[2 * u][2], st[2 * u][3]),
-                            f2bf2(st[2 * u + 1][0], st[2 * u + 1][1]), f2bf2(st[2 * u + 1][2], st[2 * u + 1][3]));
-      const s16x8 pb = *reinterpret_cast<s16x8*>(&pu);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        // V^T fragment (d = 16 dt + col over keys 32u + 4g + r and + 16): transposed reads
-        const char* vr = Vb + (32 * u * KP + dt * 16) * 2;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vr + 16 * KP * 2));
-        o[dt] = mfma_bf16(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, pb, o[dt]);
-      }
-      osum = mfma_bf16(ones, pb, osum);
-    }
-  };
-
-  const int nblk = (L + KB - 1) / KB;
-  const int nfull = L / KB;                              // blocks with every key < L
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int blk = 0; blk < nblk; ++blk) {
-    const int buf = blk & 1;
-    if (blk + 1 < nblk) gload(blk + 1);
-    if (live) {
-      if (blk < nfull) block(blk, buf, std::false_type{});
-      else block(blk, buf, std::true_type{});
-    }
-    if (blk + 1 < nblk) sstore(buf ^ 1);
-    __syncthreads();
-  }
-  if (!q_ok) return;
-  const float inv = 1.f / osum[0];
-  bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
-    store4<bf16>(O + dt * 16 + 4 * g, v);
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// ViT MHA, LDS-DMA ring form: the K / V blocks arrive by global_load_lds (no staging VGPRs,
-// no staging VALU) into a 4-slot ring with two blocks in flight beyond the one being read, so
-// the load latency is covered by two blocks of compute; one raw barrier per block (each wave
-// retires its own pieces with a counted vmcnt first).  The LDS images are unpadded 128-byte
-// rows with the 16-byte chunk XOR-swizzled by row & 7 (applied to the per-lane DMA source, so
-// the lane-linear DMA destination lands the swizzled image): K fragment reads (ds_read_b128)
-// and V^T transposed reads (ds_read_b64_tr_b16) are conflict-free.  Softmax, row sums and the
-// output are vit_attn_kernel's.
-// ------------------------------------------------------------------------------------
-template <int NW, int QT>
+// L2S (mode 2): the q rows arrive multiplied by scale * log2(e) (folded into the q projection's
+// weights and bias), so S = K Q^T is already the exponent in log2 units.  The running max then
+// enters as the MFMA's accumulator input (C = -m), S - m comes out of the matrix pipe, and the
+// softmax is one v_exp per score (no scale / subtract FMA); block 0 seeds the max.
+template <int NW, int QT, bool L2S = false>
 __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(AttnP p) {   // two workgroups per CU
   constexpr int D = 64, KB = 64, NBUF = 4, AHEAD = 2;
   constexpr int BLK = 2 * KB * D;                       // elements of one ring slot (K rows, then V rows)
@@ -557,10 +399,16 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
     const char* S0 = reinterpret_cast<const char*>(smem + (blk % NBUF) * BLK);
     const int k0 = blk * KB;
     f32x4 st[QT][4];
+    f32x4 cinit[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const float c = L2S && blk > 0 ? -m_run[t] : 0.f;
+      cinit[t] = f32x4{c, c, c, c};
+    }
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-      for (int t = 0; t < QT; ++t) st[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < QT; ++t) st[t][kt] = cinit[t];
       if (!TAIL || k0 + kt * 16 < L) {
         const s16x8 k0f = *reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff0);
         const s16x8 k1f = *reinterpret_cast<const s16x8*>(S0 + kt * 16 * 128 + koff1);
@@ -584,6 +432,28 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
 #pragma unroll
       for (int kt = 1; kt < 4; ++kt)
         lm = fmaxf(lm, fmaxf(fmaxf(st[t][kt][0], st[t][kt][1]), fmaxf(st[t][kt][2], st[t][kt][3])));
+      if constexpr (L2S) {
+        // st = S - m_run already (block 0: S, with m_run unset); rescale when a query's block max
+        // passes the running max by more than THR (block 0: always, to seed it)
+        if (blk == 0 || __any(lm > THR)) {
+          const float d = blk == 0 ? xrow4_max(lm) : fmaxf(xrow4_max(lm), 0.f);
+          if (blk > 0) {
+            const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[t][i] *= alpha;
+            osum[t] *= alpha;
+            m_run[t] += d;
+          } else {
+            m_run[t] = d;
+          }
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) st[t][kt] -= f32x4{d, d, d, d};
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st[t][kt][r] = __builtin_amdgcn_exp2f(st[t][kt][r]);
+      } else {
       if (__any((lm - m_run[t]) * sl2 > THR)) {          // rare after the first block
         const float m_new = fmaxf(m_run[t], xrow4_max(lm));
         const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * sl2);
@@ -597,6 +467,7 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) st[t][kt][r] = __builtin_amdgcn_exp2f(fmaf(st[t][kt][r], sl2, nb));
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         uint4 pu = make_uint4(f2bf2(st[t][2 * u][0], st[t][2 * u][1]), f2bf2(st[t][2 * u][2], st[t][2 * u][3]),
@@ -664,16 +535,10 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   }
 }
 
-template <int NW>
-void launch_vit(const AttnP& p, hipStream_t st) {
-  dim3 grid((unsigned)((p.L + 16 * NW - 1) / (16 * NW)), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((vit_attn_kernel<NW>), grid, dim3(NW * 64), 0, st, p);
-}
-
-template <int NW, int QT>
+template <int NW, int QT, bool L2S = false>
 void launch_vit3(const AttnP& p, hipStream_t st) {
   dim3 grid((unsigned)((p.L + 16 * NW * QT - 1) / (16 * NW * QT)), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((vit_attn3_kernel<NW, QT>), grid, dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((vit_attn3_kernel<NW, QT, L2S>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
@@ -690,39 +555,33 @@ void launch_win(const AttnP& p, hipStream_t st) {
 }
 
 int g_attn_tail_skip = 1;
-int g_attn_variant = 0;   // dense-path tiling (catseg_set_attn_variant; 0 = default)
+int g_attn_variant = 0;   // dense path: 0 = default, 7 = the generic tiling (tests)
 
 template <typename T, int D>
 void launch_dense(const AttnP& p, hipStream_t st) {
   if (p.causal) { launch<T, D, 4, 64, 2, 0, false, true>(p, st); return; }
   if constexpr (sizeof(T) == 2 && D == 64) {
-    // the ViT MHA kernels, ViT-L/14 shape (tools/micro_attn.py, XCD-remapped grids): LDS-DMA
-    // ring 8 waves 28.3 us, register-staged 10 waves 29.2, generic tiling (variant 7) 28.5;
-    // measured before the remap: ring 10 waves 33.2, ring 5 waves x 2 query tiles 37.1,
-    // 4 x 2 31.6 (the shared K / V^T fragment reads did not pay for the lost occupancy)
-    if (g_attn_variant == 0) { launch_vit3<8, 1>(p, st); return; }
-    if (g_attn_variant == 8) { launch_vit<10>(p, st); return; }
+    // the ViT MHA kernel (LDS-DMA ring, 8 waves, XCD-remapped grid); attn_variant 7 forces the
+    // generic tiling (the exact-max cross-check of the defer-max tests)
+    if (g_attn_variant != 7) { launch_vit3<8, 1>(p, st); return; }
   }
-  switch (g_attn_variant) {
-    case 1: launch<T, D, 4, 64, 2, 0, false, false>(p, st); break;
-    case 2: launch<T, D, 4, 128, 2, 0, false, false>(p, st); break;
-    case 3: launch<T, D, 8, 128, 1, 0, false, false>(p, st); break;
-    case 4: launch<T, D, 8, 64, 2, 0, false, false>(p, st); break;
-    case 5: launch<T, D, 10, 64, 1, 0, false, false>(p, st); break;
-    case 6: launch<T, D, 8, 64, 1, 0, false, false>(p, st); break;
-    case 7:
-    default:
-      // 10 waves x 16 queries when that needs fewer query blocks than 8 x 16 (ViT L = 577:
-      // 4 blocks of 160 vs 5 of 128 -> 512 workgroups, two per CU, no ragged third round):
-      // 30.0 vs 31.3 us; 5 x 2 tiles 33.1, 12 waves 31.6, 16 waves 43.2, 10 x 128 keys 34.0
-      if ((p.L + 159) / 160 < (p.L + 127) / 128) launch<T, D, 10, 64, 1, 0, false, false>(p, st);
-      else launch<T, D, 8, 64, 1, 0, false, false>(p, st);
-      break;
-  }
+  // generic tiling: 10 waves x 16 queries when that needs fewer query blocks than 8 x 16 (ViT
+  // L = 577: 4 blocks of 160 vs 5 of 128 -> 512 workgroups, two per CU, no ragged third round)
+  if ((p.L + 159) / 160 < (p.L + 127) / 128) launch<T, D, 10, 64, 1, 0, false, false>(p, st);
+  else launch<T, D, 8, 64, 1, 0, false, false>(p, st);
 }
+
+int g_attn_l2s_nw = 8;   // mode-2 ViT kernel: waves per workgroup (8 or 10; tools/micro_attn.py)
 
 template <typename T>
 int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
+  if (p.mode == 2) {
+    if constexpr (sizeof(T) != 2) return -1;
+    if (head_dim != 64 || p.causal) return -1;
+    if (g_attn_l2s_nw == 10) launch_vit3<10, 1, true>(p, st);
+    else launch_vit3<8, 1, true>(p, st);
+    return 0;
+  }
   if (p.mode == 1) {
     if (head_dim == 32 && p.img_h == 24 && p.img_w == 24 && p.ws == 12) { launch_win<T, 32, 9, 160, 1, 24>(p, st); return 0; }
     if (head_dim == 32 && p.L <= 160) { launch_win<T, 32, 9, 160, 1, 0>(p, st); return 0; }
@@ -738,6 +597,7 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
 
 CATSEG_KNOB(g_attn_variant, "attn_variant");
 CATSEG_KNOB(g_attn_tail_skip, "attn_tail_skip");
+CATSEG_KNOB(g_attn_l2s_nw, "attn_l2s_nw");
 
 extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");
@@ -757,6 +617,9 @@ extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
     CATSEG_CHECK(a->seq_len == a->window * a->window, "attention: seq_len must be window^2");
     CATSEG_CHECK(a->shift >= 0 && a->shift < a->window, "attention: bad shift");
     CATSEG_CHECK(!a->causal, "attention: causal not supported for windows");
+  } else if (a->mode == 2) {
+    CATSEG_CHECK(a->dtype == CATSEG_BF16 && a->head_dim == 64 && !a->causal,
+                 "attention: mode 2 (log2-scaled q) is bf16, head_dim 64, non-causal");
   } else {
     CATSEG_CHECK(a->mode == 0, "attention: bad mode");
   }

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 
 }  // namespace
 
-// 2 = 16 LayerNorm row steps per batch, 3 = biases in registers (A/B); >= 16: diagnostics (dbg = v - 16)
+// >= 16: diagnostics (dbg = v - 16: LN / stage-B rows all row 0, phase stamps); 0 = default
 int g_classattn_variant = 0;
 CATSEG_KNOB(g_classattn_variant, "classattn_variant");
 
@@ -371,8 +371,6 @@ extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream
   const int64_t npix = a->B * a->HW;
   const unsigned grid = (unsigned)std::min<int64_t>(npix, 2LL * cus);
   hipStream_t st = (hipStream_t)stream;
-  if (g_classattn_variant == 2) hipLaunchKernelGGL(classattn2_kernel<16>, dim3(grid), dim3(NT), 0, st, p);
-  else if (g_classattn_variant == 3) hipLaunchKernelGGL((classattn2_kernel<8, false>), dim3(grid), dim3(NT), 0, st, p);
-  else hipLaunchKernelGGL(classattn2_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL(classattn2_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
   return catseg_launch_status("class_attention");
 }

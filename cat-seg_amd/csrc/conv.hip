@@ -46,7 +46,16 @@ template <typename T, int BN>
 __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
   constexpr int VN = Vec16<T>::N;
   constexpr int CPR = BK / VN;
-  constexpr int LDR = BK + (sizeof(T) == 2 ? 8 : 4);
+  // bf16 tiles: unpadded 64-byte rows, 16-byte chunk ch of row r stored at slot ch ^ g[(r >> 2) & 3]
+  // with g = {0, 2, 3, 1}: the 16 (row, chunk) pairs of every ds_read_b128 lane group of a fragment
+  // read land in 16 distinct bank slots, and each ds_write_b128 group of the staging store writes
+  // two whole rows (was: +8-element pad, 2-way conflicts on both, ~50 % SQ_LDS_BANK_CONFLICT)
+  constexpr int LDR = BK + (sizeof(T) == 2 ? 0 : 4);
+  static_assert(sizeof(T) != 2 || BK == 32, "bf16 swizzle assumes 4 chunks per row");
+  auto soff = [](int row, int col) {       // element offset of (row, col), col a multiple of VN
+    if constexpr (sizeof(T) == 2) return row * LDR + ((((col >> 3) ^ (0x1320 >> (4 * ((row >> 2) & 3)))) & 3) << 3);
+    else return row * LDR + col;
+  };
   constexpr int A_CH = BM * CPR / NT;
   constexpr int W_TOT = BN * CPR, W_CH = (W_TOT + NT - 1) / NT;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -122,12 +131,12 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
       uint4 u = ra[i];
       if (a_zero[i]) u = make_uint4(0, 0, 0, 0);
       else if (a_gci[i] >= 0) u = gn_chunk<T>(u, gsc, gsh, a_gci[i]);
-      st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], u);
+      st16(&sA[buf][soff(a_lrow[i], a_col[i])], u);
     }
 #pragma unroll
     for (int i = 0; i < W_CH; ++i) {
       const int c = tid + i * NT;
-      if (c < W_TOT) st16(&sW[buf][(c / CPR) * LDR + (c % CPR) * VN], w_zero[i] ? make_uint4(0, 0, 0, 0) : rw[i]);
+      if (c < W_TOT) st16(&sW[buf][soff(c / CPR, (c % CPR) * VN)], w_zero[i] ? make_uint4(0, 0, 0, 0) : rw[i]);
     }
   };
 
@@ -164,10 +173,10 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(ConvP p) {
       const int r = lane & 15, kc = (lane >> 4) * 8;
       s16x8 bfrag[FM];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j + r) * LDR + kc]);
+      for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[soff(wm + 16 * j + r, kc)]);
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
-        s16x8 afrag = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i + r) * LDR + kc]);
+        s16x8 afrag = *reinterpret_cast<const s16x8*>(&Ws[soff(wn + 16 * i + r, kc)]);
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag, bfrag[j], acc[i][j]);
       }

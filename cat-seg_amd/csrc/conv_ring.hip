@@ -30,10 +30,11 @@
 #include "common.h"
 #include "capi.h"
 
+#define DEV_HOST_CONST __host__ __device__ constexpr
+
 namespace {
 
 constexpr int NT = 256;          // 4 waves
-int g_ring_variant = 0;          // A/B tiling / band knobs (catseg_set_ring_variant; 0 = default)
 int g_ring_persist = 2;          // persistent workgroups over (slice, band) units: 2 = >= 4 units each (bands by that), 1 = one-unit band rule, 0 = one unit per workgroup
 
 struct RingP {
@@ -52,6 +53,12 @@ struct RingGeom {
   static_assert(C % 16 == 0, "channels in 16-channel steps");
   static constexpr int PSB = (C * 2) % 64 == 32 ? C * 2 : C * 2 + 32;   // pixel stride, bytes
   static constexpr int PS = PSB / 2;                                     // ... elements
+  // ring row pitch = (W + 2) pixels + RPAD: a 16-pixel fragment that wraps from column W-1 of one
+  // row to column 0 of the next skips the two halo columns; the pad makes that step -2 pixel
+  // strides mod 256 bytes, so the wrapped lanes land on the banks of a contiguous run (W = 24:
+  // 1/3 more LDS cycles per fragment read without it; widths that are multiples of 16 never wrap)
+  static constexpr int RPADB = (256 - (2 * PSB) % 256) % 256;
+  static DEV_HOST_CONST int pitch(int W) { return (W + 2) * PS + RPADB / 2; }   // elements
 };
 
 
@@ -79,7 +86,8 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* ring = reinterpret_cast<bf16*>(smem);
   const int W = WFIX > 0 ? WFIX : p.W, WP = W + 2, H = p.H;
-  const int ring_elems = NR * WP * PS;
+  const int RPE = RingGeom<C>::pitch(W);                  // ring row pitch, elements
+  const int ring_elems = NR * RPE;
   float* gsc = reinterpret_cast<float*>(smem + (size_t)ring_elems * 2);   // [C]
   float* gsh = gsc + C;                                                    // [C]
 
@@ -165,10 +173,14 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) e[k] = f2bf(fmaxf(fmaf(bf2f(e[k]), gsc[ci + k], gsh[ci + k]), 0.f));
     }
-    const int pos = ((y + 1) % NR) * WP + xc;
-    st16(&ring[pos * PS + ch * 8], u);
+    st16(&ring[((y + 1) % NR) * RPE + xc * PS + ch * 8], u);
   };
   const int row_items = WP * CPX;
+  // ring-write item order: with 4 chunks per pixel (C = 32, 96-byte pixel stride) the 8 lanes of a
+  // ds_write_b128 group would write pixels p, p+1 and hit 8 banks twice; swapping bits 2 and 3 of
+  // the item index gives them pixels p, p+2 (distinct 16-byte bank slots), a bijection on every
+  // aligned block of 16 items (validity is tested on the permuted index)
+  auto perm = [](int i) { return CPX == 4 ? (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1) : i; };
 
   // ---- prime: rows needed by the first chunk ----
   __syncthreads();   // gsc/gsh
@@ -181,12 +193,12 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
       uint4 u[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = i0 + j * NT + tid;
+        const int i = perm(i0 + j * NT + tid);
         u[j] = i < total ? gload(ya + i / row_items, (i % row_items) / CPX, i % CPX) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = i0 + j * NT + tid;
+        const int i = perm(i0 + j * NT + tid);
         if (i < total) lput(ya + i / row_items, (i % row_items) / CPX, i % CPX, u[j]);
       }
     }
@@ -196,7 +208,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   int pf_code[MAXPF];
 #pragma unroll
   for (int k = 0; k < MAXPF; ++k) {
-    const int i = tid + k * NT;
+    const int i = perm(tid + k * NT);
     pf_code[k] = ((i / row_items) << 16) | (((i % row_items) / CPX) << 4) | (i % CPX);
   }
   __syncthreads();
@@ -257,7 +269,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
       for (int sy = 0; sy < 2; ++sy)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) rbu[sy][j] = (((prow[j] + pa + sy) % NR) * WP + pcol[j] + pb) * PS;
+        for (int j = 0; j < FM; ++j) rbu[sy][j] = ((prow[j] + pa + sy) % NR) * RPE + (pcol[j] + pb) * PS;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
@@ -277,7 +289,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) rb[dy][j] = (((prow[j] + dy) % NR) * WP + pcol[j]) * PS;
+      for (int j = 0; j < FM; ++j) rb[dy][j] = ((prow[j] + dy) % NR) * RPE + pcol[j] * PS;
 #pragma unroll
     for (int dy = 0; dy < (UP ? 0 : 3); ++dy) {
 #pragma unroll
@@ -392,7 +404,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 }
 
 template <int C>
-size_t ring_lds(int W, int NR) { return (size_t)NR * (W + 2) * RingGeom<C>::PS * 2 + 2 * C * 4; }
+size_t ring_lds(int W, int NR) { return (size_t)NR * RingGeom<C>::pitch(W) * 2 + 2 * C * 4; }
 
 // NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
 // <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
@@ -405,7 +417,7 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   // the measured sweep, tools/micro_ring.py, favours longer bands at W = 96), at least 2
   // workgroups per CU
   const int base = p.W >= 64 ? 6144 : 3072;
-  const int per_band = (g_ring_variant == 3 ? base / 2 : g_ring_variant == 4 ? base * 2 : base) / CH;
+  const int per_band = base / CH;
   int bands = (nchunks + per_band - 1) / per_band;
   const size_t sh = ring_lds<C>(p.W, NR);
   const int nsplit = UP ? p.up_split : 1;
@@ -569,11 +581,11 @@ static int ring_variant(const CatsegConvArgs* a, int* tile) {
   int v = 0, t = 0;
   if (C == 64 && a->c_out == 32) { v = narrow ? 1 : 2; t = 32; }
   else if (C == 48 && a->c_out == 32) {
-    v = narrow ? 3 : (g_ring_variant == 1 ? 4 : 9);
-    t = narrow || g_ring_variant != 1 ? 32 : 64;
+    v = narrow ? 3 : 9;
+    t = 32;
   } else if (C == 32 && a->c_out == 32) {
-    v = narrow ? 5 : (g_ring_variant == 2 ? 10 : 6);
-    t = !narrow && g_ring_variant == 2 ? 64 : 32;
+    v = narrow ? 5 : 6;
+    t = 32;
   }
   else if (C == 64 && a->c_out == 64 && a->W <= 50) { v = 7; t = 128; }
   else if (C == 96 && a->c_out == 64 && a->W <= 50) { v = 8; t = 64; }
@@ -605,13 +617,11 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
     case 1: return launch_ring<64, 32, 4, 1, 156>(p, st);
     case 2: return launch_ring<64, 32, 4, 1, 198, 128, 2, 5>(p, st);
     case 3: return launch_ring<48, 32, 4, 1, 156>(p, st);
-    case 4: return launch_ring<48, 32, 2, 2, 198, 128, 2, 5>(p, st);
     case 5: return launch_ring<32, 32, 4, 1, 156>(p, st);
     case 6: return launch_ring<32, 32, 4, 1, 198, 128, 2, 5>(p, st);
     case 7: return launch_ring<64, 64, 1, 4, 156>(p, st);
     case 8: return launch_ring<96, 64, 1, 4, 104, 64, 2, 5>(p, st);
     case 9: return launch_ring<48, 32, 4, 1, 198, 128, 2, 5>(p, st);
-    case 10: return launch_ring<32, 32, 2, 2, 198, 128, 2, 5>(p, st);
     default: return 1;
   }
 }
@@ -661,7 +671,6 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
   return catseg_launch_status("conv3x3_partial");
 }
 
-CATSEG_KNOB(g_ring_variant, "ring_variant");
 CATSEG_KNOB(g_ring_persist, "ring_persist");
 
 // ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
@@ -728,35 +737,19 @@ extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   p.up_split = 1;
   hipStream_t st = (hipStream_t)stream;
   // 64-pixel chunks (a 48-wide chunk spans <= 3 rows: 5-row ring, <= 2 new rows = 104 positions):
-  // 128-pixel chunks spilled ~100 VGPRs with the addend
-  // tiling variants for A/B (catseg_set_ring_variant 11..14; 0 = default)
+  // 128-pixel chunks spilled ~100 VGPRs with the addend (one 512-register workgroup per CU measured
+  // slower, as did 96-pixel chunks and four 16-channel workgroups per parity for the first block)
   int rc;
-  const int v = g_ring_variant;
   if (up2) {
-    if (v == 11) {       // 128-pixel chunks (<= 4 rows: 6-row ring, <= 3 new rows), one 512-register workgroup per CU
-      if (p.add) rc = launch_ring_t<64, 128, 1, 4, 156, 128, 1, 6, true, true, 48>(p, st);
-      else rc = launch_ring_t<64, 128, 1, 4, 156, 128, 1, 6, false, true, 48>(p, st);
-    } else {
-      if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true, 48>(p, st);
-      else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true, 48>(p, st);
-    }
+    if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true, 48>(p, st);
+    else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true, 48>(p, st);
   } else {
     // first Up block (24-wide source, 128 channels): a parity's 64 outputs x 4 taps x 4 k-steps would
     // be 256 weight VGPRs per wave, so two workgroups split them (32 each, the source ring read by
     // both); a 64-pixel chunk spans <= 4 rows (6-row ring) and adds <= 3 (78 positions)
-    if (v == 13) {       // 96-pixel chunks (4 whole rows at W = 24: 7-row ring, <= 4 new rows = 104 positions)
-      p.up_split = 2;
-      if (p.add) rc = launch_ring_t<128, 128, 1, 4, 104, 96, 1, 7, true, true, 24>(p, st);
-      else rc = launch_ring_t<128, 128, 1, 4, 104, 96, 1, 7, false, true, 24>(p, st);
-    } else if (v == 14) {  // four workgroups of 16 channels per parity, two workgroups per CU
-      p.up_split = 4;
-      if (p.add) rc = launch_ring_t<128, 64, 1, 4, 78, 64, 2, 6, true, true, 24>(p, st);
-      else rc = launch_ring_t<128, 64, 1, 4, 78, 64, 2, 6, false, true, 24>(p, st);
-    } else {
-      p.up_split = 2;
-      if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true, 24>(p, st);
-      else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true, 24>(p, st);
-    }
+    p.up_split = 2;
+    if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true, 24>(p, st);
+    else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true, 24>(p, st);
   }
   if (rc != 0) return rc;
   return catseg_launch_status("upconv3x3");

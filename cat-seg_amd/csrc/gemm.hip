@@ -597,181 +597,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   }
 }
 
-// ------------------------------------------------------------------------------------
-// bf16 256x256 "ping-pong" GEMM for the large ViT projections.
-//
-// 8 waves = 2 groups of 4 (group wr = wave / 4 holds one wave on every SIMD).  Group 1
-// runs one barrier behind group 0, so on every SIMD one wave issues its LDS fragment reads
-// and LDS-DMA while the other runs its MFMAs.  Every phase of a wave is
-//     R: ds_read its operand sub-tile, issue one 16 KB LDS-DMA piece, counted vmcnt,
-//        lgkmcnt(0), barrier
-//     M: 16 x mfma_f32_16x16x32_bf16 (one 64(m) x 32(n) quadrant of the wave's
-//        128 x 64 output, K = 64) at raised priority, barrier
-// and a K-tile is 4 phases over the quadrants (m0,n0) (m0,n1) (m1,n1) (m1,n0), so A and
-// W sub-tiles stay in registers across neighbouring phases.
-//
-// LDS: 2 K-tile buffers x 4 pieces of 128 rows x 64 k (16 KB each, 128 KB total):
-//   piece 0 = A rows of quadrant m0 (both groups), first read in phase 0 only
-//   piece 1 = W rows of n0 (all waves), read in phases 0 and 3
-//   piece 2 = W rows of n1, read in phase 1;  piece 3 = A rows of m1, read in phase 2.
-// Phases 0-3 of tile t issue piece 3, 1 of tile t+1 and pieces 0, 2 of tile t+2: every
-// buffer is rewritten exactly 2 phases after its last fragment read (so the reads, waited
-// for with lgkmcnt(0) at the start of the reader's M slot, are retired a barrier before the
-// DMA is issued), and every piece is issued >= 3 phases before its first read, retired by
-// the issuing wave's vmcnt(4) in the phase before that read and published by that phase's
-// barrier.  Rows >= M re-read row M-1 and are masked at the store.
-// Needs N % 256 == 0 and K % 64 == 0 (host-checked).
-// ------------------------------------------------------------------------------------
-DEV void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
-
-template <typename TO, bool DIAG_NOSTORE = false>
-__global__ __launch_bounds__(512) void gemm8_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
-                                                    const bf16* __restrict__ W, int64_t ldw, int64_t M, int64_t K,
-                                                    int tiles_n, EpiArgs e) {
-  constexpr int BM = 256, BN = 256, BK = 64;
-  constexpr int PIECE = 128 * BK;       // elements per piece
-  constexpr int TILE = 4 * PIECE;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-  const bool ident = amap.d1 == 1 && amap.m1 >= M && amap.s1 == 1 && amap.m2 == 1 && amap.off == 0;
-
-  // LDS-DMA sources: chunk c = g * 512 + tid of a piece -> piece row c / 8, LDS slot c % 8,
-  // holding global 16-byte chunk slot ^ ((row / 2) % 8) (the fragment-read swizzle)
-  const bf16* src[4][2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int c = g * 512 + tid, lrow = c >> 3, ch = (c & 7) ^ ((lrow >> 1) & 7);
-    const int ra0 = lrow < 64 ? lrow : lrow + 64;          // piece 0: A rows 0-63, 128-191
-    const int ra1 = lrow < 64 ? lrow + 64 : lrow + 128;    // piece 3: A rows 64-127, 192-255
-    const int rw0 = (lrow >> 5) * 64 + (lrow & 31);        // piece 1: W rows wc*64 + 0..31
-    int64_t ma = m0 + ra0, mb = m0 + ra1;
-    if (ma >= M) ma = M - 1;
-    if (mb >= M) mb = M - 1;
-    src[0][g] = A + (ident ? ma : rowmap(amap, ma)) * lda + ch * 8;
-    src[3][g] = A + (ident ? mb : rowmap(amap, mb)) * lda + ch * 8;
-    src[1][g] = W + (n0 + rw0) * ldw + ch * 8;
-    src[2][g] = W + (n0 + rw0 + 32) * ldw + ch * 8;
-  }
-  const int ktiles = (int)(K / BK);
-  auto issue = [&](int piece, int t) {
-    bf16* dst = smem + (t & 1) * TILE + piece * PIECE + wave * 64 * 8;
-    const int64_t k0 = (int64_t)t * BK;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[piece][0] + k0), (lds_void_t*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[piece][1] + k0), (lds_void_t*)(dst + 512 * 8), 16, 0, 0);
-  };
-
-  f32x4 acc[4][8];     // [n frag: nq*2 + fn][m frag: mq*4 + fm]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int r = lane & 15, q = lane >> 4;
-  // fragment read: piece row lrow, k half kh -> 16-byte chunk kh*4 + q (swizzled)
-  auto frag = [&](const bf16* buf, int piece, int lrow, int kh) -> s16x8 {
-    const int ch = (kh * 4 + q) ^ ((lrow >> 1) & 7);
-    return *reinterpret_cast<const s16x8*>(buf + piece * PIECE + (lrow * 8 + ch) * 8);
-  };
-  s16x8 fa[4][2], fb[2][2];
-  auto read_a = [&](const bf16* buf, int mq) {
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) fa[fm][kh] = frag(buf, mq ? 3 : 0, wr * 64 + fm * 16 + r, kh);
-  };
-  auto read_b = [&](const bf16* buf, int nq) {
-#pragma unroll
-    for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) fb[fn][kh] = frag(buf, nq ? 2 : 1, wc * 32 + fn * 16 + r, kh);
-  };
-
-  // prologue: tile 0 (4 pieces) and pieces 0, 2 of tile 1; retire pieces 0, 1 of tile 0
-  issue(0, 0); issue(1, 0); issue(2, 0); issue(3, 0);
-  if (ktiles > 1) { issue(0, 1); issue(2, 1); wait_vmcnt<8>(); }
-  else wait_vmcnt<4>();
-  __syncthreads();
-  if (wr == 1) __builtin_amdgcn_s_barrier();      // group 1 runs one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int t = 0; t < ktiles; ++t) {
-    const bf16* buf = smem + (t & 1) * TILE;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      // ---- R slot ----
-      if (p == 0) { read_a(buf, 0); read_b(buf, 0); }
-      else if (p == 1) read_b(buf, 1);
-      else if (p == 2) read_a(buf, 1);
-      else read_b(buf, 0);
-      // p0: piece 3 of t+1, p1: piece 1 of t+1, p2: piece 0 of t+2, p3: piece 2 of t+2
-      const int tn = p < 2 ? t + 1 : t + 2;
-      if (tn < ktiles) {
-        issue(p == 0 ? 3 : p == 1 ? 1 : p == 2 ? 0 : 2, tn);
-        wait_vmcnt<4>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- M slot: quadrant (mq, nq); the fragment reads land while the partner group issues ----
-      const int mq = p < 2 ? 0 : 1, nq = (p == 1 || p == 2) ? 1 : 0;
-      wait_lgkm0();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-          for (int fm = 0; fm < 4; ++fm)
-            acc[nq * 2 + fn][mq * 4 + fm] = mfma_bf16(fb[fn][kh], fa[fm][kh], acc[nq * 2 + fn][mq * 4 + fm]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();      // match group 1's barrier count
-  __syncthreads();
-
-  if constexpr (DIAG_NOSTORE) {   // diagnostics: main loop only (keeps the MFMAs live)
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += acc[i][j][0];
-    if (s == 1234.5f) reinterpret_cast<float*>(e.out)[tid] = s;
-    return;
-  }
-  // ---- epilogue through LDS: 4 rounds of 64 tile rows (one (group, m quadrant) each) ----
-  constexpr int SLD = BN + 4;
-  float* stg = reinterpret_cast<float*>(smem);
-  const int rq = q * 4;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const int hw = h >> 1, hm = h & 1;
-    if (wr == hw) {
-#pragma unroll
-      for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          *reinterpret_cast<f32x4*>(&stg[(fm * 16 + r) * SLD + wc * 64 + (i >> 1) * 32 + (i & 1) * 16 + rq]) =
-              acc[i][hm * 4 + fm];
-    }
-    __syncthreads();
-    for (int idx = tid; idx < 64 * (BN / 8); idx += 512) {
-      const int lrow = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
-      const int64_t m = m0 + hw * 128 + hm * 64 + lrow;
-      if (m < M)
-        epilogue8<TO>(e, m, n0 + c8, *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]),
-                      *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]));
-    }
-    __syncthreads();
-  }
-}
-
 int g_gemm_group = 4;   // gemm3 tile order: 0 = row-major, G > 0 = G m-tiles per group (catseg_set_gemm_group); 4 measured best (fc2 48.6 -> 47.4 us)
 
 EpiArgs make_epi(const CatsegGemmArgs* g) {
@@ -813,18 +638,7 @@ bool launch3f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
   return true;
 }
 
-template <typename TO, bool DIAG_NOSTORE = false>
-bool launch8(const CatsegGemmArgs* g, hipStream_t st) {
-  if (g->N % 256 != 0 || g->K % 64 != 0) return false;
-  const EpiArgs e = make_epi(g);
-  RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
-  const int tm = (int)((g->M + 255) / 256), tn = (int)(g->N / 256);
-  hipLaunchKernelGGL((gemm8_kernel<TO, DIAG_NOSTORE>), dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A, g->lda, am,
-                     (const bf16*)g->W, g->ldw, g->M, g->K, tn, e);
-  return true;
-}
-
-int g_gemm_variant = 0;   // 0 = automatic; >0 forces a gemm3 tile (tests / tuning)
+int g_gemm_variant = 0;   // 0 = automatic; >0 forces one of the automatic gemm3 tiles (tests / tuning)
 
 // returns true when a gemm3 variant was launched
 template <typename TO>
@@ -884,28 +698,14 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 2 && v == 19) return launch3<TO, 128, 128, 2, 4, 2, 64, false, 2>(g, st);
   if (epi == 1 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 1>(g, st);
   if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
+  // forced tiles (gemm_variant, tests / tools/micro_gemm.py): the automatic candidates only
   switch (v) {
     case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
-    case 2: return launch3<TO, 256, 256, 2, 4, 4, 32>(g, st);
-    case 3: return launch3<TO, 256, 256, 2, 4, 3, 32>(g, st);
-    case 4: return launch3<TO, 128, 128, 2, 2, 4, 32>(g, st);
-    case 5: return launch3<TO, 128, 128, 2, 2, 2, 64>(g, st);
-    case 6: return launch3<TO, 256, 128, 4, 2, 3, 64>(g, st);
-    case 7: return launch3<TO, 128, 256, 2, 4, 4, 32>(g, st);
-    case 8: return launch3<TO, 256, 128, 4, 2, 4, 32>(g, st);
-    case 9: return launch8<TO>(g, st);
-    case 10: return launch8<TO, true>(g, st);      // diagnostics only (no output)
-    case 11: return launch3<TO, 160, 128, 2, 2, 2, 64>(g, st);
     case 15: return launch3<TO, 160, 128, 2, 4, 2, 128>(g, st);
     case 17: return launch3<TO, 160, 128, 2, 4, 2, 64>(g, st);
-    case 18: return launch3<TO, 160, 256, 2, 4, 2, 64>(g, st);
     case 19: return launch3<TO, 128, 128, 2, 4, 2, 64>(g, st);
     case 20: return launch3<TO, 224, 256, 2, 4, 2, 64>(g, st);
-    case 21: return launch3<TO, 160, 128, 2, 4, 3, 64>(g, st);
-    case 22: return launch3<TO, 160, 128, 2, 4, 4, 64>(g, st);
-    case 23: return launch3<TO, 224, 256, 2, 4, 4, 32>(g, st);
     case 24: return launch3<TO, 96, 128, 2, 4, 2, 128>(g, st);
-    case 25: return launch3<TO, 96, 128, 2, 4, 2, 64>(g, st);
     default: return false;
   }
 }

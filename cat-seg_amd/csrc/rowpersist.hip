@@ -771,17 +771,14 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
   return catseg_launch_status("convt64_gn");
 }
 
-int g_mlp_pair = 1;   // persistent MLP hidden-unit order: 1 = paired 16-byte hidden stores (default), 0 = 8-byte
-CATSEG_KNOB(g_mlp_pair, "mlp_pair");
 int g_mlp_variant = 0;   // 0 = barrier-lean pmlp2_kernel (default), 1 = pmlp_kernel (A/B; bit-identical)
 CATSEG_KNOB(g_mlp_variant, "mlp_variant");
 
-template <bool PAIR>
 int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
                         const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e, bool res2,
                         hipStream_t st) {
   const dim3 grid(persist_grid(M)), blk(NT);
-  if (PAIR && g_mlp_variant == 0) {
+  if (g_mlp_variant == 0) {
     if (act == ACT_GELU && !res2)
       hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
     else if (act == ACT_RELU && res2)
@@ -794,13 +791,13 @@ int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g,
     return 0;
   }
   if (act == ACT_GELU && !res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, false, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
   else if (act == ACT_RELU && res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, true, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, true, false, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
   else if (act == ACT_RELU && !res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, false, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    hipLaunchKernelGGL((pmlp_kernel<ACT_RELU, false, false, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
   else if (act == ACT_GELU && res2)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, true, false, PAIR>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, true, false, true>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
   else return 1;
   return 0;
 }
@@ -812,10 +809,7 @@ int catseg_rows_mlp_persistent(const void* y, int64_t ld_y, int64_t M, const flo
   if (hidden != HID || !epi->bias || epi->res != y || epi->ld_res != ld_y || epi->add || epi->store_mode) return 1;
   const PEpi e = make_pepi(epi);
   const bool r2 = epi->res2 != nullptr;
-  return g_mlp_pair ? rows_mlp_persistent<true>((const bf16*)y, ld_y, M, g, b, eps, (const bf16*)w1, b1, act,
-                                                (const bf16*)w2, e, r2, st)
-                    : rows_mlp_persistent<false>((const bf16*)y, ld_y, M, g, b, eps, (const bf16*)w1, b1, act,
-                                                 (const bf16*)w2, e, r2, st);
+  return rows_mlp_persistent((const bf16*)y, ld_y, M, g, b, eps, (const bf16*)w1, b1, act, (const bf16*)w2, e, r2, st);
 }
 
 extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const void* x, int64_t ld_x, int64_t M,
@@ -831,16 +825,12 @@ extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const voi
   CATSEG_CHECK(out == x ? ld_out == ld_x : true, "swin_proj_mlp: in place needs ld_out == ld_x");
   PEpi e{};
   e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
-  if (g_mlp_pair && g_mlp_variant == 0)
+  if (g_mlp_variant == 0)
     hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
                        (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
-  else if (g_mlp_pair)
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
-                       (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
-                       (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
   else
-    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, false>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((pmlp_kernel<ACT_GELU, false, true, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
                        (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
   return catseg_launch_status("swin_proj_mlp");

@@ -12,7 +12,7 @@
 // attention needs (108 VGPRs), so no K / V image goes through LDS and there is no barrier between
 // projection and attention; the two workgroups of a CU interleave their MFMA and softmax phases.
 //
-// swin_win3 (swin_variant 3 / 1 / 16): one 8-wave workgroup per CU, waves w and w + 4 share head
+// swin_win3 (swin_variant 3; other guidance row maps): one 8-wave workgroup per CU, waves w and w + 4 share head
 // w % 4 (every SIMD does one head), K and V^T of each head staged in LDS:
 //   P1  LayerNorm(norm1) of the 144 rows in place in Xn (bf16, chunk-major XOR-swizzled), 16
 //       lanes per row.  The raw rows were brought in by LDS-DMA during the previous window's P3.
@@ -91,10 +91,7 @@ DEV void dma16_opaque(const void* src, unsigned lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
 }
 
-// STAMP (diagnostics, swin_variant 16): wave-lane-0 s_memtime stamps at the phase boundaries of the
-// first 4 windows of every wave, written PAST the last output row (the caller allocates
-// grid x 8 x 32 x 8 bytes more: tools/stamps_swin.py)
-template <bool SWM, bool ASMDMA, bool STAMP = false>
+template <bool SWM>
 __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 Ks[NH][4 * L * 8];       // [head][chunk][key] (chunk-major)
@@ -142,11 +139,7 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
     for (int k = wave; k < NDMA; k += NW) {
       const int sl = k * 64 + lane, c = sl / L, i = (sl % L) ^ (c & 15);
       const bf16* src = p.x + (int64_t)win_row3(slice, wloc, i, p.shift) * p.ld_x + c * 8;
-      if constexpr (ASMDMA)
-        dma16_opaque(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xn + k * 64 * 8)));
-      else
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(Xn + k * 64 * 8), 16, 0, 0);
+      dma16_opaque(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xn + k * 64 * 8)));
     }
   };
   int win = blockIdx.x;
@@ -154,22 +147,13 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
   // the first window's rows: retired here, outside the window loop, so that the counted wait at
   // the loop top is only ever reached from the previous window's P3 (tools/isa_lint.py R3)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint64_t* stp = reinterpret_cast<uint64_t*>(p.out + (int64_t)(nwin_total / NWIN) * IMG * IMG * p.ld_out) +
-                  ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * 32;
-  int it = 0;
-  auto stamp = [&](int k) {
-    if (STAMP && (threadIdx.x & 63) == 0 && it < 4) stp[it * 8 + k] = __builtin_amdgcn_s_memtime();
-  };
-  for (; win < nwin_total; win += gridDim.x, ++it) {
+  for (; win < nwin_total; win += gridDim.x) {
     const int slice = win / NWIN, wloc = win % NWIN;
-    stamp(0);
     // this wave's DMA of the window landed: only the previous window's P3 stores (2 per row tile,
     // >= 8 per wave) were issued behind it, and those may stay in flight (the first window's DMA
     // was retired before the loop)
-    if (!ASMDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();                                       // every wave's DMA visible; P3 done
-    stamp(1);
     // guidance row of token rb + r16 of this window: rowmap(slice*576) + pixel when the host
     // found the map linear in the pixel (CAT-Seg's (b, t, p) -> (b, p)), else the general map
     const int64_t gbase = p.glin ? rowmap(p.gmap, (int64_t)slice * (IMG * IMG)) : 0;
@@ -212,9 +196,7 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
           st16(&Xn[cs<L>(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
       }
     }
-    stamp(2);
     __syncthreads();
-    stamp(3);
     // ---------------- P2: q / k / v of head h for row tiles sub, sub + 2, ... ----------------
     if constexpr (SWM) {   // region one-hot of the keys (P3 of the previous window has retired its reads)
       if (gridDim.x % NWIN != 0 || win == (int)blockIdx.x) {
@@ -277,9 +259,7 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
       }
       __builtin_amdgcn_sched_barrier(0);        // no cross-tile hoisting (register pressure)
     }
-    stamp(4);
     __syncthreads();
-    stamp(5);
     // ---------------- P3: attention of head h for the same row tiles ----------------
     if (win + (int)gridDim.x < nwin_total) fetch(win + gridDim.x);   // Xn is free: P2 is done everywhere
     const bool masked = SWM && wloc != 0;       // window location 0 holds a single region
@@ -337,7 +317,6 @@ __global__ __launch_bounds__(NT) void swin_win3_kernel(Swin3P p, int nwin_total)
             make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
       __builtin_amdgcn_sched_barrier(0);
     }
-    stamp(6);
   }
 }
 
@@ -601,7 +580,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
 }  // namespace
 
 // launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
-int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool asm_dma, bool glin, bool stamps) {
+int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool glin) {
   Swin3P p;
   p.glin = glin ? 1 : 0;
   p.x = (const bf16*)a->x; p.ld_x = a->ld_x;
@@ -613,16 +592,8 @@ int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   p.shift = a->shift; p.scale = a->scale;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
-  if (stamps) {
-    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, true, true>), grid, dim3(NT), 0, st, p, nwin_total);
-    else hipLaunchKernelGGL((swin_win3_kernel<false, true, true>), grid, dim3(NT), 0, st, p, nwin_total);
-  } else if (asm_dma) {
-    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, true>), grid, dim3(NT), 0, st, p, nwin_total);
-    else hipLaunchKernelGGL((swin_win3_kernel<false, true>), grid, dim3(NT), 0, st, p, nwin_total);
-  } else {
-    if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true, false>), grid, dim3(NT), 0, st, p, nwin_total);
-    else hipLaunchKernelGGL((swin_win3_kernel<false, false>), grid, dim3(NT), 0, st, p, nwin_total);
-  }
+  if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true>), grid, dim3(NT), 0, st, p, nwin_total);
+  else hipLaunchKernelGGL((swin_win3_kernel<false>), grid, dim3(NT), 0, st, p, nwin_total);
   return 0;
 }
 

@@ -167,6 +167,10 @@ int catseg_l2normalize(const void* in, int64_t ld_in, CatsegRowMap inmap, int dt
  *   mode 1 (Swin windows): WindowAttention of model.py:86-114 with the cyclic
  *     shift and -100 region mask of model.py:161-216.  Sequence s = (slice,
  *     window); token i maps to pixel ((wy*ws + i/ws + shift) % H, ...) of slice.
+ *   mode 2 (dense, log2-scaled q): as mode 0 with the q rows already multiplied
+ *     by scale * log2(e) (the engine folds it into the ViT q projection), so
+ *     softmax(scale q.k) = 2^(q.k - max) / sum; `scale` is not read.  bf16,
+ *     head_dim 64, non-causal only.
  *   q/k/v: row pointers (columns of one head at + h*head_dim), row stride ld_qkv.
  *   out:   row stride ld_out, head h at columns h*head_dim.
  * ------------------------------------------------------------------------- */

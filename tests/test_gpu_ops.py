@@ -108,7 +108,7 @@ def test_gemm_convtranspose_store_pipelined(cout, k):
     close(got, ref, atol=2e-2, rtol=1e-2, what=f"convT pipelined cout {cout} k {k}")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 17, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [1, 15, 17, 19, 20, 24])
 def test_gemm_pipelined_variants(variant):
     """Every LDS-DMA pipelined bf16 tile (gemm.hip gemm3_kernel) against fp64: ragged M
     (sliver tile), a CLS-dropping row map, bias + QuickGELU + fp32 residual epilogue."""
@@ -309,9 +309,39 @@ def test_attention_dense(dt, L_, H, causal):
     close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("nw", [8, 10])
+@pytest.mark.parametrize("L_,spike", [(577, None), (50, None), (129, None), (577, 300), (577, 5)])
+def test_attention_dense_log2_scaled_q(nw, L_, spike):
+    """Mode 2 (the ViT blocks: q rows carry scale * log2(e), folded into the q projection; the
+    running max enters the S MFMA as its accumulator): vs fp64 softmax attention of the unscaled q,
+    including a spike key that forces the defer-max rescale in block 0 / a middle block."""
+    B, H, d = 2, 4, 64
+    qkv = rnd(B * L_, 3 * H * d, seed=31) * 2
+    if spike is not None:
+        qkv[spike, H * d:H * d + d] += 4 * qkv[200, :d]
+    c = d ** -0.5 * 1.4426950408889634
+    q = qkv.clone()
+    q[:, :H * d] *= c
+    qb = q.to(dev, torch.bfloat16)
+    out = torch.empty(B * L_, H * d, device=dev, dtype=torch.bfloat16)
+    try:
+        L.tune("attn_l2s_nw", nw)
+        ops.attention(qb[:, :H * d], qb[:, H * d:2 * H * d], qb[:, 2 * H * d:], out, n_seq=B, seq_len=L_,
+                      n_heads=H, head_dim=d, scale=0.0, mode=2)
+    finally:
+        L.tune("attn_l2s_nw", 8)
+    x = q.to(torch.bfloat16).double().reshape(B, L_, 3, H, d).permute(2, 0, 3, 1, 4)
+    s = (x[0] @ x[1].transpose(-1, -2)) * math.log(2.0)
+    ref = (torch.softmax(s, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B * L_, H * d)
+    close(out, ref, atol=1.5e-2, what=f"attn mode 2 nw={nw} L={L_} spike={spike}")
+    with pytest.raises(RuntimeError):     # fp32 / causal are not mode-2 shapes
+        ops.attention(qb[:, :H * d].float(), qb[:, H * d:2 * H * d].float(), qb[:, 2 * H * d:].float(),
+                      out.float(), n_seq=B, seq_len=L_, n_heads=H, head_dim=d, scale=0.0, mode=2)
+
+
+@pytest.mark.parametrize("variant", [7])
 def test_attention_dense_tilings(variant):
-    """Every A/B tiling of the dense path (tuning knob attn_variant) == the default tiling."""
+    """The generic tiling of the dense path (tuning knob attn_variant 7) == the default ViT kernel."""
     B, L_, H, d = 2, 577, 4, 64
     q = (rnd(B * L_, 3 * H * d, seed=19) * 2).to(dev, torch.bfloat16)
     args = (q[:, :H * d], q[:, H * d:2 * H * d], q[:, 2 * H * d:])
@@ -455,16 +485,11 @@ def test_class_attention_fused(T, n_pad, per_image):
                          head_dim=32, n_pad=n_pad, k_pad=kp, v_pad=vp)
     e2 = (y.float() - y2.float()).abs()
     assert e2.max().item() < 5e-2 and e2.mean().item() < 5e-3, (e2.max().item(), e2.mean().item())
-    # the bias-in-registers form (classattn_variant 3) computes the same bits as the default
-    lib = L.load()
+    # a second launch computes the same bits (no atomics, fixed reduction order)
     y3 = torch.empty_like(X)
-    try:
-        L.tune("classattn_variant", 3)
-        ops.class_attention(X, (g1, b1), W, bias, tg, y3, B=B, T=T, HW=HW, n_heads=4, head_dim=32,
-                            tg_bstride=T if per_image else 0, n_pad=n_pad, k_pad=kp, v_pad=vp)
-        torch.cuda.synchronize()
-    finally:
-        L.tune("classattn_variant", 0)
+    ops.class_attention(X, (g1, b1), W, bias, tg, y3, B=B, T=T, HW=HW, n_heads=4, head_dim=32,
+                        tg_bstride=T if per_image else 0, n_pad=n_pad, k_pad=kp, v_pad=vp)
+    torch.cuda.synchronize()
     assert torch.equal(y, y3)
 
 
@@ -928,14 +953,14 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
     close(out, ref, atol=1e-6, what="resize")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("shift", [0, 6, 3])
 def test_swin_window_attention_fused_vs_unfused(shift, variant):
     """catseg_swin_window_attention == catseg_rows_gemm(LN1 + q/k/v + guidance) followed by
     catseg_attention mode 1 (model.py:191-199, 86-114), bf16, on the 24x24 / 12x12 geometry.
     variant 0 = the register-resident kernel (default, swin_window.hip swin_win5: two 4-wave
-    workgroups per CU), 1 = the head-per-SIMD kernel with the builtin LDS-DMA and a row map per tile,
-    2 = the row-tile-wave kernel, 3 = the head-per-SIMD kernel with the opaque LDS-DMA; S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
+    workgroups per CU), 3 = the head-per-SIMD kernel (swin_win3, the fallback for other guidance row
+    maps); S = 7 slices = 28 windows over the persistent grid (window location varies per workgroup)."""
     B, T, HW, D = 1, 7, 576, 128
     S = B * T
     R = S * HW
@@ -989,13 +1014,12 @@ def test_swin_window_attention_fused_vs_unfused(shift, variant):
 @pytest.mark.parametrize("shift", [0, 6])
 def test_swin_window_attention_persistent_variants_agree(shift, glin):
     """Persistent grid over several windows per workgroup (S = 200 slices = 800 windows > the
-    grid, guidance map of 2 images): the head-per-SIMD opaque-DMA kernel (variant 3, whose counted
-    window-start wait lets the previous window's stores stay in flight, guidance rows from a per-window
-    base) equals the builtin-DMA / per-tile row-map kernel (variant 1) bit for bit, and so does the
-    register-resident default (variant 0, swin_win5: same LayerNorm, projection, mask and softmax
-    arithmetic).  glin=False stores the guidance pixel-major
-    (row = pixel * B + image), which no slice maps to one base + pixel: variants 3 and 0 then run
-    swin_win3's per-tile row-map path."""
+    grid, guidance map of 2 images): the register-resident default (variant 0, swin_win5) equals the
+    head-per-SIMD kernel (variant 3, swin_win3: same LayerNorm, projection, mask and softmax
+    arithmetic) bit for bit; both retire the window's opaque LDS-DMA with a counted window-start wait
+    that lets the previous window's stores stay in flight.  glin=False stores the guidance pixel-major
+    (row = pixel * B + image), which no slice maps to one base + pixel: both then run swin_win3's
+    per-tile row-map path."""
     B, T, HW, D = 2, 100, 576, 128
     S = B * T
     R = S * HW
@@ -1008,7 +1032,7 @@ def test_swin_window_attention_persistent_variants_agree(shift, glin):
     gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1) if glin else rowmap(d1=T * HW, s1=1, d2=1, m2=HW, s2=B)
     outs = []
     try:
-        for variant in (1, 3, 0):
+        for variant in (3, 0):
             L.tune("swin_variant", variant)
             o = torch.full((R, D), float("nan"), device=dev, dtype=dt)
             ops.swin_window_attention(X, (g1, b1), W, bias, gqk, gmap, o, S=S, img_hw=(24, 24), window=12,
@@ -1018,8 +1042,7 @@ def test_swin_window_attention_persistent_variants_agree(shift, glin):
     finally:
         L.tune("swin_variant", 0)
     assert torch.isfinite(outs[0]).all()
-    assert torch.equal(outs[1], outs[0])
-    assert torch.equal(outs[2], outs[0]), (outs[2] - outs[0]).abs().max().item()
+    assert torch.equal(outs[1], outs[0]), (outs[1] - outs[0]).abs().max().item()
 
 
 def test_swin_window_attention_repeat_launches_bit_identical():
@@ -1132,37 +1155,6 @@ def test_swin_proj_mlp_equals_separate_kernels():
     h = F.gelu(F.layer_norm(x1, (C,), g.double().cpu(), b.double().cpu(), 1e-5) @ w1.double().cpu().T + b1.double().cpu())
     y = x1 + h @ w2.double().cpu().T + b2.double().cpu()
     close(got, y, atol=0.08, rtol=0.02, what="swin proj+mlp vs fp64")
-
-
-@pytest.mark.parametrize("act", [L.ACT_GELU, L.ACT_RELU])
-def test_mlp_pair_order_bit_identical(act):
-    """The persistent MLP's paired hidden-unit order (tuning knob mlp_pair 1, the default: 16-byte
-    hidden-tile stores) equals the 8-byte-store order (0) bit for bit, for the Swin MLP (GELU),
-    the class MLP (ReLU, + res2) and the fused Swin proj + MLP, on ragged M."""
-    lib = L.load()
-    M, C, Hd = 2 * 577 + 9, 128, 512
-    dt = torch.bfloat16
-    y = (rnd(M, C, seed=120) * 2).to(dev, dt)
-    x = rnd(M, C, seed=121).to(dev, dt)
-    g, b = (1 + rnd(C, seed=122) * 0.2).to(dev), (rnd(C, seed=123) * 0.1).to(dev)
-    w1, b1 = (rnd(Hd, C, seed=124) / 11).to(dev, dt), rnd(Hd, seed=125).to(dev)
-    w2, b2 = (rnd(C, Hd, seed=126) / 22).to(dev, dt), rnd(C, seed=127).to(dev)
-    wp, bp = (rnd(C, C, seed=128) / 11).to(dev, dt), rnd(C, seed=129).to(dev)
-    outs = {}
-    try:
-        for pair in (1, 0):
-            L.tune("mlp_pair", pair)
-            o1 = torch.empty_like(y)
-            ops.rows_mlp(y, w1, b1, w2, o1, ln=(g, b), b2=b2, act=act, res=y,
-                         res2=x if act == L.ACT_RELU else None)
-            o2 = x.clone()
-            ops.swin_proj_mlp(y, o2, wp, bp, w1, b1, w2, b2, o2, ln=(g, b))
-            torch.cuda.synchronize()
-            outs[pair] = (o1, o2)
-    finally:
-        L.tune("mlp_pair", 1)
-    assert torch.equal(outs[1][0], outs[0][0]), (outs[1][0].float() - outs[0][0].float()).abs().max().item()
-    assert torch.equal(outs[1][1], outs[0][1]), (outs[1][1].float() - outs[0][1].float()).abs().max().item()
 
 
 @pytest.mark.parametrize("H,W", [(96, 96), (50, 96), (50, 37)])

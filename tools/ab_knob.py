@@ -1,7 +1,7 @@
 """Same-process A/B of a tuning knob (catseg_tuning_set) on the headline step (L/14@336, T=150, bs=8, bf16):
 one engine, one hipGraph per knob value (the value is read at launch, so at capture), rounds
 interleaved; prints ms/step per value and whether the logits equal the first value's bit for bit.
-usage: python tools/ab_knob.py mlp_pair 0 1 [--steps N]"""
+usage: python tools/ab_knob.py mlp_variant 0 1 [--steps N]"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]

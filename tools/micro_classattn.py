@@ -24,7 +24,7 @@ def main():
         tg = (0.5 * torch.randn(T, 2 * D, device=dev)).to(torch.bfloat16)
         kp, vp = torch.randn(D, device=dev), torch.randn(D, device=dev)
         ys = {}
-        variants = [int(v) for v in os.environ.get("CA_VARIANTS", "0,1").split(",")] + \
+        variants = [int(v) for v in os.environ.get("CA_VARIANTS", "0").split(",")] + \
             [int(v) for v in os.environ.get("CA_DBG", "").split(",") if v]
         times = {v: [] for v in variants}
         for rnd in range(7):

@@ -1,6 +1,6 @@
 """Time the fused Swin window kernel variants (tuning knob swin_variant) at config 3 (S = 1200 slices,
 24x24, 12x12 windows, 4 heads x 32) for shift 0 and 6, and compare their outputs.
-usage: python tools/micro_swin.py [variants, default 0,1]"""
+usage: python tools/micro_swin.py [variants, default 0,3]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
@@ -9,7 +9,7 @@ from cat_seg import ops
 from cat_seg import _lib as L
 from cat_seg._lib import rowmap
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,3").split(",")]
 lib = L.load()
 B, T, HW, D = 8, 150, 576, 128
 S, R = B * T, B * T * HW

@@ -24,7 +24,7 @@
     }                                                                                 \
   } while (0)
 
-constexpr int NB = 2048, NT = 512, ITERS = 32, NW = 24, NV = 14;
+constexpr int NB = 2048, NT = 512, ITERS = 32, NW = 24, NV = 18;
 
 #define PAD "s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n"
 // operand words -> v[64:87]: A16 v[64:65], B16 v[66:67], C v[68:71], A32 v[72:75], B32 v[76:79],
@@ -189,6 +189,46 @@ __device__ __forceinline__ void body(const uint32_t (&w)[NW], float (&o)[16], ui
           "v_mov_b32 v132, v90\n v_mov_b32 v133, v91\n v_mov_b32 v134, v92\n v_mov_b32 v135, v93\n"
           "v_mov_b32 v136, v82\n v_mov_b32 v137, v83\n v_mov_b32 v138, v84\n v_mov_b32 v139, v85\n");
     }
+  } else if constexpr (V >= 14) {
+    // the wrong Swin build's pattern (ffe1710, swin_win5<true,true>): MFMA B reads as srcC the
+    // result of MFMA A issued two instructions earlier (so B waits in the matrix pipe for A), and
+    // an LDS load into those srcC registers is issued 5 wait states after B.  V 14 / 15: B is
+    // K=16 / K=32; V 16 / 17: the same with A's result made ready first (padded), B then issues
+    // with no pending dependency.  P = A32b.B32 (16x16x32, C=0); B = A16.B16 + P (or A32.B32 + P)
+    if constexpr (REF) {
+      if constexpr (V == 14 || V == 16)
+        RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n" PAD
+            "v_mfma_f32_16x16x16_bf16 v[96:99], v[64:65], v[66:67], v[100:103]\n" PAD TO_R);
+      else
+        RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n" PAD
+            "v_mfma_f32_16x16x32_bf16 v[96:99], v[72:75], v[76:79], v[100:103]\n" PAD TO_R);
+    } else if constexpr (V == 14) {
+      RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n"
+          "s_nop 0\n"
+          "v_mfma_f32_16x16x16_bf16 v[96:99], v[64:65], v[66:67], v[100:103]\n"
+          "s_nop 4\n"
+          "ds_read_b128 v[100:103], %[lds]\n"
+          "s_waitcnt lgkmcnt(0)\n" PAD TO_R);
+    } else if constexpr (V == 15) {
+      RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n"
+          "s_nop 0\n"
+          "v_mfma_f32_16x16x32_bf16 v[96:99], v[72:75], v[76:79], v[100:103]\n"
+          "s_nop 4\n"
+          "ds_read_b128 v[100:103], %[lds]\n"
+          "s_waitcnt lgkmcnt(0)\n" PAD TO_R);
+    } else if constexpr (V == 16) {
+      RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n" PAD
+          "v_mfma_f32_16x16x16_bf16 v[96:99], v[64:65], v[66:67], v[100:103]\n"
+          "s_nop 4\n"
+          "ds_read_b128 v[100:103], %[lds]\n"
+          "s_waitcnt lgkmcnt(0)\n" PAD TO_R);
+    } else {
+      RUN("v_mfma_f32_16x16x32_bf16 v[100:103], v[80:83], v[76:79], 0\n" PAD
+          "v_mfma_f32_16x16x32_bf16 v[96:99], v[72:75], v[76:79], v[100:103]\n"
+          "s_nop 4\n"
+          "ds_read_b128 v[100:103], %[lds]\n"
+          "s_waitcnt lgkmcnt(0)\n" PAD TO_R);
+    }
   } else {
     // an LDS load landing in the srcC registers of a just-issued MFMA, 5 wait states later (the
     // padding hipcc gave the wrong Swin build): V 12 K=16, V 13 K=32.  The LDS words are 1e9f.
@@ -276,7 +316,9 @@ int main() {
   const char* names[NV] = {"k16 dst/srcA hi", "k16 dst/srcA lo", "k16 dst/srcB", "k16 dst/srcC up",
                            "k16 dst/srcC down", "k32 dst/srcA", "k32 dst/srcB up", "k32 dst/srcB down",
                            "k32 dst/srcC up", "k32 dst/srcC down", "swin K=16 sequence",
-                           "swin sequence on K=32", "k16 LDS->srcC after 5 ws", "k32 LDS->srcC after 5 ws"};
+                           "swin sequence on K=32", "k16 LDS->srcC after 5 ws", "k32 LDS->srcC after 5 ws",
+                           "k16 chained srcC + LDS", "k32 chained srcC + LDS", "k16 ready srcC + LDS",
+                           "k32 ready srcC + LDS"};
   for (int hammer = 0; hammer < 2; ++hammer) {
     CHECK(hipMemset(dbad, 0, (2 * NV + 1) * 8));
     launch<0>(din, dbad, hammer);
