@@ -394,7 +394,8 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   for (int dt = 0; dt < 4; ++dt)
     voff[dt] = KB * D * 2 + vrow * 128 + (((2 * dt + ((col & 3) >> 1)) ^ vswz) << 4) + (col & 1) * 8;
 
-  auto block = [&](int blk, auto tail_tag) {
+  // scores + softmax of block blk -> P fragments (bf16) in pb
+  auto scores = [&](int blk, auto tail_tag, s16x8 (&pb)[QT][2]) {
     constexpr bool TAIL = decltype(tail_tag)::value;
     const char* S0 = reinterpret_cast<const char*>(smem + (blk % NBUF) * BLK);
     const int k0 = blk * KB;
@@ -425,7 +426,6 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
           for (int r = 0; r < 4; ++r)
             if (k0 + kt * 16 + 4 * g + r >= L) st[t][kt][r] = -INFINITY;
     }
-    s16x8 pb[QT][2];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       float lm = fmaxf(fmaxf(st[t][0][0], st[t][0][1]), fmaxf(st[t][0][2], st[t][0][3]));
@@ -476,6 +476,12 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
         pb[t][u] = *reinterpret_cast<s16x8*>(&pu);
       }
     }
+  };
+  // O += P V and the row sums over block blk
+  auto pv = [&](int blk, auto tail_tag, const s16x8 (&pb)[QT][2]) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    const char* S0 = reinterpret_cast<const char*>(smem + (blk % NBUF) * BLK);
+    const int k0 = blk * KB;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (TAIL && k0 + 32 * u >= L) continue;            // P = 0 on all 32 keys
@@ -504,6 +510,7 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
 
   const int nblk = (L + KB - 1) / KB;
   const int nfull = L / KB;                              // blocks with every key < L
+  s16x8 pb[QT][2];
 #pragma unroll
   for (int b = 0; b <= AHEAD; ++b)
     if (b < nblk) issue(b);
@@ -517,8 +524,13 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
     __builtin_amdgcn_sched_barrier(0);                    // every wave is done with block blk - 1
     if (blk + AHEAD + 1 < nblk) issue(blk + AHEAD + 1);   // into block blk - 1's slot
     if (live) {
-      if (blk < nfull) block(blk, std::false_type{});
-      else block(blk, std::true_type{});
+      if (blk < nfull) {
+        scores(blk, std::false_type{}, pb);
+        pv(blk, std::false_type{}, pb);
+      } else {
+        scores(blk, std::true_type{}, pb);
+        pv(blk, std::true_type{}, pb);
+      }
     }
   }
 #pragma unroll
@@ -571,15 +583,15 @@ void launch_dense(const AttnP& p, hipStream_t st) {
   else launch<T, D, 8, 64, 1, 0, false, false>(p, st);
 }
 
-int g_attn_l2s_nw = 8;   // mode-2 ViT kernel: waves per workgroup (8 or 10; tools/micro_attn.py)
 
 template <typename T>
 int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
   if (p.mode == 2) {
     if constexpr (sizeof(T) != 2) return -1;
     if (head_dim != 64 || p.causal) return -1;
-    if (g_attn_l2s_nw == 10) launch_vit3<10, 1, true>(p, st);
-    else launch_vit3<8, 1, true>(p, st);
+    // (measured and not kept: 10 waves x 16 queries, 512 workgroups in one round, 29.4 vs 27.4 us;
+    // waves 4-7 half a block behind on a 5-slot ring, 29.3 vs 28.1 us)
+    launch_vit3<8, 1, true>(p, st);
     return 0;
   }
   if (p.mode == 1) {
@@ -597,7 +609,6 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
 
 CATSEG_KNOB(g_attn_variant, "attn_variant");
 CATSEG_KNOB(g_attn_tail_skip, "attn_tail_skip");
-CATSEG_KNOB(g_attn_l2s_nw, "attn_l2s_nw");
 
 extern "C" int catseg_attention(const CatsegAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->q && a->k && a->v && a->out, "attention: null pointer");

@@ -309,9 +309,8 @@ def test_attention_dense(dt, L_, H, causal):
     close(out, ref, atol=2e-5 if dt == torch.float32 else 1.5e-2, what="attn")
 
 
-@pytest.mark.parametrize("nw", [8, 10])
 @pytest.mark.parametrize("L_,spike", [(577, None), (50, None), (129, None), (577, 300), (577, 5)])
-def test_attention_dense_log2_scaled_q(nw, L_, spike):
+def test_attention_dense_log2_scaled_q(L_, spike):
     """Mode 2 (the ViT blocks: q rows carry scale * log2(e), folded into the q projection; the
     running max enters the S MFMA as its accumulator): vs fp64 softmax attention of the unscaled q,
     including a spike key that forces the defer-max rescale in block 0 / a middle block."""
@@ -324,16 +323,12 @@ def test_attention_dense_log2_scaled_q(nw, L_, spike):
     q[:, :H * d] *= c
     qb = q.to(dev, torch.bfloat16)
     out = torch.empty(B * L_, H * d, device=dev, dtype=torch.bfloat16)
-    try:
-        L.tune("attn_l2s_nw", nw)
-        ops.attention(qb[:, :H * d], qb[:, H * d:2 * H * d], qb[:, 2 * H * d:], out, n_seq=B, seq_len=L_,
-                      n_heads=H, head_dim=d, scale=0.0, mode=2)
-    finally:
-        L.tune("attn_l2s_nw", 8)
+    ops.attention(qb[:, :H * d], qb[:, H * d:2 * H * d], qb[:, 2 * H * d:], out, n_seq=B, seq_len=L_,
+                  n_heads=H, head_dim=d, scale=0.0, mode=2)
     x = q.to(torch.bfloat16).double().reshape(B, L_, 3, H, d).permute(2, 0, 3, 1, 4)
     s = (x[0] @ x[1].transpose(-1, -2)) * math.log(2.0)
     ref = (torch.softmax(s, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B * L_, H * d)
-    close(out, ref, atol=1.5e-2, what=f"attn mode 2 nw={nw} L={L_} spike={spike}")
+    close(out, ref, atol=1.5e-2, what=f"attn mode 2 L={L_} spike={spike}")
     with pytest.raises(RuntimeError):     # fp32 / causal are not mode-2 shapes
         ops.attention(qb[:, :H * d].float(), qb[:, H * d:2 * H * d].float(), qb[:, 2 * H * d:].float(),
                       out.float(), n_seq=B, seq_len=L_, n_heads=H, head_dim=d, scale=0.0, mode=2)

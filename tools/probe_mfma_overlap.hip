@@ -2,7 +2,7 @@
 // and the exact instruction sequence of the intermittently wrong Swin build (K=16 bf16 MFMAs) --
 // give the same bits as the same products on disjoint registers?  Standalone program:
 //   hipcc -O2 --offload-arch=gfx950 tools/probe_mfma_overlap.hip -o build/probe_mfma_overlap
-//   build/probe_mfma_overlap      -> one line per variant: mismatching result words / words checked
+//   build/probe_mfma_overlap [iters]  -> one line per variant: mismatching result words / words checked
 // Each variant runs a test form and a reference form (every operand in its own registers, 32 wait
 // states between dependent instructions) in the same lane on the same operands, 2048 workgroups x
 // 8 waves x 32 iterations; "hammer" runs the same with waves 4-7 issuing back-to-back 32x32x16
@@ -24,7 +24,7 @@
     }                                                                                 \
   } while (0)
 
-constexpr int NB = 2048, NT = 512, ITERS = 32, NW = 24, NV = 18;
+constexpr int NB = 2048, NT = 512, NW = 24, NV = 18;
 
 #define PAD "s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n"
 // operand words -> v[64:87]: A16 v[64:65], B16 v[66:67], C v[68:71], A32 v[72:75], B32 v[76:79],
@@ -256,7 +256,7 @@ typedef __attribute__((__vector_size__(16 * sizeof(float)))) float f32x16;
 
 template <int V>
 __global__ __launch_bounds__(NT) void probe(const uint32_t* __restrict__ in, unsigned long long* __restrict__ bad,
-                                            int hammer) {
+                                            int hammer, int iters) {
   __shared__ float lds[NT * 4];
   for (int k = 0; k < 4; ++k) lds[threadIdx.x * 4 + k] = 1e9f;
   __syncthreads();
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(NT) void probe(const uint32_t* __restrict__ in, uns
     bf16x8 a, b;
     for (int k = 0; k < 8; ++k) { a[k] = (__bf16)(0.001f * (threadIdx.x + k)); b[k] = (__bf16)(0.002f * k); }
     f32x16 acc[4] = {};
-    for (int it = 0; it < ITERS * 6; ++it)
+    for (int it = 0; it < iters * 6; ++it)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
     float s = 0.f;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(NT) void probe(const uint32_t* __restrict__ in, uns
   const int64_t gid = (int64_t)blockIdx.x * NT + threadIdx.x;
   const uint32_t lds_addr = (uint32_t)(uintptr_t)&lds[threadIdx.x * 4];
   unsigned long long nb = 0;
-  for (int it = 0; it < ITERS; ++it) {
+  for (int it = 0; it < iters; ++it) {
     uint32_t w[NW];
     const uint32_t* src = in + (((gid * 7 + it * 131) & 65535) * NW);
     for (int k = 0; k < NW; ++k) w[k] = src[k];
@@ -291,12 +291,14 @@ __global__ __launch_bounds__(NT) void probe(const uint32_t* __restrict__ in, uns
 }
 
 template <int V>
-void launch(const uint32_t* din, unsigned long long* dbad, int hammer) {
-  hipLaunchKernelGGL(probe<V>, dim3(NB), dim3(NT), 0, 0, din, dbad, hammer);
-  if constexpr (V + 1 < NV) launch<V + 1>(din, dbad, hammer);
+void launch(const uint32_t* din, unsigned long long* dbad, int hammer, int iters) {
+  hipLaunchKernelGGL(probe<V>, dim3(NB), dim3(NT), 0, 0, din, dbad, hammer, iters);
+  if constexpr (V + 1 < NV) launch<V + 1>(din, dbad, hammer, iters);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 32;   // iterations per wave (the test runs 4)
+  if (iters < 1 || iters > 1024) { printf("bad iteration count\n"); return 2; }
   std::vector<uint32_t> h(65536 * NW);
   uint64_t s = 88172645463325252ull;
   for (size_t e = 0; e < h.size(); ++e) {
@@ -321,13 +323,13 @@ int main() {
                            "k32 ready srcC + LDS"};
   for (int hammer = 0; hammer < 2; ++hammer) {
     CHECK(hipMemset(dbad, 0, (2 * NV + 1) * 8));
-    launch<0>(din, dbad, hammer);
+    launch<0>(din, dbad, hammer, iters);
     CHECK(hipDeviceSynchronize());
     unsigned long long hb[2 * NV + 1];
     CHECK(hipMemcpy(hb, dbad, sizeof(hb), hipMemcpyDeviceToHost));
     for (int v = 0; v < NV; ++v)
       printf("%s %-26s mismatching words %llu of %llu\n", hammer ? "hammer" : "plain ", names[v], hb[v],
-             hb[NV + v] * ITERS * 16);
+             hb[NV + v] * iters * 16);
   }
   return 0;
 }
