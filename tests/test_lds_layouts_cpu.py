@@ -1,0 +1,36 @@
+"""LDS layouts of the decoder convs against the gfx950 bank model (tools/lds_bank_model.py;
+MI355X_MICROARCH.md LDS table): the shipped ring-conv pitch / write order and the im2col conv's
+swizzle give conflict-free fragment reads, and the round-3 layouts they replace did not."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import lds_bank_model as M  # noqa: E402
+
+
+def test_bank_model_basics():
+    lin = [16 * l for l in range(64)]                        # 64 lanes, contiguous 16-byte chunks
+    assert M.read_cycles(lin) == 4 and M.write_cycles(lin) == 8
+    same_bank = [256 * l for l in range(64)]                 # every lane on banks 0-3, distinct rows
+    assert M.read_cycles(same_bank) == 4 * 16
+
+
+def test_ring_conv_layouts_conflict_free():
+    for C, W, H, CH, NR, up in M.RING_SHAPES:
+        psb = M.ring_psb(C)
+        reads = M.extra(M.ring_fragment_reads(C, W, H, CH, NR, up, psb, M.ring_pad(psb)), "read")
+        assert reads == 0.0, (C, W, reads)
+        if C in (32, 64, 128):                               # the hot-path ring widths
+            writes = M.extra(M.ring_writes(C, W, NR, psb, M.ring_pad(psb), M.ring_perm(C)), "write")
+            assert writes < 0.02, (C, W, writes)
+    # what the pad and the write order fix (round 3)
+    assert M.extra(M.ring_fragment_reads(128, 24, 24, 64, 6, True, 288, 0), "read") > 0.3
+    assert M.extra(M.ring_writes(32, 96, 5, 96, 0, lambda i: i), "write") > 0.8
+
+
+def test_im2col_conv_tile_swizzle():
+    assert M.extra(M.conv_fragment_reads(64, True), "read") == 0.0
+    assert M.extra(M.conv_stage_writes(64, True), "write") == 0.0
+    assert M.extra(M.conv_fragment_reads(80, False), "read") == 1.0
