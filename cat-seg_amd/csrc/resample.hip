@@ -475,8 +475,244 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
   }
 }
 
-// 0 = staged merge with tabulated row terms and balanced columns (sliding_merge_tab_kernel, nb == 2),
-// 1 = band kernel, 2 = staged merge (sliding_merge_stage_kernel)
+// Separable merge (nb == 2): every bilinear blend of the merge is split
+// into its vertical half, formed once per output row in LDS and shared by the whole row, and its
+// horizontal half, the only per-output work.  Per band of SEP_BY output rows (one workgroup):
+//   1. stage the global plane's source rows and the covering tile planes' source rows (96 wide);
+//      tabulate each band row's vertical taps (threads < SEP_BY);
+//   2. blend the global source rows vertically for each k-res row under the band;
+//   3. k-res global sigmoid map rows: a horizontal lerp + sigmoid per element;
+//   4. per band row: the global k-res rows blended vertically (k wide) and each covering tile
+//      plane's source rows blended vertically (w wide), into rb (aliasing steps 1-2's buffers);
+//   5. per output: a horizontal lerp of rb's global row, and per covering tile a horizontal lerp +
+//      sigmoid, the Fold average and the average with the global term.
+// The tabulated merge instead blended four LDS values per term (~45 VALU per output).  Same taps,
+// sigmoid and Fold average as the staged kernels; the blends run vertical-then-horizontal instead
+// of torch's horizontal-then-vertical order (an ulp of a probability).
+constexpr int SEP_BY = 8, SEP_MAXJ = 4;     // band rows; rb slots per thread (k + 4 w <= 1024)
+struct SepGeom {
+  int r_lo, nr, gs_lo, gs_rows, trows;
+};
+__global__ __launch_bounds__(256) void sliding_merge_sep_kernel(const float* __restrict__ lg, int T, int h, int w,
+                                                                int k, int stride, int out_res, int bands, int grows,
+                                                                int gsrows, int trows, float* __restrict__ out) {
+  extern __shared__ float smem_s[];
+  const int RW = k + 4 * w;
+  float* gsig = smem_s;                        // [grows][k]: sigmoid of the global k-res map rows
+  float* tsl = gsig + grows * k;               // [2 tile rows][2 tile cols][trows][w]: tile-plane source rows
+  float* rb = tsl + 4 * trows * w;             // [SEP_BY][k + 4 w]: vertically blended rows (step 4)
+  float* gsrc = rb;                            // [gsrows][w]: global-plane source rows (steps 1-2, aliases rb)
+  float* gvb = gsrc + gsrows * w;              // [grows][w]: global source rows blended vertically (step 2)
+  __shared__ int ti[SEP_BY][6];                // per band row: the two global k-res rows (rel. r_lo, x k);
+                                               // per tile row bi: its two source rows (rel., x w), or -1
+  __shared__ float tf[SEP_BY][3];              // ly (global), tly[0], tly[1]
+  constexpr int nb = 2, L = nb * nb + 1;
+  const int64_t nt = blockIdx.x / bands;
+  const int band = blockIdx.x % bands;
+  const int t = (int)(nt % T);
+  const int64_t n = nt / T;
+  const int Y0 = band * SEP_BY, Y1 = min(Y0 + SEP_BY, out_res), nrow = Y1 - Y0;
+  const float sg = (float)k / (float)out_res, st_ = (float)h / (float)k, sx = (float)w / (float)k;
+  int r_lo, r_hi, tmp;
+  float tl;
+  lin_src(Y0, k, sg, r_lo, tmp, tl);
+  lin_src(Y1 - 1, k, sg, tmp, r_hi, tl);
+  const int nr = r_hi - r_lo + 1;
+  int gs_lo, gs_hi;
+  lin_src(r_lo, h, st_, gs_lo, tmp, tl);
+  lin_src(r_hi, h, st_, tmp, gs_hi, tl);
+  const int64_t plane = (int64_t)h * w;
+  // 1. staging and row tables.  The five source segments (the global plane's rows, then the
+  // covering tile planes' rows, each contiguous in HBM) are copied as one flat list, SEP_LD
+  // loads per thread issued before the first LDS write, so a band pays one HBM round trip
+  // instead of one per loop trip.
+  int tlo[2] = {0, 0};
+  const float* sp[5];
+  float* sd[5];
+  int se[5];                                   // cumulative segment ends in the flat list
+  sp[0] = lg + ((n * L + L - 1) * T + t) * plane + (int64_t)gs_lo * w;
+  sd[0] = gsrc;
+  se[0] = (gs_hi - gs_lo + 1) * w;
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    const int ya = max(Y0, stride * bi), yb = min(Y1, stride * bi + k) - 1;
+    int rows = 0;
+    if (ya <= yb) {
+      int a0, a1, b0, b1;
+      float la;
+      lin_src(ya - stride * bi, h, st_, a0, a1, la);
+      lin_src(yb - stride * bi, h, st_, b0, b1, la);
+      tlo[bi] = a0;
+      rows = b1 - a0 + 1;
+    }
+#pragma unroll
+    for (int bj = 0; bj < nb; ++bj) {
+      const int sgi = 1 + bi * 2 + bj;
+      sp[sgi] = lg + ((n * L + bi * nb + bj) * T + t) * plane + (int64_t)tlo[bi] * w;
+      sd[sgi] = tsl + (bi * 2 + bj) * trows * w;
+      se[sgi] = se[sgi - 1] + rows * w;
+    }
+  }
+  constexpr int SEP_LD = 8;
+  for (int base = 0; base < se[4]; base += SEP_LD * 256) {
+    float v[SEP_LD];
+    int sgm[SEP_LD], off[SEP_LD];
+#pragma unroll
+    for (int m = 0; m < SEP_LD; ++m) {
+      const int i = min(base + (int)threadIdx.x + 256 * m, se[4] - 1);
+      const int g = (i >= se[0]) + (i >= se[1]) + (i >= se[2]) + (i >= se[3]);
+      sgm[m] = g;
+      off[m] = i - (g ? se[g - 1] : 0);
+      v[m] = sp[g][off[m]];
+    }
+#pragma unroll
+    for (int m = 0; m < SEP_LD; ++m)
+      if (base + (int)threadIdx.x + 256 * m < se[4]) sd[sgm[m]][off[m]] = v[m];
+  }
+  if (threadIdx.x < nrow) {
+    const int Y = Y0 + threadIdx.x;
+    int y0, y1;
+    float ly;
+    lin_src(Y, k, sg, y0, y1, ly);
+    ti[threadIdx.x][0] = (y0 - r_lo) * k;
+    ti[threadIdx.x][1] = (y1 - r_lo) * k;
+    tf[threadIdx.x][0] = ly;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) {
+      const int yy = Y - stride * bi;
+      if (yy < 0 || yy >= k) {
+        ti[threadIdx.x][2 + 2 * bi] = -1;
+        ti[threadIdx.x][3 + 2 * bi] = -1;
+        tf[threadIdx.x][1 + bi] = 0.f;
+      } else {
+        int ty0, ty1;
+        float tly;
+        lin_src(yy, h, st_, ty0, ty1, tly);
+        ti[threadIdx.x][2 + 2 * bi] = (ty0 - tlo[bi]) * w;
+        ti[threadIdx.x][3 + 2 * bi] = (ty1 - tlo[bi]) * w;
+        tf[threadIdx.x][1 + bi] = tly;
+      }
+    }
+  }
+  __syncthreads();
+  // 2. global source rows blended vertically, one per k-res row under the band
+  if (threadIdx.x < w) {
+    for (int i = 0; i < nr; ++i) {
+      int y0, y1;
+      float ly;
+      lin_src(r_lo + i, h, st_, y0, y1, ly);
+      gvb[i * w + threadIdx.x] = (1.f - ly) * gsrc[(y0 - gs_lo) * w + threadIdx.x] +
+                                 ly * gsrc[(y1 - gs_lo) * w + threadIdx.x];
+    }
+  }
+  __syncthreads();
+  // 3. the k-res global sigmoid rows (k <= 512: two columns per thread)
+  {
+    int x0[2], x1[2];
+    float lx[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) lin_src(min((int)threadIdx.x + 256 * m, k - 1), w, sx, x0[m], x1[m], lx[m]);
+    for (int i = 0; i < nr; ++i) {
+      const float* gv = gvb + i * w;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int x = threadIdx.x + 256 * m;
+        if (x < k) gsig[i * k + x] = sigm_fast((1.f - lx[m]) * gv[x0[m]] + lx[m] * gv[x1[m]]);
+      }
+    }
+  }
+  __syncthreads();
+  // 4. vertical blends of every band row: rb[r][j], j < k global, else tile plane q = (j - k) / w
+  {
+    int jo[SEP_MAXJ], jq[SEP_MAXJ];
+#pragma unroll
+    for (int m = 0; m < SEP_MAXJ; ++m) {
+      const int j = threadIdx.x + 256 * m;
+      jq[m] = j < k ? -1 : (j < RW ? (j - k) / w : 4);
+      jo[m] = j < k ? j : (jq[m] < 4 ? jq[m] * trows * w + (j - k - jq[m] * w) : 0);
+    }
+#pragma unroll
+    for (int r = 0; r < SEP_BY; ++r) {
+      if (r >= nrow) break;
+      const float ly = tf[r][0];
+      const float* g0 = gsig + ti[r][0];
+      const float* g1 = gsig + ti[r][1];
+      float* dst = rb + r * RW;
+#pragma unroll
+      for (int m = 0; m < SEP_MAXJ; ++m) {
+        const int j = threadIdx.x + 256 * m;
+        if (jq[m] < 0) {
+          dst[j] = (1.f - ly) * g0[jo[m]] + ly * g1[jo[m]];
+        } else if (jq[m] < 4) {
+          const int bi = jq[m] >> 1, o0 = ti[r][2 + 2 * bi];
+          if (o0 >= 0) {
+            const float tly = tf[r][1 + bi];
+            dst[j] = (1.f - tly) * tsl[jo[m] + o0] + tly * tsl[jo[m] + ti[r][3 + 2 * bi]];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // 5. outputs: columns t and t + 256 over every band row, the remainder columns split over row groups
+  float* ob = out + nt * (int64_t)out_res * out_res;
+  const int full = out_res / 256, rem = out_res % 256;
+  const int ncols = full + (rem ? 1 : 0);
+  for (int c = 0; c < ncols; ++c) {
+    int X, ya, yb;
+    if (c < full) {
+      X = threadIdx.x + 256 * c; ya = 0; yb = nrow;
+    } else {
+      const int groups = 256 / rem, gi = threadIdx.x / rem;
+      if (gi >= groups) break;
+      X = 256 * full + threadIdx.x % rem;
+      const int per = (nrow + groups - 1) / groups;
+      ya = gi * per; yb = min(nrow, ya + per);
+    }
+    int gx0, gx1;
+    float glx;
+    lin_src(X, k, sg, gx0, gx1, glx);
+    int o0[2], o1[2], ncol = 0;
+    float tlx[2];
+#pragma unroll
+    for (int bj = 0; bj < nb; ++bj) {
+      const int xx = X - stride * bj;
+      if (xx < 0 || xx >= k) continue;
+      int x0, x1;
+      lin_src(xx, w, sx, x0, x1, tlx[ncol]);
+      o0[ncol] = k + bj * w + x0;
+      o1[ncol] = k + bj * w + x1;
+      ++ncol;
+    }
+    // band rows unrolled: the tile-row coverage is integer math on Y (no LDS round trip per row),
+    // so every row's LDS reads can be in flight together
+#pragma unroll
+    for (int yi = 0; yi < SEP_BY; ++yi) {
+      if (yi < ya || yi >= yb) continue;
+      const int Y = Y0 + yi;
+      const float* br = rb + yi * RW;
+      const float glob = (1.f - glx) * br[gx0] + glx * br[gx1];
+      float sum = 0.f, cnt = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < nb; ++bi) {
+        if ((unsigned)(Y - stride * bi) >= (unsigned)k) continue;
+        const float* tr = br + bi * 2 * w;
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+          if (cc >= ncol) break;
+          sum += sigm_fast((1.f - tlx[cc]) * tr[o0[cc]] + tlx[cc] * tr[o1[cc]]);
+          cnt += 1.f;
+        }
+      }
+      ob[(int64_t)(Y0 + yi) * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
+    }
+  }
+}
+
+// 0 = staged merge with tabulated row terms (sliding_merge_tab_kernel, nb == 2), 1 = band kernel,
+// 2 = staged merge (sliding_merge_stage_kernel), 3 = the tabulated merge as well, 4 = separable
+// merge (sliding_merge_sep_kernel, nb == 2); a variant whose shape limits are not met falls
+// through in the order 4 -> 0/3 -> 2 -> 1
 int g_merge_variant = 0;
 
 }  // namespace
@@ -538,7 +774,23 @@ extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h
     // tile-plane rows under one band: (MERGE_BY - 1) output rows span (MERGE_BY - 1) h / k source rows
     const int trows = (int)((int64_t)(MERGE_BY - 1) * h / kernel) + 3;
     const size_t sh2 = ((size_t)rows * kernel + (size_t)4 * trows * w) * sizeof(float);
-    if (g_merge_variant == 0 && nb == 2 && sh2 <= 64 * 1024 && out_res <= 768) {
+    if (g_merge_variant == 4 && nb == 2 && kernel + 4 * w <= 256 * SEP_MAXJ && kernel <= 512 && w <= 256 &&
+        out_res <= 768) {
+      const int sbands = (out_res + SEP_BY - 1) / SEP_BY;
+      const int64_t sblocks = N * T * (int64_t)sbands;
+      // k-res global rows under SEP_BY output rows (+2 taps); their 96-res source rows; tile source rows
+      const int grows = (int)((int64_t)(SEP_BY - 1) * kernel / out_res) + 3;
+      const int gsrows = (int)((int64_t)(grows - 1) * h / kernel) + 3;
+      const int strows = (int)((int64_t)(SEP_BY - 1) * h / kernel) + 3;
+      const size_t rbf = std::max((size_t)SEP_BY * (kernel + 4 * w), (size_t)(gsrows + grows) * w);
+      const size_t sh_sep = ((size_t)grows * kernel + (size_t)4 * strows * w + rbf) * sizeof(float);
+      if (sh_sep <= 64 * 1024 && sblocks < ((int64_t)1 << 31)) {
+        hipLaunchKernelGGL(sliding_merge_sep_kernel, dim3((unsigned)sblocks), dim3(256), sh_sep, (hipStream_t)stream,
+                           logits, T, h, w, kernel, stride, out_res, sbands, grows, gsrows, strows, out);
+        return catseg_launch_status("sliding_merge");
+      }
+    }
+    if ((g_merge_variant == 0 || g_merge_variant == 3) && nb == 2 && sh2 <= 64 * 1024 && out_res <= 768) {
       hipLaunchKernelGGL(sliding_merge_tab_kernel, dim3((unsigned)blocks), dim3(256), sh2, (hipStream_t)stream, logits,
                          T, h, w, kernel, stride, out_res, bands, rows, trows, out);
       return catseg_launch_status("sliding_merge");

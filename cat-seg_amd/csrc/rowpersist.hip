@@ -214,10 +214,14 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
 // out = Y + act(LN(Y) . W1^T + b1) . W2^T + b2 (+ R2), hidden = 512.
 // wave w: GEMM1 hidden rows [64w, 64w+64) (W1 fragments in registers),
 //         GEMM2 output rows [16w, 16w+16) over all 512 hidden (W2 fragments in registers).
-// sH row stride: 264 dwords = 66 x 16 B makes the 16-B slot of GEMM2 fragment reads
-// (2 r16 + q) mod 16 -- conflict-free in every ds_read_b128 lane group (+8 measured 42 %
-// SQ_LDS_BANK_CONFLICT: slot r16 + q collides once per group)
-constexpr int HID = 512, LDH = HID + 16;
+// sH: unpadded 512-element rows, 16-byte chunk c of row r at slot c ^ (r & 15).  The GEMM1
+// output writes (8 lanes = rows r..r+7 of one chunk) and the GEMM2 fragment reads (lanes r16, q:
+// chunk 4 ks + q of row r16) then hit distinct bank slots in every lane group
+// (tools/lds_bank_model.py).  The round-3 pad of 16 elements (row stride 264 dwords) read
+// conflict-free but wrote 2-way conflicted (rows r and r + 4 on one slot): ~14 % of the kernel's
+// LDS cycles (SQ_LDS_BANK_CONFLICT); a pad of 8 had the reverse (42 %).
+constexpr int HID = 512, LDH = HID;
+DEV int hoff(int r, int e) { return r * LDH + ((((e >> 3) ^ (r & 15))) << 3) + (e & 7); }
 
 // PROJ (catseg_swin_proj_mlp): the Swin block's output projection + residual runs first, per
 // tile: x1 = bf16(x + attn . Wp^T + bp) (model.py:112 proj, :222 shortcut), then the MLP above
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
               if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
               else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
             }
-          st16(&sH[(16 * j + r16) * LDH + hh], pack8(v));
+          st16(&sH[hoff(16 * j + r16, hh)], pack8(v));
         }
       } else {
 #pragma unroll
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r]);
           }
-          store4<bf16>(&sH[(16 * j + r16) * LDH + hh], v);
+          store4<bf16>(&sH[hoff(16 * j + r16, hh)], v);
         }
       }
       }
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + 8 * q]);
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[hoff(16 * j + r16, ks * 32 + 8 * q)]);
         acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
       }
     }
@@ -511,7 +515,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
             if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
             else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
           }
-        st16(&sH[(16 * j + r16) * LDH + hh], pack8(v));
+        st16(&sH[hoff(16 * j + r16, hh)], pack8(v));
       }
     }
   };
@@ -580,7 +584,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
     for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + 8 * q]);
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[hoff(16 * j + r16, ks * 32 + 8 * q)]);
         acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
       }
     }

@@ -120,6 +120,29 @@ def conv_stage_writes(row_bytes: int, swizzle: bool, nt: int = 256):
                for lane in range(64)]
 
 
+# ---------------------------------------------------------------- rowpersist.hip MLP hidden tile
+def mlp_hidden_off(row: int, col: int, ldh: int, swizzle: bool) -> int:
+    """Byte offset of bf16 hidden element (row, col): chunk col / 8 at slot chunk ^ (row & 15) when swizzled."""
+    if swizzle:
+        return (row * ldh + (((col >> 3) ^ (row & 15)) << 3) + (col & 7)) * 2
+    return (row * ldh + col) * 2
+
+
+def mlp_hidden_writes(ldh: int, swizzle: bool):
+    """GEMM1's output stores: wave w, half hf, row block j; lane (r16, q) -> row 16 j + r16, column 64 w + 32 hf + 8 q."""
+    for w in range(8):
+        for hf in range(2):
+            for j in range(2):
+                yield [mlp_hidden_off(16 * j + (l & 15), 64 * w + 32 * hf + 8 * (l >> 4), ldh, swizzle) for l in range(64)]
+
+
+def mlp_hidden_reads(ldh: int, swizzle: bool):
+    """GEMM2's B fragments: row block j, k-step ks; lane (r16, q) -> row 16 j + r16, column 32 ks + 8 q."""
+    for j in range(2):
+        for ks in range(16):
+            yield [mlp_hidden_off(16 * j + (l & 15), 32 * ks + 8 * (l >> 4), ldh, swizzle) for l in range(64)]
+
+
 # the shipped ring geometries: (C, W, H, CH, NR, up) = (channels, width, height, pixels per chunk, ring rows, fold)
 RING_SHAPES = [(128, 24, 24, 64, 6, True), (64, 48, 48, 64, 5, True), (32, 96, 96, 128, 5, False),
                (64, 48, 48, 128, 6, False), (96, 48, 48, 64, 5, False)]
@@ -132,6 +155,9 @@ def main():
             r = extra(ring_fragment_reads(C, W, H, CH, NR, up, psb, rpad), "read")
             w = extra(ring_writes(C, W, NR, psb, rpad, perm), "write")
             print(f"ring C={C:3d} W={W:2d} {label}: fragment reads +{r:.3f}, ring writes +{w:.3f}")
+    for label, ldh, sw in (("round 3 (+16 pad)", 528, False), ("shipped (swizzle)", 512, True)):
+        print(f"MLP hidden tile {label}: GEMM1 stores +{extra(mlp_hidden_writes(ldh, sw), 'write'):.3f}, "
+              f"GEMM2 fragment reads +{extra(mlp_hidden_reads(ldh, sw), 'read'):.3f}")
     for label, rb, sw in (("round 3 (+16 B pad)", 80, False), ("shipped (swizzle)", 64, True)):
         print(f"im2col conv {label}: fragment reads +{extra(conv_fragment_reads(rb, sw), 'read'):.3f}, "
               f"staging writes +{extra(conv_stage_writes(rb, sw), 'write'):.3f}")
