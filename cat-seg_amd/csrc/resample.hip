@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
 // The tabulated merge instead blended four LDS values per term (~45 VALU per output).  Same taps,
 // sigmoid and Fold average as the staged kernels; the blends run vertical-then-horizontal instead
 // of torch's horizontal-then-vertical order (an ulp of a probability).
-constexpr int SEP_BY = 8, SEP_MAXJ = 4;     // band rows; rb slots per thread (k + 4 w <= 1024)
+constexpr int SEP_BY = 8;                   // band rows
 struct SepGeom {
   int r_lo, nr, gs_lo, gs_rows, trows;
 };
@@ -606,55 +606,58 @@ __global__ __launch_bounds__(256) void sliding_merge_sep_kernel(const float* __r
     }
   }
   __syncthreads();
-  // 3. the k-res global sigmoid rows (k <= 512: two columns per thread)
-  {
-    int x0[2], x1[2];
-    float lx[2];
+  // 3. the k-res global sigmoid rows (k <= 512: two columns per thread; lane tests only outside
+  // the row loops, so each loop's LDS reads can be issued together)
 #pragma unroll
-    for (int m = 0; m < 2; ++m) lin_src(min((int)threadIdx.x + 256 * m, k - 1), w, sx, x0[m], x1[m], lx[m]);
-    for (int i = 0; i < nr; ++i) {
-      const float* gv = gvb + i * w;
+  for (int m = 0; m < 2; ++m) {
+    const int x = threadIdx.x + 256 * m;
+    if (x < k) {
+      int x0, x1;
+      float lx;
+      lin_src(x, w, sx, x0, x1, lx);
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int x = threadIdx.x + 256 * m;
-        if (x < k) gsig[i * k + x] = sigm_fast((1.f - lx[m]) * gv[x0[m]] + lx[m] * gv[x1[m]]);
+      for (int i = 0; i < SEP_BY + 2; ++i) {
+        if (i >= nr) break;                        // band-uniform
+        const float* gv = gvb + i * w;
+        gsig[i * k + x] = sigm_fast((1.f - lx) * gv[x0] + lx * gv[x1]);
       }
     }
   }
   __syncthreads();
-  // 4. vertical blends of every band row: rb[r][j], j < k global, else tile plane q = (j - k) / w
-  {
-    int jo[SEP_MAXJ], jq[SEP_MAXJ];
+  // 4. vertical blends of every band row: rb[r][j], j < k global, then the 4 tile planes' w-wide rows
 #pragma unroll
-    for (int m = 0; m < SEP_MAXJ; ++m) {
-      const int j = threadIdx.x + 256 * m;
-      jq[m] = j < k ? -1 : (j < RW ? (j - k) / w : 4);
-      jo[m] = j < k ? j : (jq[m] < 4 ? jq[m] * trows * w + (j - k - jq[m] * w) : 0);
+  for (int m = 0; m < 2; ++m) {
+    const int j = threadIdx.x + 256 * m;
+    if (j < k) {
+#pragma unroll
+      for (int r = 0; r < SEP_BY; ++r) {
+        if (r >= nrow) break;
+        const float ly = tf[r][0];
+        rb[r * RW + j] = (1.f - ly) * gsig[ti[r][0] + j] + ly * gsig[ti[r][1] + j];
+      }
     }
+  }
 #pragma unroll
-    for (int r = 0; r < SEP_BY; ++r) {
-      if (r >= nrow) break;
-      const float ly = tf[r][0];
-      const float* g0 = gsig + ti[r][0];
-      const float* g1 = gsig + ti[r][1];
-      float* dst = rb + r * RW;
+  for (int m = 0; m < 2; ++m) {
+    const int j = threadIdx.x + 256 * m;
+    if (j < 4 * w) {
+      const int q = j / w, bi = q >> 1;
+      const float* src = tsl + q * trows * w + (j - q * w);
 #pragma unroll
-      for (int m = 0; m < SEP_MAXJ; ++m) {
-        const int j = threadIdx.x + 256 * m;
-        if (jq[m] < 0) {
-          dst[j] = (1.f - ly) * g0[jo[m]] + ly * g1[jo[m]];
-        } else if (jq[m] < 4) {
-          const int bi = jq[m] >> 1, o0 = ti[r][2 + 2 * bi];
-          if (o0 >= 0) {
-            const float tly = tf[r][1 + bi];
-            dst[j] = (1.f - tly) * tsl[jo[m] + o0] + tly * tsl[jo[m] + ti[r][3 + 2 * bi]];
-          }
-        }
+      for (int r = 0; r < SEP_BY; ++r) {
+        if (r >= nrow) break;
+        // a tile row that does not cover this band row leaves 0 (finite; weighted 0 in step 5)
+        const int o0 = ti[r][2 + 2 * bi];
+        const float tly = tf[r][1 + bi];
+        rb[r * RW + k + j] = o0 >= 0 ? (1.f - tly) * src[o0] + tly * src[ti[r][3 + 2 * bi]] : 0.f;
       }
     }
   }
   __syncthreads();
-  // 5. outputs: columns t and t + 256 over every band row, the remainder columns split over row groups
+  // 5. outputs: columns t and t + 256 over every band row, the remainder columns split over row
+  // groups.  Branch-free per output (exec-masked branches around each term made hipcc wait for
+  // every LDS read in turn): both tile columns are always blended, a column not covering X reads
+  // a valid slot with weight 0; a tile row's terms are skipped only by a band-uniform test on Y.
   float* ob = out + nt * (int64_t)out_res * out_res;
   const int full = out_res / 256, rem = out_res % 256;
   const int ncols = full + (rem ? 1 : 0);
@@ -672,39 +675,39 @@ __global__ __launch_bounds__(256) void sliding_merge_sep_kernel(const float* __r
     int gx0, gx1;
     float glx;
     lin_src(X, k, sg, gx0, gx1, glx);
-    int o0[2], o1[2], ncol = 0;
-    float tlx[2];
+    int o0[2], o1[2];
+    float tlx[2], cw[2];
 #pragma unroll
     for (int bj = 0; bj < nb; ++bj) {
       const int xx = X - stride * bj;
-      if (xx < 0 || xx >= k) continue;
+      const bool in = xx >= 0 && xx < k;
       int x0, x1;
-      lin_src(xx, w, sx, x0, x1, tlx[ncol]);
-      o0[ncol] = k + bj * w + x0;
-      o1[ncol] = k + bj * w + x1;
-      ++ncol;
+      float l;
+      lin_src(in ? xx : 0, w, sx, x0, x1, l);
+      o0[bj] = k + bj * w + x0;
+      o1[bj] = k + bj * w + x1;
+      tlx[bj] = l;
+      cw[bj] = in ? 1.f : 0.f;
     }
-    // band rows unrolled: the tile-row coverage is integer math on Y (no LDS round trip per row),
-    // so every row's LDS reads can be in flight together
+    const float ncw = cw[0] + cw[1];
 #pragma unroll
     for (int yi = 0; yi < SEP_BY; ++yi) {
-      if (yi < ya || yi >= yb) continue;
+      if (yi >= nrow) break;                       // band-uniform
       const int Y = Y0 + yi;
       const float* br = rb + yi * RW;
       const float glob = (1.f - glx) * br[gx0] + glx * br[gx1];
-      float sum = 0.f, cnt = 0.f;
+      float sum = 0.f, rows = 0.f;
 #pragma unroll
       for (int bi = 0; bi < nb; ++bi) {
-        if ((unsigned)(Y - stride * bi) >= (unsigned)k) continue;
+        if ((unsigned)(Y - stride * bi) >= (unsigned)k) continue;   // band-uniform
         const float* tr = br + bi * 2 * w;
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-          if (cc >= ncol) break;
-          sum += sigm_fast((1.f - tlx[cc]) * tr[o0[cc]] + tlx[cc] * tr[o1[cc]]);
-          cnt += 1.f;
-        }
+        for (int cc = 0; cc < 2; ++cc)
+          sum += cw[cc] * sigm_fast((1.f - tlx[cc]) * tr[o0[cc]] + tlx[cc] * tr[o1[cc]]);
+        rows += 1.f;
       }
-      ob[(int64_t)(Y0 + yi) * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
+      const float v = (sum * __builtin_amdgcn_rcpf(rows * ncw) + glob) * 0.5f;
+      if (yi >= ya && yi < yb) ob[(int64_t)Y * out_res + X] = v;
     }
   }
 }
@@ -774,7 +777,7 @@ extern "C" int catseg_sliding_merge(const float* logits, int64_t N, int T, int h
     // tile-plane rows under one band: (MERGE_BY - 1) output rows span (MERGE_BY - 1) h / k source rows
     const int trows = (int)((int64_t)(MERGE_BY - 1) * h / kernel) + 3;
     const size_t sh2 = ((size_t)rows * kernel + (size_t)4 * trows * w) * sizeof(float);
-    if (g_merge_variant == 4 && nb == 2 && kernel + 4 * w <= 256 * SEP_MAXJ && kernel <= 512 && w <= 256 &&
+    if (g_merge_variant == 4 && nb == 2 && kernel <= 512 && w <= 128 &&
         out_res <= 768) {
       const int sbands = (out_res + SEP_BY - 1) / SEP_BY;
       const int64_t sblocks = N * T * (int64_t)sbands;

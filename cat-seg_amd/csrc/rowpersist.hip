@@ -214,14 +214,17 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
 // out = Y + act(LN(Y) . W1^T + b1) . W2^T + b2 (+ R2), hidden = 512.
 // wave w: GEMM1 hidden rows [64w, 64w+64) (W1 fragments in registers),
 //         GEMM2 output rows [16w, 16w+16) over all 512 hidden (W2 fragments in registers).
-// sH: unpadded 512-element rows, 16-byte chunk c of row r at slot c ^ (r & 15).  The GEMM1
-// output writes (8 lanes = rows r..r+7 of one chunk) and the GEMM2 fragment reads (lanes r16, q:
-// chunk 4 ks + q of row r16) then hit distinct bank slots in every lane group
-// (tools/lds_bank_model.py).  The round-3 pad of 16 elements (row stride 264 dwords) read
-// conflict-free but wrote 2-way conflicted (rows r and r + 4 on one slot): ~14 % of the kernel's
-// LDS cycles (SQ_LDS_BANK_CONFLICT); a pad of 8 had the reverse (42 %).
-constexpr int HID = 512, LDH = HID;
-DEV int hoff(int r, int e) { return r * LDH + ((((e >> 3) ^ (r & 15))) << 3) + (e & 7); }
+// sH: 528-element rows (66 16-byte slots), 16-byte chunk c of row r at slot c ^ ((r >> 2) & 1).
+// The GEMM1 output writes (8 lanes = rows r..r+7 of one chunk) and the GEMM2 fragment reads (lanes
+// r16, q: chunk 4 ks + q of row r16) then hit distinct bank slots in every lane group
+// (tools/lds_bank_model.py), and the swizzle only flips the q part of a chunk index, so a lane's
+// 16 GEMM2 reads stay one base + immediate offsets.  Round 3's unswizzled 528 read conflict-free
+// but wrote 2-way conflicted (rows r and r + 4 on one slot; ~14 % of the kernel's LDS cycles,
+// SQ_LDS_BANK_CONFLICT); 520 had the reverse (42 %); a full 4-bit row XOR on unpadded rows is
+// conflict-free too but its per-k-step addresses pushed the projection + MLP kernel to 256 VGPRs
+// and a spill (488 vs 398 us).
+constexpr int HID = 512, LDH = HID + 16;
+DEV int hoff(int r, int e) { return r * LDH + ((((e >> 3) ^ ((r >> 2) & 1))) << 3) + (e & 7); }
 
 // PROJ (catseg_swin_proj_mlp): the Swin block's output projection + residual runs first, per
 // tile: x1 = bf16(x + attn . Wp^T + bp) (model.py:112 proj, :222 shortcut), then the MLP above
@@ -258,6 +261,9 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   const float* sbp = sPar + 3 * KD + HID;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
+  // the hidden tile's chunk swizzle (hoff) as per-lane offsets: GEMM1 stores at column hh + hsw,
+  // GEMM2 fragment reads at ks * 32 + hq
+  const int hsw = (((q ^ ((r16 >> 2) & 1)) - q) << 3), hq = (q ^ ((r16 >> 2) & 1)) << 3;
   s16x8 wpf[PROJ ? 4 : 1];           // PROJ: Wp rows 16*wave .. +15 (this wave's proj columns)
   if constexpr (PROJ) {
 #pragma unroll
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
               if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
               else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
             }
-          st16(&sH[hoff(16 * j + r16, hh)], pack8(v));
+          st16(&sH[(16 * j + r16) * LDH + hh + hsw], pack8(v));
         }
       } else {
 #pragma unroll
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
     for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[hoff(16 * j + r16, ks * 32 + 8 * q)]);
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + hq]);
         acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
       }
     }
@@ -449,6 +455,9 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
   const float* sbp = sPar + 3 * KD + HID;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
+  // the hidden tile's chunk swizzle (hoff) as per-lane offsets: GEMM1 stores at column hh + hsw,
+  // GEMM2 fragment reads at ks * 32 + hq
+  const int hsw = (((q ^ ((r16 >> 2) & 1)) - q) << 3), hq = (q ^ ((r16 >> 2) & 1)) << 3;
   s16x8 wpf[PROJ ? 4 : 1];
   if constexpr (PROJ) {
 #pragma unroll
@@ -515,7 +524,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
             if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
             else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
           }
-        st16(&sH[hoff(16 * j + r16, hh)], pack8(v));
+        st16(&sH[(16 * j + r16) * LDH + hh + hsw], pack8(v));
       }
     }
   };
@@ -584,7 +593,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
     for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[hoff(16 * j + r16, ks * 32 + 8 * q)]);
+        const s16x8 hf = *reinterpret_cast<const s16x8*>(&sH[(16 * j + r16) * LDH + ks * 32 + hq]);
         acc2[j] = mfma_bf16(w2f[ks], hf, acc2[j]);
       }
     }

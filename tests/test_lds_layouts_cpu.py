@@ -38,8 +38,8 @@ def test_im2col_conv_tile_swizzle():
 
 def test_mlp_hidden_tile_swizzle():
     """rowpersist.hip hoff(): the persistent MLP's hidden tile, written by GEMM1 and read by GEMM2."""
-    assert M.extra(M.mlp_hidden_writes(512, True), "write") == 0.0
-    assert M.extra(M.mlp_hidden_reads(512, True), "read") == 0.0
+    assert M.extra(M.mlp_hidden_writes(528, True), "write") == 0.0
+    assert M.extra(M.mlp_hidden_reads(528, True), "read") == 0.0
     # round 3's padded rows: conflict-free reads, 2-way conflicted writes (and the reverse at +8)
     assert M.extra(M.mlp_hidden_writes(528, False), "write") == 1.0
     assert M.extra(M.mlp_hidden_reads(520, False), "read") == 1.0

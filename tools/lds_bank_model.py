@@ -122,9 +122,9 @@ def conv_stage_writes(row_bytes: int, swizzle: bool, nt: int = 256):
 
 # ---------------------------------------------------------------- rowpersist.hip MLP hidden tile
 def mlp_hidden_off(row: int, col: int, ldh: int, swizzle: bool) -> int:
-    """Byte offset of bf16 hidden element (row, col): chunk col / 8 at slot chunk ^ (row & 15) when swizzled."""
+    """Byte offset of bf16 hidden element (row, col): chunk col / 8 at slot chunk ^ ((row >> 2) & 1) when swizzled."""
     if swizzle:
-        return (row * ldh + (((col >> 3) ^ (row & 15)) << 3) + (col & 7)) * 2
+        return (row * ldh + (((col >> 3) ^ ((row >> 2) & 1)) << 3) + (col & 7)) * 2
     return (row * ldh + col) * 2
 
 
@@ -155,7 +155,7 @@ def main():
             r = extra(ring_fragment_reads(C, W, H, CH, NR, up, psb, rpad), "read")
             w = extra(ring_writes(C, W, NR, psb, rpad, perm), "write")
             print(f"ring C={C:3d} W={W:2d} {label}: fragment reads +{r:.3f}, ring writes +{w:.3f}")
-    for label, ldh, sw in (("round 3 (+16 pad)", 528, False), ("shipped (swizzle)", 512, True)):
+    for label, ldh, sw in (("round 3 (+16 pad)", 528, False), ("shipped (+16 pad, swizzle)", 528, True)):
         print(f"MLP hidden tile {label}: GEMM1 stores +{extra(mlp_hidden_writes(ldh, sw), 'write'):.3f}, "
               f"GEMM2 fragment reads +{extra(mlp_hidden_reads(ldh, sw), 'read'):.3f}")
     for label, rb, sw in (("round 3 (+16 B pad)", 80, False), ("shipped (swizzle)", 64, True)):
