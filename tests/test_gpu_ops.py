@@ -928,12 +928,11 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
         t = fold(o[:-1].flatten(1).T) / fold(unfold(torch.ones([1, res, res])))
         close(merged[i], ((t + glob) / 2.0)[0], atol=1e-5, what=f"merge {i}")
     # the band kernel gathering from global (1) equals the staged merge computing the row terms per
-    # output (2) bit for bit; the tabulated staged merge (0 = 3, default) has the same taps and Fold
-    # order but the compiler contracts its blends into FMAs differently, and the separable merge (4)
-    # blends vertically first (an ulp of a probability each)
+    # output (2) bit for bit; the tabulated staged merge (0, default) has the same taps and Fold order
+    # but the compiler contracts its blends into FMAs differently (an ulp of a probability)
     lib = L.load()
     mv = {}
-    for v in (1, 2, 3, 4):
+    for v in (1, 2):
         mv[v] = torch.empty_like(merged)
         try:
             L.tune("merge_variant", v)
@@ -943,14 +942,12 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
             L.tune("merge_variant", 0)
     assert torch.equal(mv[1], mv[2])
     assert (merged - mv[2]).abs().max().item() <= 1e-6
-    assert (mv[3] - mv[2]).abs().max().item() <= 1e-6
-    assert (mv[4] - mv[2]).abs().max().item() <= 1e-6
-    # ragged band (out_res not a multiple of the 16-row band or the 2-row step) and one tile column
-    # per X in the middle: out_res 600 = 2 tiles of 360 at stride 240
+    # ragged band (out_res not a multiple of the 16-row band) with another window geometry:
+    # out_res 600 = 2 tiles of 360 at stride 240, 90-wide logits
     k2, s2, r2 = 360, 240, 600
     lg2 = rnd(1 * 5, 3, 90, 90, seed=45, scale=4.0)
     m2 = {}
-    for v in (0, 2, 4):
+    for v in (0, 2):
         m2[v] = torch.empty(1, 3, r2, r2, device=dev)
         try:
             L.tune("merge_variant", v)
@@ -959,7 +956,6 @@ def test_sliding_crops_and_merge_vs_oracle_ops():
         finally:
             L.tune("merge_variant", 0)
     assert (m2[0] - m2[2]).abs().max().item() <= 1e-6
-    assert (m2[4] - m2[2]).abs().max().item() <= 1e-6
     out = torch.empty(1, T, 480, 400, device=dev)
     ops.resize_bilinear(merged[:1], out, crop=(res, res))
     ref = F.interpolate(merged[:1].cpu(), size=(480, 400), mode="bilinear", align_corners=False)

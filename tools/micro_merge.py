@@ -1,7 +1,7 @@
 """Time catseg_sliding_merge at config 5's shape (8 images x 5 crops, T = 459, 96² logits -> 640²)
-for values of tuning knob merge_variant (0 = 3 = tabulated staged merge, 1 = band kernel, 2 = staged
-merge, 4 = separable merge), same process, and print every value's max difference from the first's.
-usage: python tools/micro_merge.py [variants, default 2,0,4]"""
+for values of tuning knob merge_variant (0 = tabulated staged merge, 1 = band kernel, 2 = staged
+merge), same process, and print every value's max difference from the first's.
+usage: python tools/micro_merge.py [variants, default 2,0]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
@@ -9,7 +9,7 @@ import torch
 from cat_seg import ops
 from cat_seg import _lib as L
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,0,4").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,0").split(",")]
 lib = L.load()
 torch.manual_seed(0)
 N, T = 8, 459
