@@ -355,7 +355,8 @@ __global__ __launch_bounds__(256) void sliding_merge_stage_kernel(const float* _
 // The global plane's source rows are staged in LDS with the tile rows, all of a band's source
 // loads issued before the first LDS write (one HBM round trip instead of one per loop trip), and
 // the k-res global sigmoid rows are blended from LDS instead of four global loads per element
-// (3.84 -> 3.59 ms per merge of 8 x 459 planes, same box).
+// (3.84 -> 3.59 ms per merge of 8 x 459 planes, same box).  The output terms are branch-light (see
+// below): 3.63 -> 3.38 ms, bit-identical.
 __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __restrict__ lg, int T, int h, int w,
                                                                 int k, int stride, int out_res, int bands, int grows,
                                                                 int trows, float* __restrict__ out) {
@@ -503,7 +504,13 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
       lin_src(xx, w, (float)w / (float)k, tx0[ncol], tx1[ncol], tlx[ncol]);
       tbj[ncol++] = bj;
     }
-#pragma unroll 4
+    // branch-light form: the second tile column duplicates the first's taps with weight 0 where
+    // only one covers X, and a term is skipped only by wave-uniform tests (no lane covers it), so
+    // no exec-masked branch separates a term's LDS reads from the next term's; x + 0 * s = x
+    // keeps the sum bit-identical
+    if (ncol == 1) { tx0[1] = tx0[0]; tx1[1] = tx1[0]; tlx[1] = tlx[0]; tbj[1] = tbj[0]; }
+    const float cw1 = ncol == 2 ? 1.f : 0.f;
+    const bool two = __builtin_amdgcn_ballot_w64(ncol == 2) != 0;
     for (int yi = ya; yi < yb; ++yi) {
       const float* g0 = gsig + ti[yi][0];
       const float* g1 = gsig + ti[yi][1];
@@ -511,14 +518,19 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
       float sum = 0.f, cnt = 0.f;
 #pragma unroll
       for (int bi = 0; bi < nb; ++bi) {
-        const int o0 = ti[yi][2 + 2 * bi];
-        if (o0 < 0) continue;
-        const int o1 = ti[yi][3 + 2 * bi];
+        const int o0r = ti[yi][2 + 2 * bi];
+        if (__builtin_amdgcn_ballot_w64(o0r >= 0) == 0) continue;
+        const float rw = o0r >= 0 ? 1.f : 0.f;
+        const int o0 = max(o0r, 0), o1 = max(ti[yi][3 + 2 * bi], 0);
         const float tly = tf[yi][1 + bi];
-        for (int cc = 0; cc < ncol; ++cc) {
-          const float* pl = tsl + (bi * 2 + tbj[cc]) * trows * w;
-          sum += sigm_fast(blend(pl[o0 + tx0[cc]], pl[o0 + tx1[cc]], pl[o1 + tx0[cc]], pl[o1 + tx1[cc]], tly, tlx[cc]));
-          cnt += 1.f;
+        const float* p0 = tsl + (bi * 2 + tbj[0]) * trows * w;
+        sum += rw * sigm_fast(blend(p0[o0 + tx0[0]], p0[o0 + tx1[0]], p0[o1 + tx0[0]], p0[o1 + tx1[0]], tly, tlx[0]));
+        cnt += rw;
+        if (two) {
+          const float* p1 = tsl + (bi * 2 + tbj[1]) * trows * w;
+          sum += rw * cw1 *
+                 sigm_fast(blend(p1[o0 + tx0[1]], p1[o0 + tx1[1]], p1[o1 + tx0[1]], p1[o1 + tx1[1]], tly, tlx[1]));
+          cnt += rw * cw1;
         }
       }
       ob[(int64_t)(Y0 + yi) * out_res + X] = (sum * __builtin_amdgcn_rcpf(cnt) + glob) * 0.5f;
