@@ -4,6 +4,7 @@
 //   catseg_upsample_add_rows  x + interpolate(x_pool, align_corners=True) (model.py:415-423)
 //   catseg_sliding_crops      640² resize + Unfold(384, 256) + global 384² (cat_seg_model.py:158-168)
 //   catseg_sliding_merge      interp 384 + sigmoid + Fold/count + global avg (cat_seg_model.py:204-213)
+#include <type_traits>
 #include "common.h"
 #include "capi.h"
 
@@ -479,6 +480,12 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
   const int full = out_res / 256, rem = out_res % 256;
   const int nrow = Y1 - Y0;
   const int ncols = full + (rem ? 1 : 0);
+  bool cov_all[2], cov_none[2];                 // tile row bi covers every / no row of the band
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    cov_all[bi] = Y0 - stride * bi >= 0 && Y1 - 1 - stride * bi < k;
+    cov_none[bi] = Y1 - 1 - stride * bi < 0 || Y0 - stride * bi >= k;
+  }
   for (int c = 0; c < ncols; ++c) {
     int X, ya, yb;
     if (c < full) {
@@ -511,6 +518,53 @@ __global__ __launch_bounds__(256) void sliding_merge_tab_kernel(const float* __r
     if (ncol == 1) { tx0[1] = tx0[0]; tx1[1] = tx1[0]; tlx[1] = tlx[0]; tbj[1] = tbj[0]; }
     const float cw1 = ncol == 2 ? 1.f : 0.f;
     const bool two = __builtin_amdgcn_ballot_w64(ncol == 2) != 0;
+    auto term = [&](int yi, int bi, int cc) {
+      const int o0 = max(ti[yi][2 + 2 * bi], 0), o1 = max(ti[yi][3 + 2 * bi], 0);
+      const float tly = tf[yi][1 + bi];
+      const float* p = tsl + (bi * 2 + tbj[cc]) * trows * w;
+      return sigm_fast(blend(p[o0 + tx0[cc]], p[o0 + tx1[cc]], p[o1 + tx0[cc]], p[o1 + tx1[cc]], tly, tlx[cc]));
+    };
+    auto global = [&](int yi) {
+      const float* g0 = gsig + ti[yi][0];
+      const float* g1 = gsig + ti[yi][1];
+      return blend(g0[gx0], g0[gx1], g1[gx0], g1[gx1], tf[yi][0], glx);
+    };
+    // bands whose rows all share one tile-row coverage (every band at 640 / 384 / 256: the
+    // coverage edges are multiples of the 16-row band) run a row loop with no coverage test;
+    // the others test each row (wave-uniform ballots)
+    auto rows_uniform = [&](auto C0, auto C1, auto TWO) {
+      constexpr bool c0 = decltype(C0)::value, c1 = decltype(C1)::value, tw = decltype(TWO)::value;
+      const float cnt = (float)((c0 ? 1 : 0) + (c1 ? 1 : 0)) * (1.f + (tw ? cw1 : 0.f));
+      const float rc = __builtin_amdgcn_rcpf(cnt);
+#pragma unroll 4
+      for (int yi = ya; yi < yb; ++yi) {
+        const float glob = global(yi);
+        float sum = 0.f;
+        if constexpr (c0) {
+          sum += term(yi, 0, 0);
+          if constexpr (tw) sum += cw1 * term(yi, 0, 1);
+        }
+        if constexpr (c1) {
+          sum += term(yi, 1, 0);
+          if constexpr (tw) sum += cw1 * term(yi, 1, 1);
+        }
+        ob[(int64_t)(Y0 + yi) * out_res + X] = (sum * rc + glob) * 0.5f;
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (cov_all[0] && cov_all[1]) {
+      if (two) rows_uniform(T_{}, T_{}, T_{}); else rows_uniform(T_{}, T_{}, F_{});
+      continue;
+    }
+    if (cov_all[0] && cov_none[1]) {
+      if (two) rows_uniform(T_{}, F_{}, T_{}); else rows_uniform(T_{}, F_{}, F_{});
+      continue;
+    }
+    if (cov_none[0] && cov_all[1]) {
+      if (two) rows_uniform(F_{}, T_{}, T_{}); else rows_uniform(F_{}, T_{}, F_{});
+      continue;
+    }
     for (int yi = ya; yi < yb; ++yi) {
       const float* g0 = gsig + ti[yi][0];
       const float* g1 = gsig + ti[yi][1];
