@@ -317,15 +317,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnP p) {
 // weights and bias), so S = K Q^T is already the exponent in log2 units.  The running max then
 // enters as the MFMA's accumulator input (C = -m), S - m comes out of the matrix pipe, and the
 // softmax is one v_exp per score (no scale / subtract FMA); block 0 seeds the max.
-// PIPE: the block loop software-pipelined one block deep -- block b+1's S MFMAs and softmax are
-// issued before block b's P.V MFMAs, so a wave's exp / pack VALU of one block runs beside the
-// matrix pipe's P.V of the previous one (the 8 waves pass each block's barrier together, so the
-// overlap has to come from within the wave).  A running-max rescale found by block b+1's scores is
-// applied to O after block b's P.V (O = alpha (O + P_b V_b) + ..., the unpipelined order exactly).
-// The ring keeps block b readable while b+1 .. b+1+AHEAD land: NBUF = AHEAD + 3.
-template <int NW, int QT, bool L2S = false, bool PIPE = false, int AHEAD_ = 2>
+template <int NW, int QT, bool L2S = false>
 __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(AttnP p) {   // two workgroups per CU
-  constexpr int D = 64, KB = 64, AHEAD = PIPE ? AHEAD_ : 2, NBUF = PIPE ? AHEAD + 3 : 4;
+  constexpr int D = 64, KB = 64, NBUF = 4, AHEAD = 2;
   constexpr int BLK = 2 * KB * D;                       // elements of one ring slot (K rows, then V rows)
   constexpr int NI = (16 + NW - 1) / NW;                // DMA pieces (1 KiB) per wave per block
   constexpr float THR = 16.f;                           // defer-max threshold (log2 units)
@@ -400,9 +394,6 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   for (int dt = 0; dt < 4; ++dt)
     voff[dt] = KB * D * 2 + vrow * 128 + (((2 * dt + ((col & 3) >> 1)) ^ vswz) << 4) + (col & 1) * 8;
 
-  // PIPE: a rescale found by scores() waits here until the previous block's P.V is in O
-  float alpha_d[QT];
-  bool resc[QT];
   // scores + softmax of block blk -> P fragments (bf16) in pb
   auto scores = [&](int blk, auto tail_tag, s16x8 (&pb)[QT][2]) {
     constexpr bool TAIL = decltype(tail_tag)::value;
@@ -444,19 +435,13 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
       if constexpr (L2S) {
         // st = S - m_run already (block 0: S, with m_run unset); rescale when a query's block max
         // passes the running max by more than THR (block 0: always, to seed it)
-        if constexpr (PIPE) resc[t] = false;
         if (blk == 0 || __any(lm > THR)) {
           const float d = blk == 0 ? xrow4_max(lm) : fmaxf(xrow4_max(lm), 0.f);
           if (blk > 0) {
             const float alpha = __builtin_amdgcn_exp2f(-d);
-            if constexpr (PIPE) {
-              alpha_d[t] = alpha;
-              resc[t] = true;
-            } else {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) o[t][i] *= alpha;
-              osum[t] *= alpha;
-            }
+            for (int i = 0; i < 4; ++i) o[t][i] *= alpha;
+            osum[t] *= alpha;
             m_run[t] += d;
           } else {
             m_run[t] = d;
@@ -469,7 +454,6 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
 #pragma unroll
           for (int r = 0; r < 4; ++r) st[t][kt][r] = __builtin_amdgcn_exp2f(st[t][kt][r]);
       } else {
-      static_assert(!PIPE, "the pipelined block loop is built for mode 2 only");
       if (__any((lm - m_run[t]) * sl2 > THR)) {          // rare after the first block
         const float m_new = fmaxf(m_run[t], xrow4_max(lm));
         const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * sl2);
@@ -530,49 +514,6 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
 #pragma unroll
   for (int b = 0; b <= AHEAD; ++b)
     if (b < nblk) issue(b);
-  if constexpr (PIPE) {
-    // wait for block b (the blocks after it, up to AHEAD of them, may stay in flight), barrier,
-    // then the ring slot of block b - 2 is free: request block b + AHEAD + 1 into it
-    auto land = [&](int b) {
-      const int after = min(AHEAD, nblk - 1 - b);
-      if (after >= 2) wait_vmcnt<2 * NI>();
-      else if (after == 1) wait_vmcnt<NI>();
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (b + AHEAD + 1 < nblk) issue(b + AHEAD + 1);
-    };
-    s16x8 pn[QT][2];
-    land(0);
-    if (live) {
-      if (0 < nfull) scores(0, std::false_type{}, pb);
-      else scores(0, std::true_type{}, pb);
-    }
-    for (int blk = 0; blk < nblk; ++blk) {
-      const bool next = blk + 1 < nblk;
-      if (next) land(blk + 1);
-      if (live) {
-        if (next) {
-          if (blk + 1 < nfull) scores(blk + 1, std::false_type{}, pn);
-          else scores(blk + 1, std::true_type{}, pn);
-        }
-        if (blk < nfull) pv(blk, std::false_type{}, pb);
-        else pv(blk, std::true_type{}, pb);
-        if (next) {
-#pragma unroll
-          for (int t = 0; t < QT; ++t) {
-            if (resc[t]) {
-#pragma unroll
-              for (int i = 0; i < 4; ++i) o[t][i] *= alpha_d[t];
-              osum[t] *= alpha_d[t];
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) pb[t][u] = pn[t][u];
-          }
-        }
-      }
-    }
-  } else
   for (int blk = 0; blk < nblk; ++blk) {
     // this wave's pieces of blocks blk+1 .. min(blk+AHEAD, nblk-1) may stay in flight
     const int after = min(AHEAD, nblk - 1 - blk);
@@ -606,10 +547,10 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
   }
 }
 
-template <int NW, int QT, bool L2S = false, bool PIPE = false, int AHEAD = 2>
+template <int NW, int QT, bool L2S = false>
 void launch_vit3(const AttnP& p, hipStream_t st) {
   dim3 grid((unsigned)((p.L + 16 * NW * QT - 1) / (16 * NW * QT)), (unsigned)(p.n_seq * p.H));
-  hipLaunchKernelGGL((vit_attn3_kernel<NW, QT, L2S, PIPE, AHEAD>), grid, dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((vit_attn3_kernel<NW, QT, L2S>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <typename T, int D, int NW, int KB, int QT, int GEO, bool SWM, bool CAUSAL>
@@ -649,10 +590,10 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
     if constexpr (sizeof(T) != 2) return -1;
     if (head_dim != 64 || p.causal) return -1;
     // (measured and not kept: 10 waves x 16 queries, 512 workgroups in one round, 29.4 vs 27.4 us;
-    // waves 4-7 half a block behind on a 5-slot ring, 29.3 vs 28.1 us)
-    if (g_attn_variant == 1) launch_vit3<8, 1, true, true, 1>(p, st);        // pipelined, 4-slot ring
-    else if (g_attn_variant == 2) launch_vit3<8, 1, true, true, 2>(p, st);   // pipelined, 5-slot ring
-    else launch_vit3<8, 1, true>(p, st);
+    // waves 4-7 half a block behind on a 5-slot ring, 29.3 vs 28.1 us; the block loop software-
+    // pipelined one block deep -- block b+1's S MFMAs and softmax issued before block b's P.V, the
+    // rescale deferred behind it -- on a 4- / 5-slot ring, 28.9 / 28.7 vs 26.9 us)
+    launch_vit3<8, 1, true>(p, st);
     return 0;
   }
   if (p.mode == 1) {

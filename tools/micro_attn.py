@@ -1,8 +1,7 @@
 """Time the dense attention tilings (tuning knob attn_variant) on the ViT-L/14@336 shape
 (8 images x 16 heads x 577 tokens, head_dim 64, bf16) and check them against variant 0.
 usage: python tools/micro_attn.py [variants, default "0,200"]
-variant 200 + v: mode 2 (q pre-scaled by scale * log2(e); the engine's ViT path) with attn_variant v
-(201 / 202: the software-pipelined block loop on a 4- / 5-slot ring)."""
+variant 200: mode 2 (q pre-scaled by scale * log2(e); the engine's ViT path)."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
@@ -10,7 +9,7 @@ import torch
 from cat_seg import ops
 from cat_seg import _lib as L
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "200,201,202").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,200").split(",")]
 B, Lq, H, d = 8, 577, 16, 64
 lib = L.load()
 torch.manual_seed(0)
@@ -25,7 +24,7 @@ def run():
                   head_dim=d, scale=d ** -0.5, mode=mode[0])
 def setv(v):
     mode[0] = 2 if v >= 200 else 0
-    L.tune("attn_variant", v - 200 if v >= 200 else v)
+    L.tune("attn_variant", 0 if v >= 200 else v)
 
 L.tune("attn_variant", 0); run(); ref = out.clone()
 flops = 4 * B * H * Lq * Lq * d
