@@ -35,6 +35,8 @@
 namespace {
 
 constexpr int NT = 256;          // 4 waves
+int g_ring_onebar = 1;           // 1 = the one-barrier-per-chunk rings (OB) where instantiated (default: bit-identical,
+                                 // Up1 fold 365 -> 347 us, the other three decoder convs within 1 %), 0 = two barriers
 int g_ring_persist = 2;          // persistent workgroups over (slice, band) units: 2 = >= 4 units each (bands by that), 1 = one-unit band rule, 0 = one unit per workgroup
 
 struct RingP {
@@ -72,7 +74,12 @@ struct RingGeom {
 // channel block wco of COUT lands at pixel (2y + a, 2x + b) of the 2H x 2W output map.
 // WFIX > 0: the map width as a compile-time constant (UP variants; the per-pixel row / column
 // divisions become multiplies), 0 = p.W
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0>
+// OB: one barrier per chunk -- the rows chunk c+1 adds are written into the ring right after chunk
+// c's epilogue, before the end-of-chunk barrier, into slots chunk c does not read; needs NR >= the
+// rows a chunk spans + the rows the next one adds (the two-barrier form writes them after a barrier
+// that retires chunk c's reads, so NR only has to cover one chunk + its additions in sequence)
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0,
+          bool OB = false>
 __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   constexpr int CPX = C / 8;
   constexpr int PS = RingGeom<C>::PS;
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
     }
 
     // ---- rotate the ring: prefetched rows into the slots the next chunk no longer needs ----
-    __syncthreads();
+    if constexpr (!OB) __syncthreads();
 #pragma unroll
     for (int k = 0; k < MAXPF; ++k)
       if ((pf_code[k] >> 16) < nnew)
@@ -409,7 +416,8 @@ size_t ring_lds(int W, int NR) { return (size_t)NR * RingGeom<C>::pitch(W) * 2 +
 // NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
 // <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
 // adds <= 2 rows (104).
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0>
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0,
+          bool OB = false>
 int launch_ring_t(const RingP& p0, hipStream_t st) {
   RingP p = p0;
   const int nchunks = p.H * p.W / CH;
@@ -433,7 +441,7 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   p.chunks_per_band = (nchunks + bands - 1) / bands;
   static size_t configured = 0;
   if (sh > configured) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX, OB>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     configured = sh;
   }
@@ -443,21 +451,25 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   }
   int64_t grid = p.S * bands * nsplit;
   if (g_ring_persist) grid = std::min(grid, cap);
-  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX>), dim3((unsigned)grid),
+  hipLaunchKernelGGL((conv_ring_kernel<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, ADD, UP, WFIX, OB>), dim3((unsigned)grid),
                      dim3(NT), sh, st, p);
   return 0;
 }
 
 // the CAT-Seg decoder widths (48, 96) get a compile-time width; others run with p.W
-template <int C, int COUT, int WPX, int WCO, int NPOS, int CH = 128, int OCC = 2, int NR = 6>
+template <int C, int COUT, int WPX, int WCO, int NPOS, int CH = 128, int OCC = 2, int NR = 6, bool OB = false>
 int launch_ring(const RingP& p0, hipStream_t st) {
   constexpr int WF = NPOS > 160 ? 96 : 48;      // the width class a variant is sized for
   if (p0.W == WF) {
-    if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true, false, WF>(p0, st);
-    return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false, false, WF>(p0, st);
+    if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true, false, WF, OB>(p0, st);
+    return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false, false, WF, OB>(p0, st);
   }
-  if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true>(p0, st);
-  return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false>(p0, st);
+  if constexpr (OB) {
+    return 1;                                   // the one-barrier rings are sized for their width class only
+  } else {
+    if (p0.add) return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, true>(p0, st);
+    return launch_ring_t<C, COUT, WPX, WCO, NPOS, CH, OCC, NR, false>(p0, st);
+  }
 }
 
 // ---- per-image partial conv (fp32 out): the guidance half of a conv over [x | g] ----
@@ -618,8 +630,14 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
     case 2: return launch_ring<64, 32, 4, 1, 198, 128, 2, 5>(p, st);
     case 3: return launch_ring<48, 32, 4, 1, 156>(p, st);
     case 5: return launch_ring<32, 32, 4, 1, 156>(p, st);
-    case 6: return launch_ring<32, 32, 4, 1, 198, 128, 2, 5>(p, st);
-    case 7: return launch_ring<64, 64, 1, 4, 156>(p, st);
+    case 6:
+      // one barrier per chunk: a 128-pixel chunk spans <= 3 rows of 96 (+2 halo), the next adds <= 2
+      if (g_ring_onebar) return launch_ring<32, 32, 4, 1, 198, 128, 2, 7, true>(p, st);
+      return launch_ring<32, 32, 4, 1, 198, 128, 2, 5>(p, st);
+    case 7:
+      // 128 pixels of 48: <= 4 rows (+2), the next adds <= 3
+      if (g_ring_onebar) return launch_ring<64, 64, 1, 4, 156, 128, 2, 9, true>(p, st);
+      return launch_ring<64, 64, 1, 4, 156>(p, st);
     case 8: return launch_ring<96, 64, 1, 4, 104, 64, 2, 5>(p, st);
     case 9: return launch_ring<48, 32, 4, 1, 198, 128, 2, 5>(p, st);
     default: return 1;
@@ -672,6 +690,7 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
 }
 
 CATSEG_KNOB(g_ring_persist, "ring_persist");
+CATSEG_KNOB(g_ring_onebar, "ring_onebar");
 
 // ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
 // The conv over the ConvTranspose output y (2H x 2W, no nonlinearity between them) equals, per
@@ -741,14 +760,22 @@ extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   // slower, as did 96-pixel chunks and four 16-channel workgroups per parity for the first block)
   int rc;
   if (up2) {
-    if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true, 48>(p, st);
+    // one barrier per chunk: 64 pixels of 48 span <= 3 rows (+2), the next chunk adds <= 2
+    if (g_ring_onebar) {
+      if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 7, true, true, 48, true>(p, st);
+      else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 7, false, true, 48, true>(p, st);
+    } else if (p.add) rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, true, true, 48>(p, st);
     else rc = launch_ring_t<64, 128, 1, 4, 104, 64, 2, 5, false, true, 48>(p, st);
   } else {
     // first Up block (24-wide source, 128 channels): a parity's 64 outputs x 4 taps x 4 k-steps would
     // be 256 weight VGPRs per wave, so two workgroups split them (32 each, the source ring read by
     // both); a 64-pixel chunk spans <= 4 rows (6-row ring) and adds <= 3 (78 positions)
     p.up_split = 2;
-    if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true, 24>(p, st);
+    // one barrier per chunk: 64 pixels of 24 span <= 4 rows (+2), the next chunk adds <= 3
+    if (g_ring_onebar) {
+      if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 9, true, true, 24, true>(p, st);
+      else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 9, false, true, 24, true>(p, st);
+    } else if (p.add) rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, true, true, 24>(p, st);
     else rc = launch_ring_t<128, 128, 1, 4, 78, 64, 1, 6, false, true, 24>(p, st);
   }
   if (rc != 0) return rc;

@@ -596,6 +596,16 @@ def test_conv3x3_ring_guidance_split(c1, c2, co, H):
     got = out.reshape(S, H, W, co).permute(0, 3, 1, 2).double().cpu()
     err = (got - ref).abs() - 2.0 ** -8 * ref.abs()
     assert err.max().item() <= 1e-5, err.max().item()
+    # the one-barrier-per-chunk rings (tuning knob ring_onebar 1, default) equal the two-barrier form bit for bit
+    L.load()
+    out1, st1 = torch.empty_like(out), torch.empty_like(st)
+    try:
+        L.tune("ring_onebar", 0)
+        ops.conv3x3(a1, wc, out1, stats=st1, **kw)
+        torch.cuda.synchronize()
+    finally:
+        L.tune("ring_onebar", 1)
+    assert torch.equal(out1, out) and torch.equal(st1, st)
     mean = torch.empty(S * (co // 16), device=dev)
     rstd = torch.empty_like(mean)
     ops.groupnorm_stats(st, S, tiles, co // 16, tile * 16, mean, rstd)
@@ -1133,6 +1143,17 @@ def test_upconv3x3_folded_convtranspose(ci, m, cg, co, H, gn_src):
     err = (got - ref).abs()
     assert err.max().item() <= 2e-2 + 2 ** -7 * ref.abs().max().item(), err.max().item()
     assert err.mean().item() <= 2e-3, err.mean().item()
+    # the one-barrier-per-chunk ring (tuning knob ring_onebar 1, default) equals the two-barrier form bit for bit
+    L.load()
+    out1, st1 = torch.empty_like(out), torch.empty_like(st)
+    try:
+        L.tune("ring_onebar", 0)
+        ops.upconv3x3(z.permute(0, 2, 3, 1).contiguous().to(dev, dt), comp.to(dev, dt), out1, S=S, H=H, W=H, c1=ci,
+                      gn=gn, stats=st1, addend=part, addend_div=T)
+        torch.cuda.synchronize()
+    finally:
+        L.tune("ring_onebar", 1)
+    assert torch.equal(out1, out) and torch.equal(st1, st)
     mean1 = torch.empty(S * (co // 16), device=dev)
     rstd1 = torch.empty_like(mean1)
     ops.groupnorm_stats(st, S, ntl, co // 16, tile * 16, mean1, rstd1)

@@ -2,7 +2,7 @@
 one tuning knob, interleaved in one process, and check each value's outputs against the first's
 bit for bit: Up1 fold (24x24x128 -> 4 parities x 64), Up1 conv2 (48x48, 64 -> 64, GN+ReLU in),
 Up2 fold (relu(GN(48x48x64)) -> 4 x 32), Up2 conv2 (96x96, 32 -> 32, GN+ReLU in).
-usage: python tools/micro_decoder.py ring_persist 0 1"""
+usage: python tools/micro_decoder.py ring_onebar 0 1"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
