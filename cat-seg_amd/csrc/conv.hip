@@ -578,6 +578,8 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 constexpr int HT_W = 96, HT_TPR = HT_W / 16, HT_NR = 6, HT_WP = HT_W + 8;
 constexpr int HT_TPS = 2 * HT_TPR / 4;      // 16-pixel tiles per wave per step (two rows, 4 waves)
 
+// PD: input steps in flight (registers) ahead of the one being computed
+template <int PD>
 __global__ __launch_bounds__(256) void head_tap_kernel(const bf16* __restrict__ x, int Tn, int H, const float* __restrict__ w,
                                                        float bias, const float* mean, const float* rstd,
                                                        const float* gamma, const float* beta, int cpg,
@@ -624,13 +626,15 @@ __global__ __launch_bounds__(256) void head_tap_kernel(const bf16* __restrict__ 
         v[j] = ld16(xs + ((int64_t)(in ? yy : 0) * HT_W + xx) * C + 8 * g);
       }
     };
-    uint4 cur[HT_TPS], nxt[HT_TPS];
+    uint4 cur[HT_TPS], nxt[HT_TPS], nn[HT_TPS];
     load(0, cur);
+    if (PD > 1 && 1 < nsteps) load(1, nxt);
     const int b = s / Tn, t = s - b * Tn;
     const int cls = classes ? classes[(int64_t)b * Tn + t] : t;
     float* o = out + ((int64_t)b * Tout + cls) * HW;
     for (int k = 0; k < nsteps; ++k) {
-      if (k + 1 < nsteps) load(k + 1, nxt);
+      if (PD == 1 && k + 1 < nsteps) load(k + 1, nxt);
+      if (PD > 1 && k + 2 < nsteps) load(k + 2, nn);
 #pragma unroll
       for (int j = 0; j < HT_TPS; ++j) {
         const int tile = wave * HT_TPS + j, i = 2 * k + tile / HT_TPR, yy = y0 - 1 + i;
@@ -659,14 +663,18 @@ __global__ __launch_bounds__(256) void head_tap_kernel(const bf16* __restrict__ 
         o[(int64_t)yy * HT_W + xx] = acc;
       }
 #pragma unroll
-      for (int j = 0; j < HT_TPS; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < HT_TPS; ++j) {
+        cur[j] = nxt[j];
+        if (PD > 1) nxt[j] = nn[j];
+      }
     }
     __syncthreads();                                 // the ring is rewritten by the next unit
   }
 }
 
-// 0 = MFMA tap-product kernel at W = 96 (head_tap_kernel), 1 = the v_dot2c band kernel with the
-// compile-time width 96, 2 = the band kernel with a runtime width
+// 0 = MFMA tap-product kernel at W = 96 (head_tap_kernel, two input steps in flight), 1 = the v_dot2c
+// band kernel with the compile-time width 96, 2 = the band kernel with a runtime width, 3 = the tap
+// kernel with one input step in flight
 int g_head_variant = 0;
 
 }  // namespace
@@ -771,14 +779,20 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       configured = true;
     }
-    if (W == 96 && g_head_variant == 0) {
+    if (W == 96 && (g_head_variant == 0 || g_head_variant == 3)) {
       const int n_cu = catseg_device_cus();
       const int RB = 24, ups = (H + RB - 1) / RB;
       const int64_t nunits = B * (int64_t)T * ups;
       CATSEG_CHECK(nunits < (1LL << 31), "conv3x3_head: too many bands");
+      // four workgroups per CU (six measured slower: 189-193 vs 171 us); two input steps in flight
+      // (one: 178-180 us, variant 3)
       const unsigned grid = (unsigned)std::min<int64_t>(nunits, 4LL * n_cu);
-      hipLaunchKernelGGL(head_tap_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, T, H, weight, bias,
-                         mean, rstd, gamma, beta, cpg, classes, T_out, out, RB, ups, (int)nunits);
+      if (g_head_variant == 3)
+        hipLaunchKernelGGL(head_tap_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, T, H, weight,
+                           bias, mean, rstd, gamma, beta, cpg, classes, T_out, out, RB, ups, (int)nunits);
+      else
+        hipLaunchKernelGGL(head_tap_kernel<2>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, T, H, weight,
+                           bias, mean, rstd, gamma, beta, cpg, classes, T_out, out, RB, ups, (int)nunits);
     } else if (W == 96 && g_head_variant != 2) {
       static bool configured96 = false;
       if (!configured96) {

@@ -619,10 +619,33 @@ __global__ __launch_bounds__(256) void post_sep_kernel(const float* lg, int h, i
   float* sgm = smem;
   float* hr = smem + ((nrows * cw + 3) & ~3);
   const float* src = lg + pl * (int64_t)h * w;
-  for (int i = threadIdx.x; i < nrows * cw; i += 256) {
-    const int r = i / cw, c = i - r * cw;
-    const float v = src[(int64_t)(ya + r) * w + c];
-    sgm[i] = SIG ? 1.f / (1.f + __expf(-v)) : v;
+  if (cw == w && (w & 3) == 0) {
+    // the band's source rows are one contiguous run: 16-byte loads, all of a thread's issued
+    // before the first LDS write (one round trip per band instead of one per loop trip)
+    const float4* s4 = reinterpret_cast<const float4*>(src + (int64_t)ya * w);
+    const int n4 = nrows * cw / 4;
+    constexpr int B4 = 4;
+    for (int base = 0; base < n4; base += 256 * B4) {
+      float4 v[B4];
+#pragma unroll
+      for (int m = 0; m < B4; ++m) v[m] = s4[min(base + (int)threadIdx.x + 256 * m, n4 - 1)];
+#pragma unroll
+      for (int m = 0; m < B4; ++m) {
+        const int i = base + (int)threadIdx.x + 256 * m;
+        if (i < n4) {
+          float e[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) e[k] = SIG ? 1.f / (1.f + __expf(-e[k])) : e[k];
+          *reinterpret_cast<float4*>(sgm + 4 * i) = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < nrows * cw; i += 256) {
+      const int r = i / cw, c = i - r * cw;
+      const float v = src[(int64_t)(ya + r) * w + c];
+      sgm[i] = SIG ? 1.f / (1.f + __expf(-v)) : v;
+    }
   }
   __syncthreads();
   const int W4 = W >> 2;

@@ -1209,7 +1209,7 @@ def test_head_conv_band(H, W):
     cls = torch.tensor([[0, 2, 4], [1, 3, 0]], dtype=torch.int32).to(dev)
     outs = {}
     try:
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             L.tune("head_variant", v)
             logits = torch.full((B, T + 2, H, W), -100.0, device=dev)
             ops.conv3x3_head(xin, B=B, T=T, H=H, W=W, C=C, weight=hw_[0].permute(1, 2, 0).reshape(-1).contiguous().to(dev),
@@ -1218,6 +1218,7 @@ def test_head_conv_band(H, W):
             outs[v] = logits.cpu()
     finally:
         L.tune("head_variant", 0)
+    assert torch.equal(outs[3], outs[0])     # tap kernel with one input step in flight instead of two
     for v in (0, 1):
         for bi in range(B):
             for t in range(T):
