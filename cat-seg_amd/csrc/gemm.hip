@@ -38,6 +38,7 @@ struct EpiArgs {
   void* out; int64_t ldo;
   int store_mode; int cvt_k, cvt_hin, cvt_win, cvt_cout;
   const float* sa; const float* sw;   // fp8 path: per-row scales of A and W (dequant in the epilogue)
+  int pf;                             // gemm3 lean epilogue: next round's residual in flight (g_epi_prefetch)
 };
 
 template <typename TO>
@@ -424,6 +425,10 @@ struct Swz {
 // (unit scales; fp8 rate = 2x bf16) consumes two 16-byte chunks per lane; A and W fragments
 // read the same chunks, so the k order inside the instruction does not matter.  The
 // epilogue multiplies by sa[m] * sw[n] (per-row dequant scales) before bias / act / residual.
+// 1 (default) = the lean one-item-per-thread epilogue with the next round's residual in flight and the
+// bias loaded once (same box, M = 4616: out-proj 20.8 -> 19.9 us, fc1 55.1 -> 52.7, fc2 48.3 -> 47.1;
+// bit-identical); 0 = one residual round trip per epilogue round
+int g_epi_prefetch = 1;
 template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false,
           int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
@@ -568,6 +573,60 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   float* stg = reinterpret_cast<float*>(smem);
   const int col = lane & 15, rq = (lane >> 4) * 4;
   const int wmi = wave % WGM;
+  // lean epilogues with one output item per thread per round (the 160 x 128 / 224 x 256 tiles): the
+  // bias of the thread's 8 columns is loaded once, and the residual rows of round h + 1 are
+  // requested before round h's barrier, so no round waits for its own global loads (the loop
+  // below issues them inside each round: one HBM round trip per round, ~5 rounds per tile)
+  constexpr bool ONE = ROWS * (BN / 8) == NT3 && EPI != 0 && !F8 && !SC;
+  if constexpr (ONE) {
+    if (e.pf) {
+      const int lrow = tid / (BN / 8), c8 = (tid % (BN / 8)) * 8;
+      const int wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
+      const int64_t n = n0 + c8;
+      float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (e.bias) load8f(e.bias + n, b);
+      auto mrow = [&](int h) { return m0 + wi * WM + (h * JR + jj) * 16 + rr; };
+      const bool res = EPI == 1 && e.res;
+      float rc[8], rn[8];
+      auto ldres = [&](int h, float (&r)[8]) {
+        if (res) load8f(reinterpret_cast<const TO*>(e.res) + std::min<int64_t>(mrow(h), M - 1) * e.ld_res + n, r);
+      };
+      ldres(0, rc);
+#pragma unroll
+      for (int h = 0; h < FM / JR; ++h) {
+        if (h + 1 < FM / JR) ldres(h + 1, rn);
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int j2 = 0; j2 < JR; ++j2)
+#pragma unroll
+          for (int i = 0; i < FN; ++i)
+            *reinterpret_cast<f32x4*>(&stg[((wmi * JR + j2) * 16 + col) * SLD + wn + 16 * i + rq]) = acc[i][h * JR + j2];
+        __syncthreads();
+        const int64_t m = mrow(h);
+        if (m < M) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]);
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (e.bias) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] += b[r];
+          }
+          if constexpr (EPI == 2) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = apply_act(v[r], ACT_QUICKGELU);
+          }
+          if (res) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] += rc[r];
+          }
+          store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) rc[r] = rn[r];
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int h = 0; h < FM / JR; ++h) {
     __builtin_amdgcn_s_barrier();
@@ -610,6 +669,7 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
   e.cvt_cout = g->cvt_cout;
   e.sa = nullptr; e.sw = nullptr;
+  e.pf = g_epi_prefetch;
   return e;
 }
 
@@ -791,6 +851,7 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
 
 CATSEG_KNOB(g_gemm_variant, "gemm_variant");
 CATSEG_KNOB(g_gemm_group, "gemm_group");
+CATSEG_KNOB(g_epi_prefetch, "epi_prefetch");
 CATSEG_KNOB(g_gemm_f8_variant, "gemm_fp8_variant");
 
 extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {

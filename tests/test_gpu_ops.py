@@ -108,6 +108,35 @@ def test_gemm_convtranspose_store_pipelined(cout, k):
     close(got, ref, atol=2e-2, rtol=1e-2, what=f"convT pipelined cout {cout} k {k}")
 
 
+@pytest.mark.parametrize("variant", [0, 15, 17, 24])
+def test_gemm_epilogue_prefetch(variant):
+    """The lean gemm3 epilogue with the next round's residual rows in flight and the bias loaded once
+    (tuning knob epi_prefetch 1, the default) equals the per-round form (0) bit for bit: bias + fp32 residual (out-proj /
+    fc2) and bias + QuickGELU to bf16 (fc1), ragged M."""
+    M, K, N = 1210, 512, 512
+    A = rnd(M, K, seed=44).to(dev, torch.bfloat16)
+    W = (rnd(N, K, seed=45) / math.sqrt(K)).to(dev, torch.bfloat16)
+    b = rnd(N, seed=46).to(dev)
+    res = rnd(M, N, seed=47).to(dev)
+    lib = L.load()
+    outs = {}
+    try:
+        L.tune("gemm_variant", variant)
+        for pf in (0, 1):
+            L.tune("epi_prefetch", pf)
+            o1 = torch.full((M, N), float("nan"), device=dev)
+            ops.gemm(A, W, o1, bias=b, res=res)
+            o2 = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+            ops.gemm(A, W, o2, bias=b, act=L.ACT_QUICKGELU)
+            torch.cuda.synchronize()
+            outs[pf] = (o1, o2)
+    finally:
+        L.tune("gemm_variant", 0)
+        L.tune("epi_prefetch", 1)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert not torch.isnan(outs[1][0]).any()
+
+
 @pytest.mark.parametrize("variant", [1, 15, 17, 19, 20, 24])
 def test_gemm_pipelined_variants(variant):
     """Every LDS-DMA pipelined bf16 tile (gemm.hip gemm3_kernel) against fp64: ragged M

@@ -12,7 +12,8 @@ from cat_seg import ops
 from cat_seg import _lib as L
 
 variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").split(",")]
-# variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (tuning knob gemm_group)
+# variants >= 1000: automatic tile, tile order grouped by (v - 1000) m-tiles (tuning knob gemm_group);
+# >= 2000: variant v - 2000 with the prefetching lean epilogue (tuning knob epi_prefetch)
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True),
@@ -40,6 +41,10 @@ for name, (N, K, act, has_res) in shapes.items():
     def run():
         ops.gemm(A, W, out, bias=bias, act=act, res=R)
     def setv(v):
+        pf = v >= 2000                 # 2000 + v: variant v with the prefetching lean epilogue (epi_prefetch 1,
+                                       # the library default); v < 2000 runs with epi_prefetch 0
+        v = v - 2000 if pf else v
+        L.tune("epi_prefetch", 1 if pf else 0)
         L.tune("gemm_variant", 0 if v >= 1000 else v)
         L.tune("gemm_group", v - 1000 if v >= 1000 else 0)
     for v in variants:
