@@ -573,23 +573,34 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   float* stg = reinterpret_cast<float*>(smem);
   const int col = lane & 15, rq = (lane >> 4) * 4;
   const int wmi = wave % WGM;
-  // lean epilogues with one output item per thread per round (the 160 x 128 / 224 x 256 tiles): the
+  // lean epilogues with one or two output items per thread per round (160 x 128, 96 x 128, 224 x 256): the
   // bias of the thread's 8 columns is loaded once, and the residual rows of round h + 1 are
   // requested before round h's barrier, so no round waits for its own global loads (the loop
   // below issues them inside each round: one HBM round trip per round, ~5 rounds per tile)
-  constexpr bool ONE = ROWS * (BN / 8) == NT3 && EPI != 0 && !F8 && !SC;
+  // IPT = output items per thread per round; every item of a thread has the same 8 columns
+  constexpr int IPT = ROWS * (BN / 8) / NT3;
+  constexpr bool ONE = IPT >= 1 && IPT <= 2 && ROWS * (BN / 8) == IPT * NT3 && NT3 % (BN / 8) == 0 && EPI != 0 &&
+                       !F8 && !SC;
   if constexpr (ONE) {
     if (e.pf) {
-      const int lrow = tid / (BN / 8), c8 = (tid % (BN / 8)) * 8;
-      const int wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
+      const int c8 = (tid % (BN / 8)) * 8;
       const int64_t n = n0 + c8;
       float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (e.bias) load8f(e.bias + n, b);
-      auto mrow = [&](int h) { return m0 + wi * WM + (h * JR + jj) * 16 + rr; };
+      auto lrow_of = [&](int k) { return (tid + k * NT3) / (BN / 8); };
+      auto mrow = [&](int h, int k) {
+        const int lrow = lrow_of(k);
+        const int wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
+        return m0 + wi * WM + (h * JR + jj) * 16 + rr;
+      };
       const bool res = EPI == 1 && e.res;
-      float rc[8], rn[8];
-      auto ldres = [&](int h, float (&r)[8]) {
-        if (res) load8f(reinterpret_cast<const TO*>(e.res) + std::min<int64_t>(mrow(h), M - 1) * e.ld_res + n, r);
+      float rc[IPT][8], rn[IPT][8];
+      auto ldres = [&](int h, float (&r)[IPT][8]) {
+        if (res) {
+#pragma unroll
+          for (int k = 0; k < IPT; ++k)
+            load8f(reinterpret_cast<const TO*>(e.res) + std::min<int64_t>(mrow(h, k), M - 1) * e.ld_res + n, r[k]);
+        }
       };
       ldres(0, rc);
 #pragma unroll
@@ -602,27 +613,33 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
           for (int i = 0; i < FN; ++i)
             *reinterpret_cast<f32x4*>(&stg[((wmi * JR + j2) * 16 + col) * SLD + wn + 16 * i + rq]) = acc[i][h * JR + j2];
         __syncthreads();
-        const int64_t m = mrow(h);
-        if (m < M) {
-          const f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]);
-          const f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]);
-          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (e.bias) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] += b[r];
-          }
-          if constexpr (EPI == 2) {
+        for (int k = 0; k < IPT; ++k) {
+          const int lrow = lrow_of(k);
+          const int64_t m = mrow(h, k);
+          if (m < M) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]);
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (e.bias) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = apply_act(v[r], ACT_QUICKGELU);
-          }
-          if (res) {
+              for (int r = 0; r < 8; ++r) v[r] += b[r];
+            }
+            if constexpr (EPI == 2) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] += rc[r];
+              for (int r = 0; r < 8; ++r) v[r] = apply_act(v[r], ACT_QUICKGELU);
+            }
+            if (res) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] += rc[k][r];
+            }
+            store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
           }
-          store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
         }
 #pragma unroll
-        for (int r = 0; r < 8; ++r) rc[r] = rn[r];
+        for (int k = 0; k < IPT; ++k)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) rc[k][r] = rn[k][r];
       }
       return;
     }

@@ -108,7 +108,7 @@ def test_gemm_convtranspose_store_pipelined(cout, k):
     close(got, ref, atol=2e-2, rtol=1e-2, what=f"convT pipelined cout {cout} k {k}")
 
 
-@pytest.mark.parametrize("variant", [0, 15, 17, 24])
+@pytest.mark.parametrize("variant", [0, 15, 17, 20, 24])
 def test_gemm_epilogue_prefetch(variant):
     """The lean gemm3 epilogue with the next round's residual rows in flight and the bias loaded once
     (tuning knob epi_prefetch 1, the default) equals the per-round form (0) bit for bit: bias + fp32 residual (out-proj /
