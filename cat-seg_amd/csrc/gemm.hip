@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   // IPT = output items per thread per round; every item of a thread has the same 8 columns
   constexpr int IPT = ROWS * (BN / 8) / NT3;
   constexpr bool ONE = IPT >= 1 && IPT <= 2 && ROWS * (BN / 8) == IPT * NT3 && NT3 % (BN / 8) == 0 && EPI != 0 &&
-                       !F8 && !SC;
+                       !SC;
   if constexpr (ONE) {
     if (e.pf) {
       const int c8 = (tid % (BN / 8)) * 8;
@@ -595,17 +595,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
       };
       const bool res = EPI == 1 && e.res;
       float rc[IPT][8], rn[IPT][8];
-      auto ldres = [&](int h, float (&r)[IPT][8]) {
-        if (res) {
+      // F8: the per-column dequant scales once, the per-row scale of each item with its residual
+      float wsc[8];
+      float sc[IPT], sn[IPT];
+      if constexpr (F8) load8f(e.sw + n, wsc);
+      auto ldres = [&](int h, float (&r)[IPT][8], float (&sr)[IPT]) {
 #pragma unroll
-          for (int k = 0; k < IPT; ++k)
-            load8f(reinterpret_cast<const TO*>(e.res) + std::min<int64_t>(mrow(h, k), M - 1) * e.ld_res + n, r[k]);
+        for (int k = 0; k < IPT; ++k) {
+          const int64_t m = std::min<int64_t>(mrow(h, k), M - 1);
+          if (res) load8f(reinterpret_cast<const TO*>(e.res) + m * e.ld_res + n, r[k]);
+          if constexpr (F8) sr[k] = e.sa[ident ? m : rowmap(amap, m)];
         }
       };
-      ldres(0, rc);
+      ldres(0, rc, sc);
 #pragma unroll
       for (int h = 0; h < FM / JR; ++h) {
-        if (h + 1 < FM / JR) ldres(h + 1, rn);
+        if (h + 1 < FM / JR) ldres(h + 1, rn, sn);
         __builtin_amdgcn_s_barrier();
 #pragma unroll
         for (int j2 = 0; j2 < JR; ++j2)
@@ -621,6 +626,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
             const f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8]);
             const f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lrow * SLD + c8 + 4]);
             float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if constexpr (F8) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] = v[r] * (wsc[r] * sc[k]);
+            }
             if (e.bias) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) v[r] += b[r];
@@ -637,9 +646,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
           }
         }
 #pragma unroll
-        for (int k = 0; k < IPT; ++k)
+        for (int k = 0; k < IPT; ++k) {
 #pragma unroll
           for (int r = 0; r < 8; ++r) rc[k][r] = rn[k][r];
+          sc[k] = sn[k];
+        }
       }
       return;
     }
@@ -702,14 +713,14 @@ bool launch3(const CatsegGemmArgs* g, hipStream_t st) {
 }
 
 // fp8: g's K / lda / ldw are in fp8 elements (bytes); the kernel sees 2-byte units
-template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK>
+template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, int EPI = 0>
 bool launch3f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStream_t st) {
   if (g->N % BN != 0 || (g->K / 2) % BK != 0) return false;
   EpiArgs e = make_epi(g);
   e.sa = sa; e.sw = sw;
   RowMap am{g->amap.d1, g->amap.m1, g->amap.s1, g->amap.d2, g->amap.m2, g->amap.s2, g->amap.off};
   const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
-  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, true>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN),
+  hipLaunchKernelGGL((gemm3_kernel<TO, BM, BN, WGM, WGN, S, BK, true, false, EPI>), dim3((unsigned)(tm * tn)), dim3(64 * WGM * WGN),
                      0, st, (const bf16*)g->A, g->lda / 2, am, (const bf16*)g->W, g->ldw / 2, g->M, g->K / 2, tn, e,
                      g_gemm_group);
   return true;
@@ -851,6 +862,15 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
     else if (g->N % 128 == 0 && g->K % 128 == 0) v = 19;
     else return false;
   }
+  // lean epilogues (bias / bias + residual, bias + QuickGELU) for the automatic tiles, as in try_gemm3
+  const bool plain = !g->add && !g->res2 && g->alpha == 1.f;
+  const int epi = plain && g->act == ACT_NONE ? 1 : plain && g->act == ACT_QUICKGELU && !g->res ? 2 : 0;
+  if (epi == 1 && v == 15) return launch3f8<TO, 160, 128, 2, 4, 2, 128, 1>(g, sa, sw, st);
+  if (epi == 1 && v == 17) return launch3f8<TO, 160, 128, 2, 4, 2, 64, 1>(g, sa, sw, st);
+  if (epi == 1 && v == 20) return launch3f8<TO, 224, 256, 2, 4, 2, 64, 1>(g, sa, sw, st);
+  if (epi == 2 && v == 15) return launch3f8<TO, 160, 128, 2, 4, 2, 128, 2>(g, sa, sw, st);
+  if (epi == 2 && v == 17) return launch3f8<TO, 160, 128, 2, 4, 2, 64, 2>(g, sa, sw, st);
+  if (epi == 2 && v == 20) return launch3f8<TO, 224, 256, 2, 4, 2, 64, 2>(g, sa, sw, st);
   switch (v) {
     case 1: return launch3f8<TO, 256, 256, 2, 4, 2, 64>(g, sa, sw, st);
     case 15: return launch3f8<TO, 160, 128, 2, 4, 2, 128>(g, sa, sw, st);

@@ -251,6 +251,38 @@ def test_gemm_fp8_variants(variant):
         L.tune("gemm_fp8_variant", 0)
 
 
+@pytest.mark.parametrize("variant", [15, 17, 20])
+def test_gemm_fp8_epilogue_prefetch(variant):
+    """fp8 GEMM with the lean prefetching epilogue (per-column scales once, per-row scale and fp32
+    residual of the next round in flight; epi_prefetch 1, default) == the per-round form, bit for bit,
+    with a CLS-dropping row map: bias + residual and bias + QuickGELU."""
+    B, L_, K, N = 3, 401, 1024, 768
+    M = B * (L_ - 1)
+    qa, sa = _quant_ref(rnd(B * L_, K, seed=54))
+    qw, sw = _quant_ref(rnd(N, K, seed=55) / math.sqrt(K))
+    b = rnd(N, seed=56).to(dev)
+    res = rnd(M, N, seed=57).to(dev)
+    amap = rowmap(d1=L_ - 1, s1=L_, d2=1, m2=L_ - 1, s2=1, off=1)
+    lib = L.load()
+    outs = {}
+    try:
+        L.tune("gemm_fp8_variant", variant)
+        for pf in (0, 1):
+            L.tune("epi_prefetch", pf)
+            o1 = torch.full((M, N), float("nan"), device=dev)
+            ops.gemm_fp8(qa.to(dev), sa.to(dev), qw.to(dev), sw.to(dev), o1, M=M, bias=b, res=res, amap=amap)
+            o2 = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+            ops.gemm_fp8(qa.to(dev), sa.to(dev), qw.to(dev), sw.to(dev), o2, M=M, bias=b, act=L.ACT_QUICKGELU,
+                         amap=amap)
+            torch.cuda.synchronize()
+            outs[pf] = (o1, o2)
+    finally:
+        L.tune("gemm_fp8_variant", 0)
+        L.tune("epi_prefetch", 1)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert not torch.isnan(outs[1][0]).any()
+
+
 def test_gemm_fp8_vit_shapes_vs_bf16():
     """The ViT-L/14 block shapes (M = 8 x 577) through the automatic fp8 tile choice: the
     dequantized-operand product to fp32 accuracy, and within e4m3 error of the bf16 GEMM."""
