@@ -254,8 +254,9 @@ def test_gemm_fp8_variants(variant):
 @pytest.mark.parametrize("variant", [15, 17, 20])
 def test_gemm_fp8_epilogue_prefetch(variant):
     """fp8 GEMM with the lean prefetching epilogue (per-column scales once, per-row scale and fp32
-    residual of the next round in flight; epi_prefetch 1, default) == the per-round form, bit for bit,
-    with a CLS-dropping row map: bias + residual and bias + QuickGELU."""
+    residual of the next round in flight; epi_prefetch 1, default) vs the per-round form, with a
+    CLS-dropping row map: bias + residual and bias + QuickGELU.  The dequant multiply and the bias add
+    may contract into one FMA in one form and not the other: an ulp of the fp32 result."""
     B, L_, K, N = 3, 401, 1024, 768
     M = B * (L_ - 1)
     qa, sa = _quant_ref(rnd(B * L_, K, seed=54))
@@ -279,7 +280,10 @@ def test_gemm_fp8_epilogue_prefetch(variant):
     finally:
         L.tune("gemm_fp8_variant", 0)
         L.tune("epi_prefetch", 1)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    d1 = (outs[0][0] - outs[1][0]).abs()                  # O(1) values: a few fp32 ulps of the sum
+    assert d1.max().item() <= 4e-6, d1.max().item()
+    d2 = (outs[0][1].float() - outs[1][1].float()).abs()
+    assert d2.max().item() <= 2 ** -7 * outs[0][1].float().abs().max().item()     # a bf16 ulp at most
     assert not torch.isnan(outs[1][0]).any()
 
 
