@@ -592,7 +592,8 @@ int dispatch(const AttnP& p, int head_dim, hipStream_t st) {
     // (measured and not kept: 10 waves x 16 queries, 512 workgroups in one round, 29.4 vs 27.4 us;
     // waves 4-7 half a block behind on a 5-slot ring, 29.3 vs 28.1 us; the block loop software-
     // pipelined one block deep -- block b+1's S MFMAs and softmax issued before block b's P.V, the
-    // rescale deferred behind it -- on a 4- / 5-slot ring, 28.9 / 28.7 vs 26.9 us)
+    // rescale deferred behind it -- on a 4- / 5-slot ring, 28.9 / 28.7 vs 26.9 us; 9 waves x 16
+    // queries, so that 576 of the 577 queries fill four workgroups per (image, head): 27.0 vs 27.0 us)
     launch_vit3<8, 1, true>(p, st);
     return 0;
   }
