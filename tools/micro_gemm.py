@@ -42,7 +42,9 @@ for name, (N, K, act, has_res) in shapes.items():
         ops.gemm(A, W, out, bias=bias, act=act, res=R)
     def setv(v):
         pf = v >= 2000                 # 2000 + v: variant v with the prefetching lean epilogue (epi_prefetch 1,
-                                       # the library default); v < 2000 runs with epi_prefetch 0
+                                       # the library default); v < 2000 runs with epi_prefetch 0;
+                                       # 3000 + g = 2000 + (1000 + g): the automatic tile, prefetching
+                                       # epilogue, tile-order group g
         v = v - 2000 if pf else v
         L.tune("epi_prefetch", 1 if pf else 0)
         L.tune("gemm_variant", 0 if v >= 1000 else v)
