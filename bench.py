@@ -261,7 +261,7 @@ def main():
 
     roofline, kernels = None, None
     if rank == 0 and not args.no_roofline:
-        roofline, kernels = roofline_pass(step, stream, dtype, vit_fp8)
+        roofline, kernels = roofline_pass(step, stream, dtype, vit_fp8, args.config)
     cpu = None
     n_cpu = B if args.cpu_images < 0 else args.cpu_images
     if rank == 0 and world == 1 and n_cpu > 0:
@@ -317,10 +317,12 @@ def _version_key(path):
     return tuple(nums)
 
 
-def pmc_traffic(family):
+def pmc_traffic(family, bench_config=3):
     """HBM bytes per launch of `family` from a committed PMC summary (profiles/**/pmc_traffic.json,
     written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes;
-    FETCH_SIZE doubled per the gfx950 note).  Prefers the newest summary recorded for this exact
+    FETCH_SIZE doubled per the gfx950 note).  Only summaries taken on the same bench configuration
+    count (tools/pmc_step.py runs the headline, config 3: a config-4 GEMM at M = 2308 moves other
+    bytes than the headline's at M = 4616).  Prefers the newest summary recorded for this exact
     kernel build (lib_sha16 of the loaded libcatseg_hip.so), else the newest by round / version
     number.  Returns (bytes, source, same_build)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True),
@@ -329,6 +331,9 @@ def pmc_traffic(family):
         return None, None, False
     sha = lib_sha16()
     docs = [(f, json.load(open(f))) for f in files]
+    docs = [(f, d) for f, d in docs if d.get("bench_config", 3) == bench_config]
+    if not docs:
+        return None, None, False
     same = [(f, d) for f, d in docs if d.get("lib_sha16") == sha]
     f, d = (same or docs)[-1]
     fam = d["families"].get(family)
@@ -337,7 +342,7 @@ def pmc_traffic(family):
     return fam["traffic_bytes_per_launch"], os.path.relpath(f, ROOT), bool(same)
 
 
-def roofline_pass(step, stream, dtype, vit_fp8=False):
+def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
     """One eager pass with HIP events around every wrapped launch (on the launch stream)."""
     ops.PROFILE = []
     with torch.no_grad(), torch.cuda.stream(stream):
@@ -356,7 +361,7 @@ def roofline_pass(step, stream, dtype, vit_fp8=False):
     top = max(agg, key=lambda k: agg[k]["ms"])
     a = agg[top]
     avg_s = a["ms"] / a["launches"] / 1e3
-    traffic, tsrc, tsame = pmc_traffic(top)
+    traffic, tsrc, tsame = pmc_traffic(top, bench_config)
     common = {"launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2), "traffic": traffic,
               "traffic_source": tsrc, "traffic_same_build": tsame, "lib_sha16": lib_sha16()}
     if a["flops"] > 0:

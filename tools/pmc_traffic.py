@@ -70,7 +70,8 @@ def main():
     sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
     head = sys.argv[sys.argv.index("--head") + 1] if "--head" in sys.argv else None
     if out:
-        json.dump({"lib_sha16": sha, "git_head": head, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/pmc_step.py "
+        json.dump({"lib_sha16": sha, "git_head": head, "bench_config": 3,
+                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/pmc_step.py "
                              "(one L/14@336 T=150 bs=8 bf16 forward, eager); fetch = 2 x FETCH_SIZE",
                    "families": res}, open(out, "w"), indent=1)
 
