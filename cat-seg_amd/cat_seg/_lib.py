@@ -138,6 +138,7 @@ _SIGS = {
     "catseg_conv3x3_partial": [vp, i64, i32, i32, i32, vp, i32, vp, i32, vp],
     "catseg_upconv3x3": [C.POINTER(ConvArgs), vp],
     "catseg_bce_onehot_loss": [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp, vp, vp],
+    "catseg_bce_onehot_loss_backward": [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp, vp, vp, vp],
     "catseg_swin_proj_mlp": [vp, i64, vp, i64, i64, vp, vp, vp, vp, C.c_float, vp, vp, i64, vp, vp, vp, i64, vp],
     "catseg_upconv3x3_stats_tile": [],
     "catseg_upconv_addend": [vp, i64, i32, i32, i32, vp, vp, i32, vp, i32, vp],

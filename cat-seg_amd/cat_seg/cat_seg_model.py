@@ -203,9 +203,10 @@ class CATSeg(nn.Module):
     def _training_loss(self, batched_inputs: List[dict]):
         """The training branch's loss (cat_seg_model.py:189-203): head logits of the batch, upsampled
         to the targets' size, BCE-with-logits against one-hot targets (ignore_value rows zero), as
-        {"loss_sem_seg": 0-d tensor} on the device (catseg_bce_onehot_loss).  Forward only: the HIP
-        path computes no gradients, so the loss does not require grad (a training loop's backward()
-        fails loudly); SURVEY §8(f) rank 4 -- backward kernels are outside the inference north star."""
+        {"loss_sem_seg": 0-d tensor} on the device (catseg_bce_onehot_loss).  The loss has a HIP
+        backward to the logits (catseg_bce_onehot_loss_backward, ops.BCEOneHotLoss), but the head and
+        backbone have none, so this loss does not require grad (a training loop's backward() fails
+        loudly); SURVEY §8(f) rank 4 -- the network's backward is outside the inference north star."""
         with torch.no_grad():
             eng = self.engine
             # training re-encodes the (training) class set every step, uncached (cat_seg_predictor.py:190-224);

@@ -609,6 +609,40 @@ def bce_onehot_loss(logits, targets, ignore_value=255):
     return loss
 
 
+def bce_onehot_loss_backward(logits, targets, ignore_value=255, grad_loss=None):
+    """d bce_onehot_loss / d logits on the device (catseg_bce_onehot_loss_backward): what autograd
+    computes for cat_seg_model.py:192-203 (BCE mean backward through the bilinear upsample's
+    backward), times grad_loss (0-d device fp32 tensor, None = 1).  Returns (B, T, h, w) fp32."""
+    B, T, h, w = logits.shape
+    Bt, H, W = targets.shape
+    assert Bt == B and logits.dtype == torch.float32 and logits.is_contiguous()
+    tg = targets.to(torch.int32).contiguous()
+    gl = None if grad_loss is None else grad_loss.to(device=logits.device, dtype=torch.float32).contiguous()
+    ws = torch.empty(B * T * H * w, device=logits.device, dtype=torch.float32)
+    grad = torch.empty_like(logits)
+    with _rec("bce_onehot_loss_backward", 0, logits.numel() * 8 + tg.numel() * 4 + ws.numel() * 8):
+        call("catseg_bce_onehot_loss_backward", logits.data_ptr(), B, T, h, w, tg.data_ptr(), H, W, ignore_value,
+             None if gl is None else gl.data_ptr(), ws.data_ptr(), grad.data_ptr(), _stream())
+    return grad
+
+
+class BCEOneHotLoss(torch.autograd.Function):
+    """bce_onehot_loss with its HIP backward: loss = BCEOneHotLoss.apply(logits, targets, ignore);
+    loss.backward() fills logits.grad through catseg_bce_onehot_loss_backward (targets get none)."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_value=255):
+        logits = logits.contiguous()
+        ctx.save_for_backward(logits, targets)
+        ctx.ignore_value = ignore_value
+        return bce_onehot_loss(logits, targets, ignore_value)
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        logits, targets = ctx.saved_tensors
+        return bce_onehot_loss_backward(logits, targets, ctx.ignore_value, grad_loss), None, None
+
+
 def semseg_confusion(probs, gt, conf, n_invalid, *, num_classes, ignore_label=255, clamp_pred=-1):
     """conf += bincount((N+1) * argmax(probs) + gt') on the device (catseg_semseg_confusion).
     probs (T, H, W) fp32, gt (H, W) int32, conf ((N+1)^2,) int64, n_invalid (1,) int64."""

@@ -107,7 +107,92 @@ __global__ __launch_bounds__(256) void bce_final_kernel(const double* __restrict
   if (threadIdx.x == 0) loss[0] = (float)(red[0] / denom);
 }
 
+// ---- its gradient w.r.t. the logits: dL/dlogits = U^T (sigmoid(U logits) - onehot) * g / denom,
+// U the separable bilinear upsample.  Gather form (each output element sums its own
+// contributions in a fixed order -- no atomics, deterministic), in two passes:
+//   pass 1 (one block per (image, target row y)): G[b][t][y][j] = sum over the target columns x
+//          whose taps include logit column j of wx(x, j) * (sigmoid(v(y, x)) - z(y, x)), v recomputed
+//          from the 4 logits taps exactly as the forward does;
+//   pass 2 (one block per (image*class, logit row i)): grad[b][t][i][j] = g / denom * sum over the
+//          target rows y whose taps include i of wy(y, i) * G[b][t][y][j].
+// The x (y) range of logit column j (row i) is the contiguous run of targets with x0(x) in {j-1, j}
+// (x0 is nondecreasing); the loop starts a few targets below the analytic start and skips zeros.
+DEV int bce_first_src(int j, int in_size, int out_size) {
+  // first target index whose floor source index can be >= j-1, minus a margin of 2
+  const int s = (int)floorf(((float)j - 1.5f) * (float)out_size / (float)in_size) - 2;
+  return s < 0 ? 0 : s;
+}
+
+__global__ __launch_bounds__(256) void bce_grad_rows_kernel(const float* __restrict__ logits, int T, int h, int w,
+                                                            const int32_t* __restrict__ tgt, int H, int W, int ignore,
+                                                            float* __restrict__ G) {
+  const int y = blockIdx.x, b = blockIdx.y;
+  int y0, y1;
+  float ly;
+  bce_lin(y, h, (float)h / (float)H, y0, y1, ly);
+  const float sx = (float)w / (float)W;
+  const int32_t* trow = tgt + ((int64_t)b * H + y) * W;
+  for (int idx = threadIdx.x; idx < T * w; idx += blockDim.x) {
+    const int t = idx / w, j = idx - t * w;
+    const float* L = logits + ((int64_t)b * T + t) * h * w;
+    const float* r0 = L + (int64_t)y0 * w;
+    const float* r1 = L + (int64_t)y1 * w;
+    float acc = 0.f;
+    for (int x = bce_first_src(j, w, W); x < W; ++x) {
+      int x0, x1;
+      float lx;
+      bce_lin(x, w, sx, x0, x1, lx);
+      if (x0 > j) break;
+      if (x1 < j) continue;
+      const float wt = (x0 == j ? 1.f - lx : 0.f) + (x1 == j ? lx : 0.f);
+      const float v = (1.f - ly) * ((1.f - lx) * r0[x0] + lx * r0[x1]) + ly * ((1.f - lx) * r1[x0] + lx * r1[x1]);
+      const int cls = trow[x];
+      const float z = (cls != ignore && t == cls) ? 1.f : 0.f;
+      acc += wt * (1.f / (1.f + __expf(-v)) - z);
+    }
+    G[(((int64_t)b * T + t) * H + y) * w + j] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void bce_grad_cols_kernel(const float* __restrict__ G, int h, int w, int H,
+                                                            const float* __restrict__ gscale, float inv_denom,
+                                                            float* __restrict__ grad) {
+  const int i = blockIdx.x;
+  const int64_t bt = blockIdx.y;
+  const float sy = (float)h / (float)H;
+  const float scale = (gscale ? gscale[0] : 1.f) * inv_denom;
+  const float* Gp = G + bt * H * w;
+  for (int j = threadIdx.x; j < w; j += blockDim.x) {
+    float acc = 0.f;
+    for (int y = bce_first_src(i, h, H); y < H; ++y) {
+      int y0, y1;
+      float ly;
+      bce_lin(y, h, sy, y0, y1, ly);
+      if (y0 > i) break;
+      if (y1 < i) continue;
+      const float wt = (y0 == i ? 1.f - ly : 0.f) + (y1 == i ? ly : 0.f);
+      acc += wt * Gp[(int64_t)y * w + j];
+    }
+    grad[(bt * h + i) * w + j] = acc * scale;
+  }
+}
+
 }  // namespace
+
+extern "C" int catseg_bce_onehot_loss_backward(const float* logits, int64_t B, int T, int h, int w,
+                                               const int32_t* targets, int H, int W, int ignore_value,
+                                               const float* grad_loss, float* workspace, float* grad_logits,
+                                               void* stream) {
+  CATSEG_CHECK(logits && targets && workspace && grad_logits, "bce_onehot_loss_backward: null pointer");
+  CATSEG_CHECK(B > 0 && T > 0 && h > 0 && w > 0 && H > 0 && W > 0 && B * T < 65536 && B < 65536,
+               "bce_onehot_loss_backward: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bce_grad_rows_kernel, dim3((unsigned)H, (unsigned)B), dim3(256), 0, st, logits, T, h, w,
+                     targets, H, W, ignore_value, workspace);
+  hipLaunchKernelGGL(bce_grad_cols_kernel, dim3((unsigned)h, (unsigned)(B * T)), dim3(256), 0, st, workspace, h, w,
+                     H, grad_loss, (float)(1.0 / ((double)B * H * W * T)), grad_logits);
+  return catseg_launch_status("bce_onehot_loss_backward");
+}
 
 extern "C" int catseg_bce_onehot_loss(const float* logits, int64_t B, int T, int h, int w, const int32_t* targets,
                                       int H, int W, int ignore_value, double* workspace, float* loss, void* stream) {

@@ -451,9 +451,18 @@ int catseg_eot_gather(const float* x, const int32_t* tokens, int64_t n, int ctx,
  * BCE-with-logits against one-hot targets built from targets [B][H][W] int32 (ignore_value
  * pixels have an all-zero target row and still count), mean over B*H*W*T -> *loss (fp32, device).
  * workspace: >= B*H doubles (caller-allocated).  Deterministic (fixed-order fp64 partial sums).
- * Forward only: the HIP path has no backward (training is outside the inference north star). */
+ * Its gradient w.r.t. the logits is catseg_bce_onehot_loss_backward. */
 int catseg_bce_onehot_loss(const float* logits, int64_t B, int T, int h, int w, const int32_t* targets, int H, int W,
                            int ignore_value, double* workspace, float* loss, void* stream);
+/* catseg_bce_onehot_loss_backward — d loss / d logits of catseg_bce_onehot_loss (what autograd
+ * computes for cat_seg_model.py:192-203: the BCE-with-logits mean's backward through
+ * F.interpolate's bilinear backward): grad_logits[B][T][h][w] = *grad_loss / (B*H*W*T) *
+ * U^T (sigmoid(U logits) - onehot), U the bilinear upsample.  grad_loss: device fp32 scalar (the
+ * upstream gradient; NULL = 1).  workspace: >= B*T*H*w floats.  Gather form, no atomics:
+ * deterministic.  Needs B*T < 65536. */
+int catseg_bce_onehot_loss_backward(const float* logits, int64_t B, int T, int h, int w, const int32_t* targets,
+                                    int H, int W, int ignore_value, const float* grad_loss, float* workspace,
+                                    float* grad_logits, void* stream);
 
 /* ---------------------------------------------------------------------------
  * catseg_semseg_confusion — the confusion-matrix update of detectron2's

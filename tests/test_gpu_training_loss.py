@@ -1,7 +1,8 @@
 """The training branch's loss (cat_seg_model.py:189-203) on the device: catseg_bce_onehot_loss vs
 the reference's own arithmetic (F.interpolate bilinear align_corners=False to the target size,
 one-hot targets with ignore rows left zero, F.binary_cross_entropy_with_logits mean) in fp64, and
-CATSeg.forward in training mode.  Forward only (no backward kernels)."""
+CATSeg.forward in training mode; the loss's backward to the logits (catseg_bce_onehot_loss_backward)
+vs torch autograd of the same arithmetic.  The network itself has no backward."""
 import os
 
 import numpy as np
@@ -100,3 +101,51 @@ def test_train_eval_alternation_keeps_the_test_class_set():
     model.eval()
     second = model([{"image": im}])[0]["sem_seg"]
     assert second.shape == first.shape and torch.equal(second, first)
+
+
+def reference_grad(logits, targets, ignore, scale=1.0):
+    """autograd of cat_seg_model.py:190-201 (interpolate -> BCE mean) in float64 on the CPU."""
+    x = logits.double().clone().requires_grad_(True)
+    out = F.interpolate(x, size=targets.shape[-2:], mode="bilinear", align_corners=False)
+    T = out.shape[1]
+    mask = targets != ignore
+    out = out.permute(0, 2, 3, 1)
+    tg = torch.zeros(out.shape, dtype=torch.float64)
+    tg[mask] = F.one_hot(targets[mask].long(), num_classes=T).double()
+    (F.binary_cross_entropy_with_logits(out, tg) * scale).backward()
+    return x.grad
+
+
+@pytest.mark.parametrize("B,T,h,w,H,W", [(2, 7, 24, 24, 96, 96), (3, 150, 24, 24, 50, 37), (1, 5, 96, 96, 384, 512),
+                                         (2, 3, 17, 29, 17, 29), (1, 4, 40, 30, 20, 45)])
+def test_bce_onehot_loss_backward_matches_autograd(B, T, h, w, H, W):
+    """catseg_bce_onehot_loss_backward vs torch autograd of the reference loss (fp64): upsampling by
+    4, ragged factors, identity size and a mixed down/up resize; deterministic (gather form)."""
+    g = torch.Generator().manual_seed(B * 1000 + T + h)
+    logits = torch.randn(B, T, h, w, generator=g) * 3
+    targets = torch.randint(0, T, (B, H, W), generator=g, dtype=torch.int32)
+    targets[torch.rand(B, H, W, generator=g) < 0.2] = 255
+    ref = reference_grad(logits, targets, 255)
+    got = ops.bce_onehot_loss_backward(logits.cuda(), targets.cuda(), 255).cpu().double()
+    assert got.shape == ref.shape
+    tol = 2e-5 * ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= tol, ((got - ref).abs().max().item(), tol)
+    again = ops.bce_onehot_loss_backward(logits.cuda(), targets.cuda(), 255).cpu().double()
+    assert torch.equal(again, got)
+
+
+def test_bce_onehot_loss_autograd_function():
+    """BCEOneHotLoss.apply(...).backward() on the device: loss equals bce_onehot_loss and
+    logits.grad equals the fp64 autograd gradient of the reference loss times the upstream scale."""
+    g = torch.Generator().manual_seed(11)
+    logits = torch.randn(2, 9, 24, 24, generator=g) * 2
+    targets = torch.randint(0, 9, (2, 96, 96), generator=g, dtype=torch.int32)
+    targets[:, :5] = 255
+    x = logits.cuda().requires_grad_(True)
+    loss = ops.BCEOneHotLoss.apply(x, targets.cuda(), 255)
+    assert loss.requires_grad
+    (loss * 3.0).backward()
+    assert abs(loss.item() - reference_loss(logits, targets, 255)) <= 1e-5 * abs(loss.item()) + 1e-6
+    ref = reference_grad(logits, targets, 255, scale=3.0)
+    got = x.grad.cpu().double()
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
