@@ -12,8 +12,11 @@ Mirrors the evaluators the reference registers (train_net.py:89-149):
 `process()` bins every pixel with `catseg_semseg_confusion` (argmax over the class planes +
 int64 bincount, exact); `evaluate()` sums the matrices over ranks (torch.distributed, as
 detectron2's `all_gather`, plain_train_net.py:136-146) and forms the metrics on the host
-from the small (N+1)^2 matrix.  Not reproduced: the COCO-RLE `sem_seg_predictions.json`
-dump (`encode_json_sem_seg`, needs pycocotools).
+from the small (N+1)^2 matrix.  With an `output_dir`, `process()` also keeps the COCO-stuff
+RLE records of every prediction (`encode_json_sem_seg`, plain_train_net.py:125,207-228; the RLE
+is pycocotools' `mask.encode`, restated in `coco_rle_encode` since pycocotools is absent) and
+`evaluate()` gathers them over ranks and writes `sem_seg_predictions.json`
+(plain_train_net.py:139-152).
 """
 from __future__ import annotations
 
@@ -45,6 +48,37 @@ def _catalog_gt_loader(dataset_name):
         with Image.open(table[inp["file_name"]]) as im:
             return np.array(im, dtype=np.int64)
     return load
+
+
+def coco_rle_encode(mask: np.ndarray) -> dict:
+    """pycocotools `mask.encode` of one H x W binary mask (the call in plain_train_net.py:223), as
+    {"size": [H, W], "counts": str}: run lengths over the column-major pixels, alternating and
+    starting with a run of zeros (0 when pixel (0, 0) is set) -- maskApi.c rleEncode -- written
+    with maskApi.c rleToString's compression: from the third count on, each count minus the count
+    two before, in 5-bit groups low first, 0x20 = more groups follow, 0x10 of the last group = the
+    sign, each group + 48 as one ASCII character.  pycocotools is not installed here: the string is
+    checked against hand-derived vectors of that published algorithm and an independent decoder
+    (tests/test_eval_cpu.py), not against pycocotools itself."""
+    mask = np.asarray(mask)
+    h, w = mask.shape
+    flat = np.asarray(mask, dtype=bool).ravel(order="F")
+    if flat.size == 0:
+        cnts = [0]
+    else:
+        edges = np.flatnonzero(flat[1:] != flat[:-1]) + 1
+        runs = np.diff(np.concatenate(([0], edges, [flat.size])))
+        cnts = ([0] if flat[0] else []) + runs.tolist()
+    out = []
+    for i, c in enumerate(cnts):
+        x = int(c) - (int(cnts[i - 2]) if i > 2 else 0)
+        while True:
+            g = x & 0x1F
+            x >>= 5
+            more = (x != -1) if (g & 0x10) else (x != 0)
+            out.append(chr((g | 0x20 if more else g) + 48))
+            if not more:
+                break
+    return {"size": [int(h), int(w)], "counts": "".join(out)}
 
 
 def reduce_confusion(conf: torch.Tensor) -> torch.Tensor:
@@ -115,12 +149,16 @@ class SemSegEvaluator:
         self._dataset_name = dataset_name
         self._gt_loader = gt_loader
         self._device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        # contiguous training ids -> dataset category ids for the RLE records (plain_train_net.py:84-90)
+        c2d = meta.get("stuff_dataset_id_to_contiguous_id") if meta is not None else None
+        self._contiguous_id_to_dataset_id = {v: k for k, v in c2d.items()} if c2d else None
         self.reset()
 
     def reset(self):
         n1 = self._num_classes + 1
         self._conf = torch.zeros(n1 * n1, dtype=torch.int64, device=self._device)
         self._invalid = torch.zeros(1, dtype=torch.int64, device=self._device)
+        self._predictions = []
 
     def _gt(self, inp) -> torch.Tensor:
         gt = inp.get("sem_seg_gt")
@@ -146,6 +184,38 @@ class SemSegEvaluator:
                 raise ValueError(f"gt {tuple(gt.shape)} vs prediction {tuple(probs.shape[1:])}")
             ops.semseg_confusion(probs, gt, self._conf, self._invalid, num_classes=self._num_classes,
                                  ignore_label=self._ignore_label, clamp_pred=self.clamp_pred)
+            if self._output_dir:
+                # the records are written only with an output_dir, so only then is the argmax map
+                # brought to the host (the reference builds them for every image)
+                pred = probs.argmax(dim=0)
+                if self.clamp_pred >= 0:
+                    pred = pred.clamp(max=self.clamp_pred)
+                self._predictions.extend(self.encode_json_sem_seg(pred.cpu().numpy(), inp.get("file_name")))
+
+    def encode_json_sem_seg(self, sem_seg: np.ndarray, input_file_name) -> list:
+        """COCO-stuff records of one argmax map (plain_train_net.py:207-228): one per label present,
+        {"file_name", "category_id", "segmentation": RLE}, labels mapped to dataset ids when the
+        metadata has stuff_dataset_id_to_contiguous_id."""
+        records = []
+        for label in np.unique(sem_seg):
+            if self._contiguous_id_to_dataset_id is not None:
+                if int(label) not in self._contiguous_id_to_dataset_id:
+                    raise AssertionError(f"Label {label} is not in the metadata info for {self._dataset_name}")
+                dataset_id = self._contiguous_id_to_dataset_id[int(label)]
+            else:
+                dataset_id = int(label)
+            records.append({"file_name": input_file_name, "category_id": dataset_id,
+                            "segmentation": coco_rle_encode(sem_seg == label)})
+        return records
+
+    def predictions(self) -> list:
+        """The RLE records of every processed image, gathered over ranks in rank order
+        (plain_train_net.py:139-140)."""
+        if self._distributed and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            parts = [None] * dist.get_world_size()
+            dist.all_gather_object(parts, self._predictions)
+            return [r for part in parts for r in part]
+        return list(self._predictions)
 
     def confusion_matrix(self) -> np.ndarray:
         n1 = self._num_classes + 1
@@ -161,12 +231,17 @@ class SemSegEvaluator:
             # the reference's bincount would outgrow the matrix and its reshape would fail
             raise ValueError(f"{invalid} ground-truth labels outside [0, {self._num_classes}) and != ignore_label")
         conf = self.confusion_matrix()
+        preds = self.predictions() if self._output_dir else None
         if self._distributed and dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
             return None
-        res = self._metrics(conf)
         if self._output_dir:
+            import json
             import os
             os.makedirs(self._output_dir, exist_ok=True)
+            with open(os.path.join(self._output_dir, "sem_seg_predictions.json"), "w") as f:
+                f.write(json.dumps(preds))
+        res = self._metrics(conf)
+        if self._output_dir:
             torch.save(res, os.path.join(self._output_dir, "sem_seg_evaluation.pth"))
         return OrderedDict({"sem_seg": res})
 

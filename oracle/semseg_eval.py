@@ -66,3 +66,70 @@ def metrics(conf: np.ndarray, class_names, val_extra_classes=()) -> dict:
         res["unseen_IoU"] = unseen
         res["harmonic mean"] = 2 * seen * unseen / (seen + unseen)
     return res
+
+
+def rle_encode(mask: np.ndarray) -> dict:
+    """pycocotools `mask.encode` of one H x W binary mask (plain_train_net.py:223; pycocotools is
+    not vendored in the reference and not installed here), restated with plain loops after its
+    published C source: maskApi.c rleEncode (column-major run lengths, alternating, starting with
+    zeros) then rleToString (delta against the count two back from the third on, 5-bit groups with
+    continuation bit 0x20 and sign bit 0x10, + 48).  Parity unpinned against pycocotools itself."""
+    mask = np.asarray(mask)
+    h, w = mask.shape
+    cnts, prev, run = [], 0, 0
+    for j in range(w):
+        for i in range(h):
+            v = 1 if mask[i, j] else 0
+            if v != prev:
+                cnts.append(run)
+                run, prev = 0, v
+            run += 1
+    cnts.append(run)
+    s = []
+    for i, c in enumerate(cnts):
+        x = c - cnts[i - 2] if i > 2 else c
+        more = True
+        while more:
+            g = x & 0x1F
+            x >>= 5
+            more = x != -1 if g & 0x10 else x != 0
+            if more:
+                g |= 0x20
+            s.append(chr(g + 48))
+    return {"size": [h, w], "counts": "".join(s)}
+
+
+def rle_decode(rle: dict) -> np.ndarray:
+    """maskApi.c rleFrString + rleDecode: the inverse of rle_encode (an H x W uint8 mask)."""
+    h, w = rle["size"]
+    s, p, cnts = rle["counts"], 0, []
+    while p < len(s):
+        x, k, more = 0, 0, True
+        while more:
+            c = ord(s[p]) - 48
+            x |= (c & 0x1F) << (5 * k)
+            more = bool(c & 0x20)
+            p += 1
+            k += 1
+            if not more and (c & 0x10):
+                x |= -1 << (5 * k)
+        if len(cnts) > 2:
+            x += cnts[-2]
+        cnts.append(x)
+    flat = np.zeros(h * w, np.uint8)
+    pos, v = 0, 0
+    for c in cnts:
+        flat[pos:pos + c] = v
+        pos += c
+        v ^= 1
+    assert pos == h * w, "counts do not cover the mask"
+    return flat.reshape(w, h).T
+
+
+def sem_seg_records(pred: np.ndarray, file_name, contiguous_to_dataset=None) -> list:
+    """encode_json_sem_seg (plain_train_net.py:207-228) of one argmax map."""
+    out = []
+    for label in np.unique(pred):
+        cid = contiguous_to_dataset[int(label)] if contiguous_to_dataset is not None else int(label)
+        out.append({"file_name": file_name, "category_id": cid, "segmentation": rle_encode(pred == label)})
+    return out

@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from cat_seg.evaluation import reduce_confusion, semseg_metrics
+from cat_seg.evaluation import SemSegEvaluator, coco_rle_encode, reduce_confusion, semseg_metrics
 from oracle import semseg_eval as OE
 
 
@@ -91,3 +91,95 @@ def test_reduce_confusion_gloo_world2():
         p.join(timeout=60)
     expect = [3 * i for i in range(9)]
     assert got[0] == expect and got[1] == expect
+
+
+# ---- sem_seg_predictions.json: COCO RLE records (plain_train_net.py:125,139-152,207-228) ----
+
+def _column(counts):
+    """an N x 1 mask with the given alternating run lengths (zeros first)"""
+    v, out = 0, []
+    for c in counts:
+        out += [v] * c
+        v ^= 1
+    return np.array(out, np.uint8)[:, None]
+
+
+@pytest.mark.parametrize("counts,expect", [([4], "4"), ([0, 1], "01"), ([100], "T3"), ([10, 20, 5], ":d05"),
+                                           ([10, 20, 5, 3], ":d05_O"), ([0, 40, 2, 40], "0X120")])
+def test_coco_rle_hand_vectors(counts, expect):
+    """strings derived by hand from maskApi.c rleToString: 100 -> 'T3' (groups 4 | 0x20, 3); 20 ->
+    'd0' (0x10 set, so a second group carries the sign); the fourth count as a delta: 3 - 20 = -17
+    -> '_O', 40 - 40 = 0 -> '0'; 40 -> 'X1'."""
+    m = _column(counts)
+    if counts == [4]:
+        m = np.zeros((2, 2), np.uint8)
+    got = coco_rle_encode(m)
+    assert got == OE.rle_encode(m)
+    assert got["counts"] == expect, (got["counts"], expect)
+    assert got["size"] == list(m.shape)
+    assert np.array_equal(OE.rle_decode(got), m)
+
+
+@pytest.mark.parametrize("shape,density", [((37, 53), 0.5), ((64, 64), 0.02), ((1, 97), 0.7), ((120, 5), 0.98),
+                                           ((16, 16), 0.0), ((16, 16), 1.0)])
+def test_coco_rle_matches_loop_restatement(shape, density):
+    rng = np.random.default_rng(shape[0] * 7 + int(density * 100))
+    m = (rng.random(shape) < density).astype(np.uint8)
+    if 0 < density < 1:                 # long runs too, so multi-group and negative deltas occur
+        m[: shape[0] // 2, : shape[1] // 3] = 1
+    got = coco_rle_encode(m)
+    assert got == OE.rle_encode(m)
+    assert np.array_equal(OE.rle_decode(got), m)
+
+
+def test_encode_json_sem_seg_records_and_dataset_ids():
+    ev = SemSegEvaluator(None, distributed=False, class_names=list("abcde"), ignore_label=255, device="cpu")
+    pred = np.random.default_rng(0).integers(0, 5, (23, 31))
+    pred[pred == 3] = 4                                     # label 3 absent: no record
+    recs = ev.encode_json_sem_seg(pred, "img.jpg")
+    assert recs == OE.sem_seg_records(pred, "img.jpg")
+    assert [r["category_id"] for r in recs] == [0, 1, 2, 4]
+    ev._contiguous_id_to_dataset_id = {0: 10, 1: 11, 2: 12, 3: 13, 4: 20}
+    mapped = ev.encode_json_sem_seg(pred, "img.jpg")
+    assert [r["category_id"] for r in mapped] == [10, 11, 12, 20]
+    ev._contiguous_id_to_dataset_id = {0: 10}
+    with pytest.raises(AssertionError):
+        ev.encode_json_sem_seg(pred, "img.jpg")
+
+
+def _rank_dump(rank, world, port, out_dir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ev = SemSegEvaluator(None, distributed=True, output_dir=out_dir, class_names=["a", "b", "c"], ignore_label=255,
+                         device="cpu")
+    ev._conf += torch.arange(16, dtype=torch.int64)         # a non-empty matrix; no device kernel on the CPU
+    pred = np.full((4, 6), rank, np.int64)
+    pred[0, :2] = 2
+    ev._predictions.extend(ev.encode_json_sem_seg(pred, f"img{rank}.jpg"))
+    res = ev.evaluate()
+    q.put((rank, res is not None))
+    dist.destroy_process_group()
+
+
+def test_predictions_json_gathered_over_ranks(tmp_path):
+    """evaluate() with an output_dir gathers every rank's records in rank order and rank 0 writes
+    sem_seg_predictions.json (plain_train_net.py:139-152) beside sem_seg_evaluation.pth."""
+    import json
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_dump, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert got == {0: True, 1: False}
+    recs = json.loads((tmp_path / "sem_seg_predictions.json").read_text())
+    expect = []
+    for r in range(2):
+        pred = np.full((4, 6), r, np.int64)
+        pred[0, :2] = 2
+        expect += OE.sem_seg_records(pred, f"img{r}.jpg")
+    assert recs == expect
+    assert (tmp_path / "sem_seg_evaluation.pth").exists()

@@ -107,3 +107,28 @@ def test_evaluator_raises_on_invalid_gt():
     ev.process([{"sem_seg_gt": np.full((4, 4), 9)}], [{"sem_seg": torch.rand(2, 4, 4).cuda()}])
     with pytest.raises(ValueError):
         ev.evaluate()
+
+
+@pytest.mark.parametrize("cls", [SemSegEvaluator, VOCbEvaluator])
+def test_evaluator_writes_predictions_json(cls, tmp_path):
+    """process() with an output_dir keeps the COCO RLE records of every prediction's argmax map
+    (VOC-b: folded at 20 first, train_net.py:60,71) and evaluate() writes them as
+    sem_seg_predictions.json (plain_train_net.py:125,148-152): equal to the oracle's records of
+    the numpy argmax, each decoding back to its label's mask."""
+    import json
+    T = 23 if cls is VOCbEvaluator else 9
+    names = [f"c{i}" for i in range(T)]
+    ev = cls(None, distributed=False, output_dir=str(tmp_path), class_names=names, ignore_label=255)
+    expect = []
+    for i in range(2):
+        probs, gt = _case(T, 40 + i, 52, seed=30 + i, n_levels=50)
+        ev.process([{"sem_seg_gt": gt.numpy(), "file_name": f"im{i}.png"}], [{"sem_seg": probs.cuda()}])
+        pred = probs.numpy().argmax(0)
+        if cls.clamp_pred >= 0:
+            pred[pred >= cls.clamp_pred] = cls.clamp_pred
+        expect += OE.sem_seg_records(pred, f"im{i}.png")
+    ev.evaluate()
+    recs = json.loads((tmp_path / "sem_seg_predictions.json").read_text())
+    assert recs == expect
+    for r in recs[:5]:
+        assert OE.rle_decode(r["segmentation"]).shape == (40, 52) or OE.rle_decode(r["segmentation"]).shape == (41, 52)
