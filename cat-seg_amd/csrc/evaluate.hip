@@ -73,13 +73,22 @@ __global__ __launch_bounds__(256) void bce_rows_kernel(const float* __restrict__
     float lx;
     bce_lin(x, w, (float)w / (float)W, x0, x1, lx);
     const int cls = tgt[((int64_t)b * H + y) * W + x];
+    // the class planes' taps are independent loads: unrolled so a batch is in flight per round trip;
+    // softplus(-|v|) as log(1 + e) with the hardware log / exp (absolute error ~1e-7 per term)
+    const float* L0 = logits + (int64_t)b * T * h * w + (int64_t)y0 * w;
+    const float* L1 = logits + (int64_t)b * T * h * w + (int64_t)y1 * w;
+    const int64_t plane = (int64_t)h * w;
     float s = 0.f;
+#pragma unroll 8
     for (int t = 0; t < T; ++t) {
-      const float* L = logits + ((int64_t)b * T + t) * h * w;
-      const float v = (1.f - ly) * ((1.f - lx) * L[y0 * w + x0] + lx * L[y0 * w + x1]) +
-                      ly * ((1.f - lx) * L[y1 * w + x0] + lx * L[y1 * w + x1]);
-      const float z = (cls != ignore && t == cls) ? 1.f : 0.f;
-      s += fmaxf(v, 0.f) - v * z + log1pf(__expf(-fabsf(v)));
+      const float v = (1.f - ly) * ((1.f - lx) * L0[t * plane + x0] + lx * L0[t * plane + x1]) +
+                      ly * ((1.f - lx) * L1[t * plane + x0] + lx * L1[t * plane + x1]);
+      s += fmaxf(v, 0.f) + __logf(1.f + __expf(-fabsf(v)));
+    }
+    if (cls != ignore && cls >= 0 && cls < T) {
+      const float v = (1.f - ly) * ((1.f - lx) * L0[cls * plane + x0] + lx * L0[cls * plane + x1]) +
+                      ly * ((1.f - lx) * L1[cls * plane + x0] + lx * L1[cls * plane + x1]);
+      s -= v;
     }
     acc += (double)s;
   }
@@ -111,73 +120,118 @@ __global__ __launch_bounds__(256) void bce_final_kernel(const double* __restrict
 // U the separable bilinear upsample.  Gather form (each output element sums its own
 // contributions in a fixed order -- no atomics, deterministic), in two passes:
 //   pass 1 (one block per (image, target row y)): G[b][t][y][j] = sum over the target columns x
-//          whose taps include logit column j of wx(x, j) * (sigmoid(v(y, x)) - z(y, x)), v recomputed
+//          whose taps include logit column j of wx(x, j) * (sigmoid(v(y, x)) - z(y, x)), v computed
 //          from the 4 logits taps exactly as the forward does;
-//   pass 2 (one block per (image*class, logit row i)): grad[b][t][i][j] = g / denom * sum over the
-//          target rows y whose taps include i of wy(y, i) * G[b][t][y][j].
+//   pass 2 (one thread per logit): grad[b][t][i][j] = g / denom * sum over the target rows y
+//          whose taps include i of wy(y, i) * G[b][t][y][j].
 // The x (y) range of logit column j (row i) is the contiguous run of targets with x0(x) in {j-1, j}
-// (x0 is nondecreasing); the loop starts a few targets below the analytic start and skips zeros.
+// (x0 is nondecreasing); the scan starts a few targets below the analytic start.
 DEV int bce_first_src(int j, int in_size, int out_size) {
   // first target index whose floor source index can be >= j-1, minus a margin of 2
   const int s = (int)floorf(((float)j - 1.5f) * (float)out_size / (float)in_size) - 2;
   return s < 0 ? 0 : s;
 }
 
+// the contributing run [a, b) of targets for source index j (index arithmetic only)
+DEV void bce_run(int j, int in_size, int out_size, float scale, int& a, int& b) {
+  a = bce_first_src(j, in_size, out_size);
+  for (; a < out_size; ++a) {
+    int i0, i1;
+    float l1;
+    bce_lin(a, in_size, scale, i0, i1, l1);
+    if (i1 >= j) break;
+  }
+  for (b = a; b < out_size; ++b) {
+    int i0, i1;
+    float l1;
+    bce_lin(b, in_size, scale, i0, i1, l1);
+    if (i0 > j) break;
+  }
+}
+
+// pass 1: one block per (image, target row y).  Per chunk of TC classes the residuals
+// r[t][x] = sigmoid(v) - z of the whole target row are computed once into LDS (x on the lanes:
+// the logits taps of a class plane are neighbouring loads), then every (class, logit column j)
+// sums its run of x from LDS.  The per-column runs are computed once per block.
 __global__ __launch_bounds__(256) void bce_grad_rows_kernel(const float* __restrict__ logits, int T, int h, int w,
                                                             const int32_t* __restrict__ tgt, int H, int W, int ignore,
-                                                            float* __restrict__ G) {
+                                                            int TC, float* __restrict__ G) {
+  extern __shared__ float lds[];
+  float* R = lds;                                  // [TC][W]
+  int* run = reinterpret_cast<int*>(lds + TC * W); // [w][2]
   const int y = blockIdx.x, b = blockIdx.y;
   int y0, y1;
   float ly;
   bce_lin(y, h, (float)h / (float)H, y0, y1, ly);
   const float sx = (float)w / (float)W;
   const int32_t* trow = tgt + ((int64_t)b * H + y) * W;
-  for (int idx = threadIdx.x; idx < T * w; idx += blockDim.x) {
-    const int t = idx / w, j = idx - t * w;
-    const float* L = logits + ((int64_t)b * T + t) * h * w;
-    const float* r0 = L + (int64_t)y0 * w;
-    const float* r1 = L + (int64_t)y1 * w;
-    float acc = 0.f;
-    for (int x = bce_first_src(j, w, W); x < W; ++x) {
+  const int64_t plane = (int64_t)h * w;
+  const float* L0 = logits + (int64_t)b * T * plane + (int64_t)y0 * w;
+  const float* L1 = logits + (int64_t)b * T * plane + (int64_t)y1 * w;
+  for (int j = threadIdx.x; j < w; j += blockDim.x) bce_run(j, w, W, sx, run[2 * j], run[2 * j + 1]);
+  for (int t0 = 0; t0 < T; t0 += TC) {
+    const int nt = min(TC, T - t0);
+    __syncthreads();                               // runs written / previous chunk consumed
+    // a lane owns target column x and walks the chunk's classes: the taps of 8 classes in flight
+    // per round trip (one class per iteration would pay a round trip each)
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
       int x0, x1;
       float lx;
       bce_lin(x, w, sx, x0, x1, lx);
-      if (x0 > j) break;
-      if (x1 < j) continue;
-      const float wt = (x0 == j ? 1.f - lx : 0.f) + (x1 == j ? lx : 0.f);
-      const float v = (1.f - ly) * ((1.f - lx) * r0[x0] + lx * r0[x1]) + ly * ((1.f - lx) * r1[x0] + lx * r1[x1]);
       const int cls = trow[x];
-      const float z = (cls != ignore && t == cls) ? 1.f : 0.f;
-      acc += wt * (1.f / (1.f + __expf(-v)) - z);
+      const int zt = (cls != ignore) ? cls - t0 : -1;
+#pragma unroll 8
+      for (int tt = 0; tt < nt; ++tt) {
+        const float* r0 = L0 + (int64_t)(t0 + tt) * plane;
+        const float* r1 = L1 + (int64_t)(t0 + tt) * plane;
+        const float v = (1.f - ly) * ((1.f - lx) * r0[x0] + lx * r0[x1]) + ly * ((1.f - lx) * r1[x0] + lx * r1[x1]);
+        R[tt * W + x] = __builtin_amdgcn_rcpf(1.f + __expf(-v)) - (tt == zt ? 1.f : 0.f);
+      }
     }
-    G[(((int64_t)b * T + t) * H + y) * w + j] = acc;
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nt * w; idx += blockDim.x) {
+      const int tt = idx / w, j = idx - tt * w;
+      const float* Rt = R + tt * W;
+      float acc = 0.f;
+      for (int x = run[2 * j]; x < run[2 * j + 1]; ++x) {
+        int x0, x1;
+        float lx;
+        bce_lin(x, w, sx, x0, x1, lx);
+        acc += ((x0 == j ? 1.f - lx : 0.f) + (x1 == j ? lx : 0.f)) * Rt[x];
+      }
+      G[(((int64_t)b * T + t0 + tt) * H + y) * w + j] = acc;
+    }
   }
 }
 
+// pass 2: one thread per logit (class plane bt, row i, column j); grid (ceil(h*w / 256), B*T).
 __global__ __launch_bounds__(256) void bce_grad_cols_kernel(const float* __restrict__ G, int h, int w, int H,
                                                             const float* __restrict__ gscale, float inv_denom,
                                                             float* __restrict__ grad) {
-  const int i = blockIdx.x;
   const int64_t bt = blockIdx.y;
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= h * w) return;
+  const int i = o / w, j = o - i * w;
   const float sy = (float)h / (float)H;
   const float scale = (gscale ? gscale[0] : 1.f) * inv_denom;
-  const float* Gp = G + bt * H * w;
-  for (int j = threadIdx.x; j < w; j += blockDim.x) {
-    float acc = 0.f;
-    for (int y = bce_first_src(i, h, H); y < H; ++y) {
-      int y0, y1;
-      float ly;
-      bce_lin(y, h, sy, y0, y1, ly);
-      if (y0 > i) break;
-      if (y1 < i) continue;
-      const float wt = (y0 == i ? 1.f - ly : 0.f) + (y1 == i ? ly : 0.f);
-      acc += wt * Gp[(int64_t)y * w + j];
-    }
-    grad[(bt * h + i) * w + j] = acc * scale;
+  const float* Gp = G + bt * H * w + j;
+  int ya, yb;
+  bce_run(i, h, H, sy, ya, yb);
+  float acc = 0.f;
+#pragma unroll 4
+  for (int y = ya; y < yb; ++y) {
+    int y0, y1;
+    float ly;
+    bce_lin(y, h, sy, y0, y1, ly);
+    acc += ((y0 == i ? 1.f - ly : 0.f) + (y1 == i ? ly : 0.f)) * Gp[(int64_t)y * w];
   }
+  grad[bt * h * w + o] = acc * scale;
 }
 
 }  // namespace
+
+int g_bce_classes = 0;   // classes per LDS chunk in the loss backward's rows pass (0 = auto)
+CATSEG_KNOB(g_bce_classes, "bce_classes");
 
 extern "C" int catseg_bce_onehot_loss_backward(const float* logits, int64_t B, int T, int h, int w,
                                                const int32_t* targets, int H, int W, int ignore_value,
@@ -186,11 +240,17 @@ extern "C" int catseg_bce_onehot_loss_backward(const float* logits, int64_t B, i
   CATSEG_CHECK(logits && targets && workspace && grad_logits, "bce_onehot_loss_backward: null pointer");
   CATSEG_CHECK(B > 0 && T > 0 && h > 0 && w > 0 && H > 0 && W > 0 && B * T < 65536 && B < 65536,
                "bce_onehot_loss_backward: bad shape");
+  // LDS for the rows pass: TC class rows of W residuals + the w column runs.  Auto: 16 classes
+  // (24 KB at W = 384), capped at 32 KB; at the training shape 4 / 8 / 16 / 21 / 32 classes measured
+  // 355 / 315 / 306 / 415 / 404 us (tools/micro_bce.py)
+  const int TC = std::max(1, std::min(T, g_bce_classes > 0 ? g_bce_classes : std::min(16, 8192 / W)));
+  const size_t lds = (size_t)TC * W * 4 + (size_t)w * 8;
+  CATSEG_CHECK(lds <= 64 * 1024, "bce_onehot_loss_backward: target or logits rows too wide");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bce_grad_rows_kernel, dim3((unsigned)H, (unsigned)B), dim3(256), 0, st, logits, T, h, w,
-                     targets, H, W, ignore_value, workspace);
-  hipLaunchKernelGGL(bce_grad_cols_kernel, dim3((unsigned)h, (unsigned)(B * T)), dim3(256), 0, st, workspace, h, w,
-                     H, grad_loss, (float)(1.0 / ((double)B * H * W * T)), grad_logits);
+  hipLaunchKernelGGL(bce_grad_rows_kernel, dim3((unsigned)H, (unsigned)B), dim3(256), lds, st, logits, T, h, w,
+                     targets, H, W, ignore_value, TC, workspace);
+  hipLaunchKernelGGL(bce_grad_cols_kernel, dim3((unsigned)((h * w + 255) / 256), (unsigned)(B * T)), dim3(256), 0,
+                     st, workspace, h, w, H, grad_loss, (float)(1.0 / ((double)B * H * W * T)), grad_logits);
   return catseg_launch_status("bce_onehot_loss_backward");
 }
 

@@ -132,6 +132,14 @@ def test_bce_onehot_loss_backward_matches_autograd(B, T, h, w, H, W):
     assert (got - ref).abs().max().item() <= tol, ((got - ref).abs().max().item(), tol)
     again = ops.bce_onehot_loss_backward(logits.cuda(), targets.cuda(), 255).cpu().double()
     assert torch.equal(again, got)
+    # the rows pass's LDS class chunk (knob bce_classes) does not change any sum's order
+    from cat_seg import _lib as L
+    try:
+        for c in (1, 5, 32):
+            L.tune("bce_classes", c)
+            assert torch.equal(ops.bce_onehot_loss_backward(logits.cuda(), targets.cuda(), 255).cpu().double(), got)
+    finally:
+        L.tune("bce_classes", 0)
 
 
 def test_bce_onehot_loss_autograd_function():

@@ -2,7 +2,7 @@
 configs: 384^2 crops, COCO-Stuff's 171 training classes, logits 96^2, 4 images per GPU):
 catseg_bce_onehot_loss, catseg_bce_onehot_loss_backward, and torch's own GPU autograd of the same
 arithmetic (F.interpolate + one-hot BCE, fp32) beside them; checks the gradients agree.
-usage: python tools/micro_bce.py [B]"""
+usage: python tools/micro_bce.py [B] [bce_classes values for the backward's LDS chunk, e.g. 0,4,8,16]"""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
@@ -33,6 +33,10 @@ def torch_fwd_bwd():
 fns = {"loss": lambda: ops.bce_onehot_loss(logits, targets, 255),
        "loss_backward": lambda: ops.bce_onehot_loss_backward(logits, targets, 255),
        "torch_autograd_fwd_bwd": torch_fwd_bwd}
+chunks = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else []
+for c in chunks:
+    fns[f"loss_backward_classes{c}"] = (lambda c=c: (L.tune("bce_classes", c),
+                                                     ops.bce_onehot_loss_backward(logits, targets, 255))[1])
 res = {}
 for name, f in fns.items():
     f()
@@ -47,6 +51,7 @@ for name, f in fns.items():
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 5 * 1e3)
     res[name] = round(best, 1)
+L.tune("bce_classes", 0)
 ref = torch_fwd_bwd()
 got = ops.bce_onehot_loss_backward(logits, targets, 255)
 err = (got - ref).abs().max().item() / ref.abs().max().item()
