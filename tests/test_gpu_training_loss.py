@@ -142,6 +142,25 @@ def test_bce_onehot_loss_backward_matches_autograd(B, T, h, w, H, W):
         L.tune("bce_classes", 0)
 
 
+@pytest.mark.parametrize("case", ["all_ignored", "one_class", "one_pixel_logits", "wide_targets"])
+def test_bce_onehot_loss_backward_edges(case):
+    """edge cases of the gather ranges and the one-hot: every target pixel ignored (all-zero rows),
+    T = 1, a 1 x 1 logit map (every target reads the same logit), targets wider than one LDS chunk
+    row (W = 2100: the automatic class chunk drops to 3)."""
+    g = torch.Generator().manual_seed(5)
+    B, T, h, w, H, W = {"all_ignored": (2, 6, 12, 12, 48, 48), "one_class": (2, 1, 24, 24, 96, 96),
+                        "one_pixel_logits": (1, 4, 1, 1, 9, 13), "wide_targets": (1, 5, 8, 300, 16, 2100)}[case]
+    logits = torch.randn(B, T, h, w, generator=g) * 3
+    targets = torch.randint(0, T, (B, H, W), generator=g, dtype=torch.int32)
+    if case == "all_ignored":
+        targets[:] = 255
+    ref = reference_grad(logits, targets, 255)
+    got = ops.bce_onehot_loss_backward(logits.cuda(), targets.cuda(), 255).cpu().double()
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+    loss = ops.bce_onehot_loss(logits.cuda(), targets.cuda(), 255).item()
+    assert abs(loss - reference_loss(logits, targets, 255)) <= 1e-5 * abs(loss) + 1e-6
+
+
 def test_bce_onehot_loss_autograd_function():
     """BCEOneHotLoss.apply(...).backward() on the device: loss equals bce_onehot_loss and
     logits.grad equals the fp64 autograd gradient of the reference loss times the upstream scale."""
