@@ -121,6 +121,54 @@ class ConvArgs(C.Structure):
     ]
 
 
+class GemmExArgs(C.Structure):
+    _fields_ = [
+        ("A", vp), ("a_sm", i64), ("a_sk", i64),
+        ("B", vp), ("b_sk", i64), ("b_sn", i64),
+        ("M", i64), ("N", i64), ("K", i64),
+        ("C", vp), ("ldc", i64),
+        ("alpha", f32), ("beta", i32),
+        ("workspace", vp), ("workspace_bytes", i64),
+    ]
+
+
+class WinAttnBwdArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
+        ("o", vp), ("ld_o", i64),
+        ("dout", vp), ("ld_dout", i64),
+        ("dq", vp), ("dk", vp), ("dv", vp), ("ld_dqkv", i64),
+        ("S", i64), ("img_h", i32), ("img_w", i32), ("window", i32), ("shift", i32), ("n_heads", i32),
+        ("head_dim", i32), ("scale", f32),
+    ]
+
+
+class LinAttnBwdArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
+        ("dy", vp), ("ld_dy", i64),
+        ("dq", vp), ("dk", vp), ("dv", vp), ("ld_dqkv", i64),
+        ("B", i64), ("T", i32), ("HW", i32), ("n_heads", i32), ("head_dim", i32),
+        ("n_pad", i32), ("k_pad", vp), ("v_pad", vp), ("eps", f32),
+        ("dk_pad", vp), ("dv_pad", vp),
+        ("workspace", vp), ("workspace_bytes", i64),
+    ]
+
+
+class Conv2dArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ld_x", i64),
+        ("S", i64), ("H", i32), ("W", i32), ("cin", i32),
+        ("w", vp), ("ld_w", i64),
+        ("cout", i32), ("ksize", i32), ("pad", i32),
+        ("bias", vp), ("act", i32),
+        ("y", vp), ("ld_y", i64),
+        ("alpha", f32), ("beta", i32),
+        ("dw", vp),
+        ("workspace", vp), ("workspace_bytes", i64),
+    ]
+
+
 # name -> (argtypes); every entry returns int
 _SIGS = {
     "catseg_gemm": [C.POINTER(GemmArgs), vp],
@@ -169,6 +217,34 @@ _SIGS = {
     "catseg_token_embed": [vp, i64, i32, vp, vp, i32, vp, vp],
     "catseg_eot_gather": [vp, vp, i64, i32, i32, vp, vp],
     "catseg_convt64_gn": [vp, i64, i64, vp, vp, vp, vp, i32, vp, i64, C.POINTER(RowsEpi), vp],
+    # training-side entry points (include/catseg_hip_train.h)
+    "catseg_gemm_ex": [C.POINTER(GemmExArgs), vp],
+    "catseg_gemm_ex_workspace": [i64, i64, i64],
+    "catseg_colsum": [vp, i64, i64, i64, vp, f32, i32, vp, i64, vp],
+    "catseg_colsum_workspace": [i64, i64],
+    "catseg_layernorm_backward": [vp, i64, vp, vp, i64, vp, i64, i32, i64, i64, f32, vp, vp, i32, vp, i64, vp],
+    "catseg_layernorm_backward_workspace": [i64, i64],
+    "catseg_act_forward": [vp, vp, i64, i32, vp],
+    "catseg_act_backward": [vp, vp, vp, i64, i32, vp],
+    "catseg_groupnorm_stats_rows": [vp, i64, i64, i32, i32, f32, vp, vp, vp],
+    "catseg_groupnorm_relu_backward": [vp, vp, vp, i64, i64, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, i64, vp],
+    "catseg_groupnorm_relu_backward_workspace": [i64, i32],
+    "catseg_l2normalize_backward": [vp, i64, RowMap, vp, i64, vp, i64, RowMap, i32, i64, i64, f32, vp],
+    "catseg_axpby": [vp, vp, vp, i64, f32, f32, vp],
+    "catseg_add_dev_scalar": [vp, i64, vp, vp],
+    "catseg_sum_classes": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
+    "catseg_sum_pixels": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
+    "catseg_avgpool_backward_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
+    "catseg_upsample_ac_backward_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
+    "catseg_convt_gather": [vp, i64, i64, i32, i32, i32, i32, vp, vp],
+    "catseg_window_attention_backward": [C.POINTER(WinAttnBwdArgs), vp],
+    "catseg_linear_attention_backward": [C.POINTER(LinAttnBwdArgs), vp],
+    "catseg_linear_attention_backward_workspace": [i64, i32],
+    "catseg_conv2d_nhwc": [C.POINTER(Conv2dArgs), vp],
+    "catseg_conv2d_wgrad": [C.POINTER(Conv2dArgs), vp],
+    "catseg_conv2d_wgrad_workspace": [C.POINTER(Conv2dArgs)],
+    "catseg_head_conv_backward": [vp, vp, vp, vp, vp, i64, i32, i32, i32, vp, i64, vp],
+    "catseg_head_conv_backward_workspace": [i64, i32, i32, i32],
     "catseg_abi_version": [],
     "catseg_last_error": [],
 }
@@ -198,7 +274,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = (C.c_char_p if name in ("catseg_last_error", "catseg_tuning_list") else
-                      C.c_int64 if name == "catseg_conv3x3_workspace" else C.c_int)
+                      C.c_int64 if name.endswith("_workspace") else C.c_int)
     _lib = lib
     return lib
 

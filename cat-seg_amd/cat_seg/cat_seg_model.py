@@ -17,7 +17,8 @@ deterministically when no checkpoint is given.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from collections import OrderedDict
+from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
 from torch import nn
@@ -27,10 +28,17 @@ from . import ops
 from .arch import CatSegArch, arch_from_cfg
 from .engine import CatSegEngine
 from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401  (registers the head)
+from .params import apply_clip_finetune, attach_parameters
 from .registry import META_ARCH_REGISTRY, build_sem_seg_head, configurable
+from .training import head_train_forward
 from .weights import CLIP as CLIP_PREFIX, synthesize_state_dict
 
 _DTYPES = {"bf16": torch.bfloat16, "f32": torch.float32, "fp32": torch.float32}
+
+
+def _weights_version(params: Iterable[nn.Parameter]) -> int:
+    """Sum of the parameters' in-place version counters: an optimizer step or a copy_ bumps it."""
+    return sum(p._version for p in params)
 
 
 def convert_openai_clip_keys(sd: Dict[str, torch.Tensor], prefix: str = "") -> Dict[str, torch.Tensor]:
@@ -79,8 +87,16 @@ class CATSeg(nn.Module):
         self.compute_dtype = _DTYPES[dtype]
         self.return_all_images = return_all_images
         self.vit_fp8 = bool(vit_fp8)
-        self._sd = synthesize_state_dict(self.arch, seed=synthetic_seed)
+        # the weights as real nn.Parameters under the reference's module names (cat_seg.params):
+        # CLIP under sem_seg_head.predictor.clip_model, the Aggregator under .transformer, and the
+        # guidance upsamplers (cat_seg_model.py:81-82); requires_grad per CLIP_FINETUNE (:57-75)
+        sd = synthesize_state_dict(self.arch, seed=synthetic_seed)
+        attach_parameters(self, sd)
+        apply_clip_finetune(self.sem_seg_head.predictor.clip_model, clip_finetune)
+        # the engines hold kernel-layout copies of the weights, keyed by the parameters' version counters
         self._engine: Optional[CatSegEngine] = None
+        self._train_engine: Optional[CatSegEngine] = None
+        self._engine_key = self._train_engine_key = None
         self.input_format = "RGB"          # read by SemanticSegmentorWithTTA / DefaultPredictor
 
     @classmethod
@@ -112,8 +128,13 @@ class CATSeg(nn.Module):
     def device(self):
         return self.pixel_mean.device
 
+    @property
+    def _sd(self) -> Dict[str, torch.Tensor]:
+        """The weights by reference checkpoint key (detached views of the nn.Parameters)."""
+        return OrderedDict((k, p.detach()) for k, p in self.named_parameters())
+
     def state_dict(self, *args, **kwargs):        # reference checkpoint keys
-        return dict(self._sd)
+        return OrderedDict(self._sd)
 
     def load_state_dict(self, state_dict, strict: bool = True, **_):
         """Reference checkpoint keys (detectron2 `{"model": sd}` accepted, OpenAI `in_proj_weight`
@@ -127,16 +148,18 @@ class CATSeg(nn.Module):
             # module prefix: its keys belong under sem_seg_head.predictor.clip_model.
             prefix = "" if any(k.startswith(CLIP_PREFIX) for k in sd) else CLIP_PREFIX
             sd = convert_openai_clip_keys(sd, prefix)
-        missing = [k for k in self._sd if k not in sd]
-        unexpected = [k for k in sd if k not in self._sd]
+        params = dict(self.named_parameters())
+        missing = [k for k in params if k not in sd]
+        unexpected = [k for k in sd if k not in params]
         if strict and (missing or unexpected):
             raise KeyError(f"load_state_dict: missing {missing[:5]}... unexpected {unexpected[:5]}...")
-        for k in self._sd:
-            if k in sd:
-                if tuple(sd[k].shape) != tuple(self._sd[k].shape):
-                    raise ValueError(f"{k}: shape {tuple(sd[k].shape)} != {tuple(self._sd[k].shape)}")
-                self._sd[k] = sd[k].float().cpu()
-        self._engine = None
+        with torch.no_grad():
+            for k, p in params.items():
+                if k in sd:
+                    if tuple(sd[k].shape) != tuple(p.shape):
+                        raise ValueError(f"{k}: shape {tuple(sd[k].shape)} != {tuple(p.shape)}")
+                    p.copy_(sd[k].to(p.device, p.dtype))
+        self._engine = self._train_engine = None
         return _IncompatibleKeys(list(missing), list(unexpected))
 
     def _engine_device(self) -> torch.device:
@@ -152,11 +175,24 @@ class CATSeg(nn.Module):
         """Built once per resolved device (weights converted / uploaded once), rebuilt only when
         the model moves to another GPU or new weights are loaded."""
         dev = self._engine_device()
-        if self._engine is None or self._engine.device != dev:
+        key = (dev, _weights_version(self.parameters()))
+        if self._engine is None or self._engine_key != key:
             self._engine = CatSegEngine(self.arch, self._sd, dtype=self.compute_dtype, device=dev,
                                         vit_fp8=self.vit_fp8)
+            self._engine_key = key
             self.sem_seg_head.predictor.attach_engine(self._engine)
         return self._engine
+
+    @property
+    def train_engine(self) -> CatSegEngine:
+        """fp32 engine for the training step's CLIP encoders (the reference trains in fp32), rebuilt
+        when a CLIP weight changed (an optimizer step or a checkpoint load bumps its version)."""
+        dev = self._engine_device()
+        key = (dev, _weights_version(self.sem_seg_head.predictor.clip_model.parameters()))
+        if self._train_engine is None or self._train_engine_key != key:
+            self._train_engine = CatSegEngine(self.arch, self._sd, dtype=torch.float32, device=dev)
+            self._train_engine_key = key
+        return self._train_engine
 
     # ------------------------------------------------------------------ forward
     def _batch(self, eng: CatSegEngine, images: List[torch.Tensor]):
@@ -201,21 +237,25 @@ class CATSeg(nn.Module):
 
 
     def _training_loss(self, batched_inputs: List[dict]):
-        """The training branch's loss (cat_seg_model.py:189-203): head logits of the batch, upsampled
-        to the targets' size, BCE-with-logits against one-hot targets (ignore_value rows zero), as
-        {"loss_sem_seg": 0-d tensor} on the device (catseg_bce_onehot_loss).  The loss has a HIP
-        backward to the logits (catseg_bce_onehot_loss_backward, ops.BCEOneHotLoss), but the head and
-        backbone have none, so this loss does not require grad (a training loop's backward() fails
-        loudly); SURVEY §8(f) rank 4 -- the network's backward is outside the inference north star."""
+        """The training branch (cat_seg_model.py:136-146,178-203): fp32 CLIP dense features + hooks and
+        the training class set's text embeddings (re-encoded every step, cat_seg_predictor.py:190-224),
+        the head with its HIP backward (cat_seg.training.head_train_forward), the logits upsampled to
+        the targets' size and BCE-with-logits against one-hot targets (ops.BCEOneHotLoss).
+        Returns {"loss_sem_seg": 0-d tensor}; `loss.backward()` fills `.grad` of every Aggregator and
+        upsampler parameter.  The CLIP encoders run without a graph: their fine-tuned parameters
+        (CLIP_FINETUNE, cat_seg_model.py:57-75) get no gradient from this build."""
+        if self.device.type != "cuda":
+            raise RuntimeError("CATSeg training runs on the GPU: move the model there first (model.to('cuda'))")
+        eng = self.train_engine
+        pred = self.sem_seg_head.predictor
         with torch.no_grad():
-            eng = self.engine
-            # training re-encodes the (training) class set every step, uncached (cat_seg_predictor.py:190-224);
-            # get_text_embeds installs it on the engine, and the next eval call re-installs the test cache
-            self.sem_seg_head.predictor.get_text_embeds()
+            text = eng.encode_text(pred.class_tokens("train"))
             raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in batched_inputs])
-            logits = eng.head_logits(raw, sizes_dev)
-            targets = torch.stack([x["sem_seg"].to(eng.device) for x in batched_inputs], dim=0)
-            loss = ops.bce_onehot_loss(logits.contiguous(), targets, self.sem_seg_head.ignore_value)
+            feats, hooks = eng.encode_image(raw, sizes_dev)
+        params = dict(self.named_parameters())
+        logits = head_train_forward(self.arch, params, feats, hooks, text)
+        targets = torch.stack([x["sem_seg"].to(eng.device) for x in batched_inputs], dim=0)
+        loss = ops.BCEOneHotLoss.apply(logits, targets, self.sem_seg_head.ignore_value)
         return {"loss_sem_seg": loss}
 
     def _forward_sliding(self, batched_inputs: List[dict]):

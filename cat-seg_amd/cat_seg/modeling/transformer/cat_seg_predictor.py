@@ -101,6 +101,12 @@ class CATSegPredictor(nn.Module):
                                "MODEL.CATSEG_HIP.BPE_VOCAB to CLIP's bpe_simple_vocab_16e6.txt.gz")
         return torch.from_numpy(toks)
 
+    def class_tokens(self, mode: str) -> torch.Tensor:
+        """Prompt token ids of the train ("train": TRAIN_CLASS_JSON) or test class set, cached."""
+        if self.tokens[mode] is None:
+            self.tokens[mode] = self.tokenize(self.class_texts if mode == "train" else self.test_class_texts)
+        return self.tokens[mode]
+
     def get_text_embeds(self, classnames=None, templates=None, clip_model=None, prompt=None):
         """Encode + L2-normalize (cat_seg_predictor.py:190-224).  Returns (T, 1, C_o).
 

@@ -1,0 +1,273 @@
+// Training-side GEMMs (the network's backward).
+//
+// catseg_gemm_ex: the general fp32 contraction the backward needs in every operand layout
+//   C[m][n] = alpha * sum_k A(m,k) B(k,n) + beta * C[m][n]
+//   A(m,k) = A[m*a_sm + k*a_sk],  B(k,n) = B[k*b_sk + n*b_sn]
+// with one unit stride per operand (the contiguous dimension is read in 16-byte vectors):
+//   dX = dY . W          (A = dY rows, k-contiguous;   B = W [N_out][K_in], n-contiguous)
+//   dW = dY^T . X        (A = dY^T,    m-contiguous;   B = X rows, n-contiguous; K = rows)
+//   cost-volume grads    (model.py:648-652 einsum backward)
+// so no operand is ever transposed in HBM.  Exact-f32 MFMA (v_mfma_f32_16x16x4_f32, fp32
+// accumulate).  Tall reductions (K = the row count of a weight gradient) split K over
+// grid.y into fp32 partials summed in a fixed order by a second kernel: deterministic,
+// no atomics.
+//
+// catseg_colsum: out[c] = alpha * sum_r x[r][c] (+ beta * out[c]), the bias gradients,
+// two-stage fixed-order reduction.
+#include "common.h"
+#include "capi.h"
+#include "catseg_hip_train.h"
+
+namespace {
+
+constexpr int TBM = 128, TBN = 128, TBK = 16, TNT = 256;
+constexpr int LP = TBM + 16;  // LDS row (one k) of a tile: 144 floats, the 4 k rows of a fragment read on
+                               // disjoint 16-bank groups
+
+// AM: A is m-contiguous (a_sm == 1) else k-contiguous (a_sk == 1).
+// BN: B is n-contiguous (b_sn == 1) else k-contiguous (b_sk == 1).
+template <bool AM, bool BNC>
+__global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ A, int64_t a_sm, int64_t a_sk,
+                                                      const float* __restrict__ B, int64_t b_sk, int64_t b_sn,
+                                                      int64_t M, int64_t N, int64_t K, int64_t k_chunk,
+                                                      float* __restrict__ C, int64_t ldc, float alpha, int beta,
+                                                      float* __restrict__ part, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float As[2][TBK * LP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TBK * LP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntiles = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, ntiles);
+  const int64_t m0 = (int64_t)(lin / tiles_n) * TBM, n0 = (int64_t)(lin % tiles_n) * TBN;
+  const int64_t kb = (int64_t)blockIdx.y * k_chunk;
+  const int64_t ke = kb + k_chunk < K ? kb + k_chunk : K;
+  const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
+
+  // staging: 2 x 16-byte chunks per operand per thread per k-slab
+  float4 ra[2], rb[2];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * TNT;
+      if constexpr (AM) {                      // chunk = 4 consecutive m at one k
+        const int k = c >> 5, m4 = (c & 31) * 4;
+        const int64_t gm = m0 + m4, gk = k0 + k;
+        ra[i] = (gm < M && gk < ke) ? *reinterpret_cast<const float4*>(A + gm + gk * a_sk) : make_float4(0, 0, 0, 0);
+      } else {                                 // chunk = 4 consecutive k at one m
+        const int m = c >> 2, k4 = (c & 3) * 4;
+        const int64_t gm = m0 + m, gk = k0 + k4;
+        ra[i] = (gm < M && gk < ke) ? *reinterpret_cast<const float4*>(A + gm * a_sm + gk) : make_float4(0, 0, 0, 0);
+      }
+      if constexpr (BNC) {
+        const int k = c >> 5, n4 = (c & 31) * 4;
+        const int64_t gn = n0 + n4, gk = k0 + k;
+        rb[i] = (gn < N && gk < ke) ? *reinterpret_cast<const float4*>(B + gn + gk * b_sk) : make_float4(0, 0, 0, 0);
+      } else {
+        const int n = c >> 2, k4 = (c & 3) * 4;
+        const int64_t gn = n0 + n, gk = k0 + k4;
+        rb[i] = (gn < N && gk < ke) ? *reinterpret_cast<const float4*>(B + gn * b_sn + gk) : make_float4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * TNT;
+      if constexpr (AM) {
+        *reinterpret_cast<float4*>(&As[buf][(c >> 5) * LP + (c & 31) * 4]) = ra[i];
+      } else {
+        const int m = c >> 2, k4 = (c & 3) * 4;
+        As[buf][(k4 + 0) * LP + m] = ra[i].x; As[buf][(k4 + 1) * LP + m] = ra[i].y;
+        As[buf][(k4 + 2) * LP + m] = ra[i].z; As[buf][(k4 + 3) * LP + m] = ra[i].w;
+      }
+      if constexpr (BNC) {
+        *reinterpret_cast<float4*>(&Bs[buf][(c >> 5) * LP + (c & 31) * 4]) = rb[i];
+      } else {
+        const int n = c >> 2, k4 = (c & 3) * 4;
+        Bs[buf][(k4 + 0) * LP + n] = rb[i].x; Bs[buf][(k4 + 1) * LP + n] = rb[i].y;
+        Bs[buf][(k4 + 2) * LP + n] = rb[i].z; Bs[buf][(k4 + 3) * LP + n] = rb[i].w;
+      }
+    }
+  };
+
+  // D^T = B^T . A^T: the first MFMA operand is B^T (rows n), the second A^T (columns m), so a
+  // lane ends with 4 consecutive n of one m (16-byte stores)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((ke - kb + TBK - 1) / TBK);
+  const int r = lane & 15, g = lane >> 4;
+  if (nk > 0) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kb + (int64_t)(kt + 1) * TBK);
+    const float* as = As[buf];
+    const float* bs = Bs[buf];
+#pragma unroll
+    for (int kk = 0; kk < TBK; kk += 4) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) av[j] = as[(kk + g) * LP + wm + 16 * j + r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = bs[(kk + g) * LP + wn + 16 * i + r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[m = .. + r][n = .. + 4g .. 4g+3]
+  float* dst = part ? part + (int64_t)blockIdx.y * M * N : C;
+  const int64_t ld = part ? N : ldc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t n = n0 + wn + 16 * i + 4 * g;
+    if (n >= N) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + wm + 16 * j + r;
+      if (m >= M) continue;
+      float4* p = reinterpret_cast<float4*>(dst + m * ld + n);
+      float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      if (!part) {
+        v.x *= alpha; v.y *= alpha; v.z *= alpha; v.w *= alpha;
+        if (beta) { const float4 o = *p; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+      }
+      *p = v;
+    }
+  }
+}
+
+// C[m][n] = alpha * sum_s part[s][m][n] + beta * C[m][n], s in order
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, int64_t M,
+                                                            int64_t N, float* __restrict__ C, int64_t ldc, float alpha,
+                                                            int beta) {
+  const int64_t n4 = N / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * n4) return;
+  const int64_t m = i / n4, n = (i % n4) * 4;
+  float4 s = make_float4(0, 0, 0, 0);
+  for (int z = 0; z < splits; ++z) {
+    const float4 v = *reinterpret_cast<const float4*>(part + ((int64_t)z * M + m) * N + n);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float4* p = reinterpret_cast<float4*>(C + m * ldc + n);
+  s.x *= alpha; s.y *= alpha; s.z *= alpha; s.w *= alpha;
+  if (beta) { const float4 o = *p; s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w; }
+  *p = s;
+}
+
+// Split count: fill ~2 rounds of 256 CUs with tiles x splits, each split at least 16 k-slabs.
+// Depends on the shape only (never the device), so results are reproducible across parts.
+int gemm_ex_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+  if (tiles >= 512) return 1;
+  int64_t s = (512 + tiles - 1) / tiles;
+  const int64_t kmax = K / (TBK * 16);
+  if (s > kmax) s = kmax;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : (int)s;
+}
+
+// column sums: partial[chunk][c] over rows [chunk*CR, (chunk+1)*CR)
+constexpr int CR = 1024;
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t ld, int64_t rows,
+                                                             int64_t cols, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + c;
+  const int64_t r0 = (int64_t)blockIdx.y * CR;
+  const int64_t r1 = r0 + CR < rows ? r0 + CR : rows;
+  float s = 0.f;
+  if (col < cols)
+    for (int64_t rr = r0 + q; rr < r1; rr += 4) s += x[rr * ld + col];
+  red[q][c] = s;
+  __syncthreads();
+  if (q == 0 && col < cols) part[(int64_t)blockIdx.y * cols + col] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int64_t cols,
+                                                           float* __restrict__ out, float alpha, int beta) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int z = 0; z < chunks; ++z) s += part[(int64_t)z * cols + c];
+  out[c] = alpha * s + (beta ? out[c] : 0.f);
+}
+
+}  // namespace
+
+extern "C" int64_t catseg_gemm_ex_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int s = gemm_ex_splits(M, N, K);
+  return s > 1 ? (int64_t)s * M * N * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
+  CATSEG_CHECK(g && g->A && g->B && g->C, "gemm_ex: null pointer");
+  CATSEG_CHECK(g->M > 0 && g->N > 0 && g->K > 0, "gemm_ex: empty shape");
+  const bool am = g->a_sm == 1, ak = g->a_sk == 1, bn = g->b_sn == 1, bk = g->b_sk == 1;
+  CATSEG_CHECK(am || ak, "gemm_ex: A needs a unit stride (a_sm or a_sk == 1)");
+  CATSEG_CHECK(bn || bk, "gemm_ex: B needs a unit stride (b_sn or b_sk == 1)");
+  const bool AM = am && (!ak || (g->M % 4 == 0 && g->a_sk % 4 == 0));
+  const bool BNC = bn && (!bk || (g->N % 4 == 0 && g->b_sk % 4 == 0));
+  // the contiguous extent and the other stride must keep 16-byte vectors aligned
+  if (AM) CATSEG_CHECK(g->M % 4 == 0 && g->a_sk % 4 == 0, "gemm_ex: m-contiguous A needs M % 4 == 0, a_sk % 4 == 0");
+  else CATSEG_CHECK(g->K % 4 == 0 && g->a_sm % 4 == 0, "gemm_ex: k-contiguous A needs K % 4 == 0, a_sm % 4 == 0");
+  if (BNC) CATSEG_CHECK(g->N % 4 == 0 && g->b_sk % 4 == 0, "gemm_ex: n-contiguous B needs N % 4 == 0, b_sk % 4 == 0");
+  else CATSEG_CHECK(g->K % 4 == 0 && g->b_sn % 4 == 0, "gemm_ex: k-contiguous B needs K % 4 == 0, b_sn % 4 == 0");
+  CATSEG_CHECK(g->N % 4 == 0 && g->ldc % 4 == 0 && g->ldc >= g->N, "gemm_ex: C needs N % 4 == 0, ldc % 4 == 0, ldc >= N");
+  CATSEG_CHECK(((uintptr_t)g->A % 16) == 0 && ((uintptr_t)g->B % 16) == 0 && ((uintptr_t)g->C % 16) == 0,
+               "gemm_ex: A, B, C must be 16-byte aligned");
+  const int64_t tm = (g->M + TBM - 1) / TBM, tn = (g->N + TBN - 1) / TBN;
+  CATSEG_CHECK(tm * tn < (1LL << 31), "gemm_ex: too many tiles");
+  const int splits = gemm_ex_splits(g->M, g->N, g->K);
+  const int64_t ws_need = splits > 1 ? (int64_t)splits * g->M * g->N * (int64_t)sizeof(float) : 0;
+  if (splits > 1) CATSEG_CHECK(g->workspace && g->workspace_bytes >= ws_need, "gemm_ex: workspace too small");
+  int64_t kc = (g->K + splits - 1) / splits;
+  kc = (kc + TBK - 1) / TBK * TBK;
+  hipStream_t st = (hipStream_t)stream;
+  float* part = splits > 1 ? (float*)g->workspace : nullptr;
+  dim3 grid((unsigned)(tm * tn), (unsigned)splits);
+#define GEX(a_, b_) hipLaunchKernelGGL((gemm_ex_kernel<a_, b_>), grid, dim3(TNT), 0, st, (const float*)g->A, g->a_sm, \
+                                       g->a_sk, (const float*)g->B, g->b_sk, g->b_sn, g->M, g->N, g->K, kc, (float*)g->C, \
+                                       g->ldc, g->alpha, g->beta, part, (int)tn)
+  if (AM && BNC) GEX(true, true);
+  else if (AM) GEX(true, false);
+  else if (BNC) GEX(false, true);
+  else GEX(false, false);
+#undef GEX
+  if (splits > 1) {
+    const int64_t n = g->M * (g->N / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, splits, g->M,
+                       g->N, (float*)g->C, g->ldc, g->alpha, g->beta);
+  }
+  return catseg_launch_status("gemm_ex");
+}
+
+extern "C" int64_t catseg_colsum_workspace(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return ((rows + CR - 1) / CR) * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int catseg_colsum(const float* x, int64_t ld, int64_t rows, int64_t cols, float* out, float alpha, int beta,
+                             void* workspace, int64_t workspace_bytes, void* stream) {
+  CATSEG_CHECK(x && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
+  const int64_t chunks = (rows + CR - 1) / CR;
+  CATSEG_CHECK(workspace && workspace_bytes >= chunks * cols * (int64_t)sizeof(float), "colsum: workspace too small");
+  CATSEG_CHECK(chunks < 65536, "colsum: too many rows");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)chunks), dim3(256), 0, st, x, ld,
+                     rows, cols, (float*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st,
+                     (const float*)workspace, (int)chunks, cols, out, alpha, beta);
+  return catseg_launch_status("colsum");
+}

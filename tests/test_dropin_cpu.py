@@ -105,7 +105,7 @@ def test_openai_clip_state_dict_is_split_like_the_reference():
     """model_vpt.py:515-531: in_proj_weight -> q/k/v_proj_weight (chunk 3 on dim 0), metadata
     keys dropped; an unprefixed OpenAI dict lands under sem_seg_head.predictor.clip_model."""
     m = build_model(tiny_cfg())
-    ref = m.state_dict()
+    ref = {k: v.clone() for k, v in m.state_dict().items()}     # state_dict() aliases the parameters
     openai = {}
     for k, v in ref.items():
         if not k.startswith(CLIP):
