@@ -143,6 +143,17 @@ class WinAttnBwdArgs(C.Structure):
     ]
 
 
+class AttnBwdArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
+        ("o", vp), ("ld_o", i64),
+        ("dout", vp), ("ld_dout", i64),
+        ("dq", vp), ("dk", vp), ("dv", vp), ("ld_dqkv", i64),
+        ("n_seq", i64), ("seq_len", i32), ("n_heads", i32), ("head_dim", i32), ("scale", f32), ("causal", i32),
+        ("workspace", vp), ("workspace_bytes", i64),
+    ]
+
+
 class LinAttnBwdArgs(C.Structure):
     _fields_ = [
         ("q", vp), ("k", vp), ("v", vp), ("ld_qkv", i64),
@@ -232,12 +243,16 @@ _SIGS = {
     "catseg_l2normalize_backward": [vp, i64, RowMap, vp, i64, vp, i64, RowMap, i32, i64, i64, f32, vp],
     "catseg_axpby": [vp, vp, vp, i64, f32, f32, vp],
     "catseg_add_dev_scalar": [vp, i64, vp, vp],
+    "catseg_scatter_rows": [vp, i64, vp, i64, i64, vp, i64, vp],
+    "catseg_corr_embed_backward_input": [vp, vp, vp, i64, i32, i32, i32, i32, vp],
     "catseg_sum_classes": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
     "catseg_sum_pixels": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
     "catseg_avgpool_backward_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
     "catseg_upsample_ac_backward_rows": [vp, i64, i32, i32, i32, i32, i32, vp, i32, vp],
     "catseg_convt_gather": [vp, i64, i64, i32, i32, i32, i32, vp, vp],
     "catseg_window_attention_backward": [C.POINTER(WinAttnBwdArgs), vp],
+    "catseg_attention_backward": [C.POINTER(AttnBwdArgs), vp],
+    "catseg_attention_backward_workspace": [i64, i32, i32],
     "catseg_linear_attention_backward": [C.POINTER(LinAttnBwdArgs), vp],
     "catseg_linear_attention_backward_workspace": [i64, i32],
     "catseg_conv2d_nhwc": [C.POINTER(Conv2dArgs), vp],

@@ -30,7 +30,7 @@ from .engine import CatSegEngine
 from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401  (registers the head)
 from .params import apply_clip_finetune, attach_parameters
 from .registry import META_ARCH_REGISTRY, build_sem_seg_head, configurable
-from .training import head_train_forward
+from .training import clip_image_train_forward, clip_text_train_forward, head_train_forward
 from .weights import CLIP as CLIP_PREFIX, synthesize_state_dict
 
 _DTYPES = {"bf16": torch.bfloat16, "f32": torch.float32, "fp32": torch.float32}
@@ -185,10 +185,14 @@ class CATSeg(nn.Module):
 
     @property
     def train_engine(self) -> CatSegEngine:
-        """fp32 engine for the training step's CLIP encoders (the reference trains in fp32), rebuilt
-        when a CLIP weight changed (an optimizer step or a checkpoint load bumps its version)."""
+        """fp32 engine for the training step's CLIP encoders (the reference trains in fp32).  With CLIP
+        fine-tuning the autograd path reads the trained block weights from the parameters directly and
+        uses the engine only for the frozen embeddings, so it is rebuilt when a frozen CLIP weight changed
+        (a checkpoint load bumps its version), not after every optimizer step."""
         dev = self._engine_device()
-        key = (dev, _weights_version(self.sem_seg_head.predictor.clip_model.parameters()))
+        clip = self.sem_seg_head.predictor.clip_model
+        trains = any(p.requires_grad for p in clip.parameters())
+        key = (dev, _weights_version(p for p in clip.parameters() if not (trains and p.requires_grad)))
         if self._train_engine is None or self._train_engine_key != key:
             self._train_engine = CatSegEngine(self.arch, self._sd, dtype=torch.float32, device=dev)
             self._train_engine_key = key
@@ -242,17 +246,23 @@ class CATSeg(nn.Module):
         the head with its HIP backward (cat_seg.training.head_train_forward), the logits upsampled to
         the targets' size and BCE-with-logits against one-hot targets (ops.BCEOneHotLoss).
         Returns {"loss_sem_seg": 0-d tensor}; `loss.backward()` fills `.grad` of every Aggregator and
-        upsampler parameter.  The CLIP encoders run without a graph: their fine-tuned parameters
-        (CLIP_FINETUNE, cat_seg_model.py:57-75) get no gradient from this build."""
+        upsampler parameter and of the CLIP parameters CLIP_FINETUNE trains (cat_seg_model.py:57-75:
+        'attention' = the q / v projections of both encoders' blocks): with any of those the CLIP
+        encoders run as autograd Functions too (cat_seg.training.clip_*_train_forward), else without
+        a graph on the engine."""
         if self.device.type != "cuda":
             raise RuntimeError("CATSeg training runs on the GPU: move the model there first (model.to('cuda'))")
         eng = self.train_engine
         pred = self.sem_seg_head.predictor
-        with torch.no_grad():
-            text = eng.encode_text(pred.class_tokens("train"))
-            raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in batched_inputs])
-            feats, hooks = eng.encode_image(raw, sizes_dev)
         params = dict(self.named_parameters())
+        raw, sizes_dev, _ = self._batch(eng, [x["image"] for x in batched_inputs])
+        if any(p.requires_grad for p in pred.clip_model.parameters()):
+            text = clip_text_train_forward(self.arch, params, eng, pred.class_tokens("train"))
+            feats, hooks = clip_image_train_forward(self.arch, params, eng, raw, sizes_dev)
+        else:
+            with torch.no_grad():
+                text = eng.encode_text(pred.class_tokens("train"))
+                feats, hooks = eng.encode_image(raw, sizes_dev)
         logits = head_train_forward(self.arch, params, feats, hooks, text)
         targets = torch.stack([x["sem_seg"].to(eng.device) for x in batched_inputs], dim=0)
         loss = ops.BCEOneHotLoss.apply(logits, targets, self.sem_seg_head.ignore_value)

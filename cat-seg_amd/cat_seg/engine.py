@@ -152,7 +152,7 @@ class CatSegEngine:
         ci, m = wt.shape[:2]
         co = wc.shape[0]
         wt64, wc64 = wt.double(), wc.double()
-        comp = torch.zeros(4, co, 3, 3, ci, dtype=torch.float64)
+        comp = torch.zeros(4, co, 3, 3, ci, dtype=torch.float64, device=wt64.device)
         for a_ in (0, 1):
             for b_ in (0, 1):
                 for dy in (-1, 0, 1):
@@ -393,21 +393,38 @@ class CatSegEngine:
         self._text = _NS(T=T, txn=txn, tgqk=tgqk, tgkt=tgkt or None, src=text)
 
     # ------------------------------------------------------------------ image encoder
-    def encode_image(self, raw: torch.Tensor, sizes: torch.Tensor):
-        """Pre-processing + CLIP dense encoder + hooks.  raw (B,3,Hp,Wp) fp32 0-255 on device,
-        sizes (B,2) int32 valid (h, w).  Returns feats fp32 (B*L, C_o), [hook0, hook1] fp32 (B*L, W)."""
+    def embed_image(self, raw: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+        """cat_seg_model.py:149-154 + VisualTransformer.forward up to the transformer (model_vpt.py:288-300):
+        normalize, pad, resize, patch conv, CLS + pos, ln_pre.  Returns fp32 (B*(1+grid^2), width) rows."""
         a, dev, dt, w = self.arch, self.device, self.dt, self.w
         B = raw.shape[0]
         G2 = a.grid * a.grid
-        Lt = G2 + 1
         W = a.vision_width
         cols = torch.empty(B * G2, w.patch_k, device=dev, dtype=dt)
         ops.preprocess_im2col(raw, sizes, mean=w.pix_mean, std=w.pix_std, res=a.clip_resolution,
                               patch=a.vision_patch, out=cols)
         patches = torch.empty(B * G2, W, device=dev, dtype=_f32)
         ops.gemm(cols, w.patch_w, patches)
-        x = torch.empty(B * Lt, W, device=dev, dtype=_f32)
+        x = torch.empty(B * (G2 + 1), W, device=dev, dtype=_f32)
         ops.vit_embed(patches, w.cls, w.pos, *w.ln_pre, x, B=B, G2=G2, width=W)
+        return x
+
+    def embed_text(self, tokens: torch.Tensor) -> torch.Tensor:
+        """CLIP.encode_text up to the transformer (model_vpt.py:421-427): token + positional embedding.
+        tokens (n, ctx) int32 on the device.  Returns fp32 (n*ctx, text_width) rows."""
+        n, ctx = tokens.shape
+        x = torch.empty(n * ctx, self.arch.text_width, device=self.device, dtype=_f32)
+        ops.token_embed(tokens, self.w.tok_emb, self.w.tpos[:ctx].contiguous(), x)
+        return x
+
+    def encode_image(self, raw: torch.Tensor, sizes: torch.Tensor):
+        """Pre-processing + CLIP dense encoder + hooks.  raw (B,3,Hp,Wp) fp32 0-255 on device,
+        sizes (B,2) int32 valid (h, w).  Returns feats fp32 (B*L, C_o), [hook0, hook1] fp32 (B*L, W)."""
+        a, dev, dt, w = self.arch, self.device, self.dt, self.w
+        B = raw.shape[0]
+        Lt = a.grid * a.grid + 1
+        W = a.vision_width
+        x = self.embed_image(raw, sizes)
         hooks: List[torch.Tensor] = []
         x = self._resblocks(x, w.vblocks[:-1], B, Lt, a.vision_heads, False,
                             hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8, l2s=self.vit_l2s)

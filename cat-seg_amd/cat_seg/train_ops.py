@@ -137,6 +137,24 @@ def axpby(x, y, out, alpha=1.0, beta=1.0):
     return out
 
 
+def scatter_rows(x, idx, out):
+    """out[idx[r]] = x[r] (catseg_scatter_rows); idx int32 on the device."""
+    _chk(x, out)
+    call("catseg_scatter_rows", x.data_ptr(), x.stride(-2), idx.data_ptr(), x.shape[0], x.shape[1], out.data_ptr(),
+         out.stride(-2), _stream())
+    return out
+
+
+def corr_embed_backward_input(dX, weight, dcorr, *, S, H, W):
+    """dcorr [S][H*W] of corr_embed's conv (catseg_corr_embed_backward_input); weight (D, 1, k, k)."""
+    _chk(dX, weight, dcorr)
+    D, _, k, _ = weight.shape
+    with _rec("corr_embed_backward_input", 2 * S * H * W * D * k * k):
+        call("catseg_corr_embed_backward_input", dX.data_ptr(), weight.data_ptr(), dcorr.data_ptr(), S, H, W, D, k,
+             _stream())
+    return dcorr
+
+
 def add_dev_scalar(x, s):
     _chk(x, s)
     call("catseg_add_dev_scalar", x.data_ptr(), x.numel(), s.data_ptr(), _stream())
@@ -197,6 +215,24 @@ def window_attention_backward(qkv, o, dout, dqkv, *, S, img_hw, window, shift, n
     R = S * img_hw[0] * img_hw[1]
     with _rec("window_attention_backward", 8 * R * window * window * D):
         call("catseg_window_attention_backward", a, _stream())
+    return dqkv
+
+
+def attention_backward(qkv, o, dout, dqkv, *, n_seq, seq_len, n_heads, head_dim, scale, causal=False):
+    """dq | dk | dv of the dense (CLIP) attention (catseg_attention_backward); qkv / dqkv are [R][3W]
+    row buffers (q, k, v at column offsets 0, W, 2W)."""
+    _chk(qkv, o, dout, dqkv)
+    W = n_heads * head_dim
+    a = L.AttnBwdArgs()
+    a.q, a.k, a.v, a.ld_qkv = qkv.data_ptr(), qkv[:, W:].data_ptr(), qkv[:, 2 * W:].data_ptr(), qkv.stride(0)
+    a.o, a.ld_o = o.data_ptr(), o.stride(0)
+    a.dout, a.ld_dout = dout.data_ptr(), dout.stride(0)
+    a.dq, a.dk, a.dv, a.ld_dqkv = dqkv.data_ptr(), dqkv[:, W:].data_ptr(), dqkv[:, 2 * W:].data_ptr(), dqkv.stride(0)
+    a.n_seq, a.seq_len, a.n_heads, a.head_dim, a.scale, a.causal = n_seq, seq_len, n_heads, head_dim, scale, int(causal)
+    ws = _ws(L.load().catseg_attention_backward_workspace(n_seq, seq_len, n_heads), qkv.device)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    with _rec("attention_backward", 10 * n_seq * n_heads * seq_len * seq_len * head_dim):
+        call("catseg_attention_backward", a, _stream())
     return dqkv
 
 

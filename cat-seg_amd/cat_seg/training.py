@@ -304,7 +304,8 @@ class CorrEmbedFn(torch.autograd.Function):
         TO.conv2d_wgrad(corr.reshape(-1, 1), dX, dw, S=B * T, H=G, W=G, cin=1, cout=D, ksize=k, ld_x=1)
         dcorr = None
         if ctx.needs_input_grad[0]:
-            raise NotImplementedError("corr_embed input gradient (the CLIP fine-tune path) is not built")
+            dcorr = torch.empty_like(corr)
+            TO.corr_embed_backward_input(dX, w.detach().contiguous(), dcorr, S=B * T, H=G, W=G)
         return dcorr, _conv_dw(dw, w), _colsum(dX), None
 
 
@@ -671,6 +672,268 @@ class HeadConvFn(torch.autograd.Function):
         db = _empty(1, like=x)
         TO.colsum(dl.reshape(-1, 1), db, rows=dl.numel(), cols=1, ld=1)
         return dx, dwt.reshape(3, 3, C).permute(2, 0, 1).reshape(w.shape).contiguous(), db.reshape(1), None, None
+
+
+# ------------------------------------------------------------------------------------- CLIP encoders
+def _ln_bwd(x, w, dh, dx, need_param, acc_dx=True):
+    """LayerNorm backward into dx (accumulated); the parameter gradients only when asked for."""
+    if need_param:
+        dw, db = _empty(x.shape[1], like=x), _empty(x.shape[1], like=x)
+        TO.layernorm_backward(x, w.detach(), dh, dx, acc_dx=acc_dx, dgamma=dw, dbeta=db)
+        return dw, db
+    TO.layernorm_backward(x, w.detach(), dh, dx, acc_dx=acc_dx)
+    return None, None
+
+
+class ClipBlockFn(torch.autograd.Function):
+    """ResidualAttentionBlock.forward (model_vpt.py:208-217): x1 = x + out_proj(MHA(ln_1(x))) with split
+    q/k/v weights + in_proj_bias (model_vpt.py:169-182), x2 = x1 + c_proj(QuickGELU(c_fc(ln_2(x1)))).
+    Rows [n_seq*L][W] token-major per sequence; causal = the text encoder's mask (model_vpt.py:400-406).
+    Every parameter's gradient is computed only when autograd asks for it (CLIP_FINETUNE 'attention'
+    trains the q / v projections only, cat_seg_model.py:57-75)."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, ln1w, ln1b, qw, kw, vw, ipb, ow, ob, ln2w, ln2b, fcw, fcb, pw, pb):
+        n_seq, L_, nh, causal = cfg
+        x = x.contiguous()
+        R, W = x.shape
+        h = torch.empty_like(x)
+        ops.layernorm(x, ln1w.detach(), ln1b.detach(), h)
+        wqkv = torch.cat([qw.detach(), kw.detach(), vw.detach()], 0).contiguous()
+        qkv = _empty(R, 3 * W, like=x)
+        ops.gemm(h, wqkv, qkv, bias=ipb.detach().contiguous())
+        o = torch.empty_like(x)
+        hd = W // nh
+        ops.attention(qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:], o, n_seq=n_seq, seq_len=L_, n_heads=nh,
+                      head_dim=hd, scale=hd ** -0.5, causal=causal)
+        x1 = torch.empty_like(x)
+        ops.gemm(o, ow.detach().contiguous(), x1, bias=ob.detach().contiguous(), res=x)
+        h2 = torch.empty_like(x)
+        ops.layernorm(x1, ln2w.detach(), ln2b.detach(), h2)
+        u = _empty(R, fcw.shape[0], like=x)
+        ops.gemm(h2, fcw.detach().contiguous(), u, bias=fcb.detach().contiguous())
+        a = TO.act_forward(u, L.ACT_QUICKGELU)
+        out = torch.empty_like(x)
+        ops.gemm(a, pw.detach().contiguous(), out, bias=pb.detach().contiguous(), res=x1)
+        ctx.save_for_backward(x, h, qkv, o, x1, h2, u, a, ln1w, qw, kw, vw, ow, ln2w, fcw, pw)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, h, qkv, o, x1, h2, u, a, ln1w, qw, kw, vw, ow, ln2w, fcw, pw = ctx.saved_tensors
+        n_seq, L_, nh, causal = ctx.cfg
+        ni = ctx.needs_input_grad
+        R, W = x.shape
+        dout = dout.contiguous()
+        g = [None] * 16
+        if ni[14]:
+            g[14] = _mm_t(dout, a)
+        if ni[15]:
+            g[15] = _colsum(dout)
+        da = TO.mm(dout, pw.detach())
+        du = TO.act_backward(u, da, L.ACT_QUICKGELU, out=da)
+        if ni[12]:
+            g[12] = _mm_t(du, h2)
+        if ni[13]:
+            g[13] = _colsum(du)
+        dh2 = TO.mm(du, fcw.detach())
+        del da, du
+        dx1 = dout.clone()
+        g[10], g[11] = _ln_bwd(x1, ln2w, dh2, dx1, ni[10] or ni[11])
+        if ni[8]:
+            g[8] = _mm_t(dx1, o)
+        if ni[9]:
+            g[9] = _colsum(dx1)
+        do = TO.mm(dx1, ow.detach())
+        hd = W // nh
+        dqkv = _empty(R, 3 * W, like=x)
+        TO.attention_backward(qkv, o, do, dqkv, n_seq=n_seq, seq_len=L_, n_heads=nh, head_dim=hd, scale=hd ** -0.5,
+                              causal=causal)
+        del do
+        for i, j in ((4, 0), (5, 1), (6, 2)):
+            if ni[i]:
+                g[i] = _mm_t(dqkv[:, j * W:(j + 1) * W], h)
+        if ni[7]:
+            g[7] = _colsum(dqkv)
+        dh = TO.mm(dqkv, torch.cat([qw.detach(), kw.detach(), vw.detach()], 0).contiguous())
+        dx = dx1
+        g[2], g[3] = _ln_bwd(x, ln1w, dh, dx, ni[2] or ni[3])
+        g[0] = dx
+        return tuple(g)
+
+
+class ClipDenseBlockFn(torch.autograd.Function):
+    """ResidualAttentionBlock.forward_dense (model_vpt.py:219-240), the image encoder's last block:
+    v = ln_1(x) . v_proj^T + b_v; vo = out_proj(v) + x[CLS] (the input CLS token of each image, broadcast
+    over its tokens); out = vo + c_proj(QuickGELU(c_fc(ln_2(vo)))).  The q / k projections feed dead
+    outputs in the reference (their out_proj results are discarded): their gradients are zero."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, ln1w, ln1b, qw, kw, vw, ipb, ow, ob, ln2w, ln2b, fcw, fcb, pw, pb):
+        n_img, L_ = cfg
+        x = x.contiguous()
+        R, W = x.shape
+        y = torch.empty_like(x)
+        ops.layernorm(x, ln1w.detach(), ln1b.detach(), y)
+        v = torch.empty_like(x)
+        ops.gemm(y, vw.detach().contiguous(), v, bias=ipb.detach()[2 * W:].contiguous())
+        vo = torch.empty_like(x)
+        ops.gemm(v, ow.detach().contiguous(), vo, bias=ob.detach().contiguous(), add=x, addmap=rowmap(d1=L_, s1=L_))
+        h2 = torch.empty_like(x)
+        ops.layernorm(vo, ln2w.detach(), ln2b.detach(), h2)
+        u = _empty(R, fcw.shape[0], like=x)
+        ops.gemm(h2, fcw.detach().contiguous(), u, bias=fcb.detach().contiguous())
+        a = TO.act_forward(u, L.ACT_QUICKGELU)
+        out = torch.empty_like(x)
+        ops.gemm(a, pw.detach().contiguous(), out, bias=pb.detach().contiguous(), res=vo)
+        ctx.save_for_backward(x, y, v, vo, h2, u, a, ln1w, vw, ow, ln2w, fcw, pw, qw, kw)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y, v, vo, h2, u, a, ln1w, vw, ow, ln2w, fcw, pw, qw, kw = ctx.saved_tensors
+        n_img, L_ = ctx.cfg
+        ni = ctx.needs_input_grad
+        R, W = x.shape
+        dout = dout.contiguous()
+        g = [None] * 16
+        if ni[14]:
+            g[14] = _mm_t(dout, a)
+        if ni[15]:
+            g[15] = _colsum(dout)
+        da = TO.mm(dout, pw.detach())
+        du = TO.act_backward(u, da, L.ACT_QUICKGELU, out=da)
+        if ni[12]:
+            g[12] = _mm_t(du, h2)
+        if ni[13]:
+            g[13] = _colsum(du)
+        dh2 = TO.mm(du, fcw.detach())
+        del da, du
+        dvo = dout.clone()
+        g[10], g[11] = _ln_bwd(vo, ln2w, dh2, dvo, ni[10] or ni[11])
+        if ni[8]:
+            g[8] = _mm_t(dvo, v)
+        if ni[9]:
+            g[9] = _colsum(dvo)
+        dv = TO.mm(dvo, ow.detach())
+        if ni[6]:
+            g[6] = _mm_t(dv, y)
+        if ni[4]:
+            g[4] = torch.zeros_like(qw)
+        if ni[5]:
+            g[5] = torch.zeros_like(kw)
+        if ni[7]:
+            g[7] = torch.zeros(3 * W, device=x.device, dtype=_f32)
+            _colsum(dv, out=g[7][2 * W:])
+        dy = TO.mm(dv, vw.detach())
+        dx = torch.empty_like(x)
+        g[2], g[3] = _ln_bwd(x, ln1w, dy, dx, ni[2] or ni[3], acc_dx=False)
+        # + x[:1]: the CLS row of each image receives the sum over the image's tokens (catseg_sum_classes
+        # over the L token rows of each image, written to row b at stride L*W = the CLS rows)
+        TO.sum_classes(dvo, dx.view(n_img, L_ * W), B=n_img, T=L_, HW=1, C_=W, beta=1)
+        g[0] = dx
+        return tuple(g)
+
+
+class LnProjFn(torch.autograd.Function):
+    """y = LayerNorm(x) @ proj: ln_post + visual.proj (model_vpt.py:306-313) and ln_final +
+    text_projection (model_vpt.py:434-437).  proj [W][C_o]."""
+
+    @staticmethod
+    def forward(ctx, x, lnw, lnb, proj):
+        x = x.contiguous()
+        h = torch.empty_like(x)
+        ops.layernorm(x, lnw.detach(), lnb.detach(), h)
+        y = _empty(x.shape[0], proj.shape[1], like=x)
+        ops.gemm(h, proj.detach().t().contiguous(), y)
+        ctx.save_for_backward(x, h, lnw, proj)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, lnw, proj = ctx.saved_tensors
+        ni = ctx.needs_input_grad
+        dy = dy.contiguous()
+        W, Co = proj.shape
+        pr = proj.detach()
+        dh = _empty(x.shape[0], W, like=x)
+        TO.gemm_ex(dy, Co, 1, pr, 1, Co, dh, M=x.shape[0], N=W, K=Co)        # dh = dy . proj^T
+        dproj = _mm_t(h, dy) if ni[3] else None
+        dx = torch.empty_like(x)
+        dlw, dlb = _ln_bwd(x, lnw, dh, dx, ni[1] or ni[2], acc_dx=False)
+        return dx, dlw, dlb, dproj
+
+
+class EotGatherFn(torch.autograd.Function):
+    """x[arange(n), tokens.argmax(-1)] (model_vpt.py:436): rows [n*ctx][W] -> [n][W]."""
+
+    @staticmethod
+    def forward(ctx, x, tokens, eot_rows):
+        x = x.contiguous()
+        n, cl = tokens.shape
+        out = _empty(n, x.shape[1], like=x)
+        ops.eot_gather(x, tokens, out)
+        ctx.save_for_backward(eot_rows)
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (eot_rows,) = ctx.saved_tensors
+        dx = torch.zeros(ctx.shape, device=dy.device, dtype=_f32)
+        TO.scatter_rows(dy.contiguous(), eot_rows, dx)
+        return dx, None, None
+
+
+def _clip_block_params(P, p):
+    return [P[p + k] for k in ("ln_1.weight", "ln_1.bias", "attn.q_proj_weight", "attn.k_proj_weight",
+                               "attn.v_proj_weight", "attn.in_proj_bias", "attn.out_proj.weight",
+                               "attn.out_proj.bias", "ln_2.weight", "ln_2.bias", "mlp.c_fc.weight", "mlp.c_fc.bias",
+                               "mlp.c_proj.weight", "mlp.c_proj.bias")]
+
+
+def clip_image_train_forward(arch: CatSegArch, P: Dict[str, torch.Tensor], eng, raw: torch.Tensor,
+                             sizes: torch.Tensor):
+    """CLIP.encode_image(dense=True) with the forward hooks (cat_seg_model.py:84-87,144-146,
+    model_vpt.py:288-314), the transformer blocks as autograd Functions.  The embedding (patch conv,
+    class / positional embedding, ln_pre) is outside `transformer` and frozen under every CLIP_FINETUNE
+    mode (cat_seg_model.py:58-75): the engine computes it without a graph.
+    Returns feats [B*(1+G^2)][C_o] and the two hook outputs [B*(1+G^2)][W]."""
+    from .weights import CLIP
+    B = raw.shape[0]
+    L_ = arch.grid * arch.grid + 1
+    x = eng.embed_image(raw, sizes)
+    p = CLIP + "visual."
+    hooks: List[torch.Tensor] = []
+    for i in range(arch.vision_layers - 1):
+        x = ClipBlockFn.apply(x, (B, L_, arch.vision_heads, False),
+                              *_clip_block_params(P, f"{p}transformer.resblocks.{i}."))
+        if i in arch.hook_layers:
+            hooks.append(x)
+    x = ClipDenseBlockFn.apply(x, (B, L_), *_clip_block_params(P, f"{p}transformer.resblocks.{arch.vision_layers - 1}."))
+    feats = LnProjFn.apply(x, P[p + "ln_post.weight"], P[p + "ln_post.bias"], P[p + "proj"])
+    return feats, hooks
+
+
+def clip_text_train_forward(arch: CatSegArch, P: Dict[str, torch.Tensor], eng, tokens: torch.Tensor) -> torch.Tensor:
+    """CLIP.encode_text + L2 norm (model_vpt.py:421-438, cat_seg_predictor.py:214-216) with the causal
+    blocks as autograd Functions, on the first max(EOT)+1 positions (causal: later positions never reach
+    the EOT rows, forward or backward).  tokens (T, ctx) int.  Returns [T][C_o]."""
+    from .weights import CLIP
+    toks = torch.as_tensor(tokens)
+    last = int(toks.argmax(dim=1).max()) + 1
+    toks = toks[:, :last]
+    n, cl = toks.shape
+    eot_rows = (torch.arange(n) * cl + toks.argmax(dim=1)).to(torch.int32)
+    tdev = toks.to(eng.device, torch.int32).contiguous()
+    x = eng.embed_text(tdev)
+    for i in range(arch.text_layers):
+        x = ClipBlockFn.apply(x, (n, cl, arch.text_heads, True), *_clip_block_params(P, f"{CLIP}transformer.resblocks.{i}."))
+    e = EotGatherFn.apply(x, tdev, eot_rows.to(eng.device))
+    t = LnProjFn.apply(e, P[CLIP + "ln_final.weight"], P[CLIP + "ln_final.bias"], P[CLIP + "text_projection"])
+    return L2NormFn.apply(t)
 
 
 # ------------------------------------------------------------------------------------- the head

@@ -210,6 +210,232 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
   }
 }
 
+// ------------------------------------------------------------------------------ dense attention
+// nn.MultiheadAttention of the CLIP blocks (model_vpt.py:169-182,202-206; causal text encoder
+// model_vpt.py:400-406), head_dim 64, fp32.  Three kernels, each one workgroup of 4 waves per
+// (sequence, head, 64-row block):
+//   dense_stats  per query: softmax max m, 1/sum l over the keys, D = dO . O
+//   dense_dkv    waves own 16-key tiles (K, V rows in registers), the query blocks stream through LDS:
+//                dV += P^T dO, dK += scale dS^T Q
+//   dense_dq     waves own 16-query tiles (Q, dO rows in registers), the key blocks stream through LDS:
+//                dQ += scale dS K
+// No atomics: every output element is owned by one wave.  Rows past L are staged as zeros and masked.
+constexpr int HD = 64;          // head_dim
+constexpr int DP = HD + 4;      // LDS pitch: a fragment read's 16 rows x 4 k on 64 distinct banks
+
+struct DenseP {
+  const float* q; const float* k; const float* v; int64_t ld_qkv;
+  const float* o; int64_t ld_o;
+  const float* dout; int64_t ld_dout;
+  float* dq; float* dk; float* dv; int64_t ld_dqkv;
+  float* stats;                  // [n_seq * H * L][3]: m, 1/l, D
+  int64_t n_seq; int L; int H; float scale; int causal;
+};
+
+DEV bool dense_mask_ok(const DenseP& p, int q, int key) {
+  return q < p.L && key < p.L && (!p.causal || key <= q);
+}
+
+// stage rows [r0, r0 + 64) x head columns of `src` into an LDS tile [64][DP] (zeros past L)
+DEV void stage64(float* tile, const float* src, int64_t ld, int64_t row0, int r0, int L, int col) {
+  for (int e = threadIdx.x; e < 64 * (HD / 4); e += 256) {
+    const int i = e / (HD / 4), c = (e % (HD / 4)) * 4;
+    float4 v = make_float4(0, 0, 0, 0);
+    if (r0 + i < L) v = *reinterpret_cast<const float4*>(src + (row0 + r0 + i) * ld + col + c);
+    float* d = tile + i * DP + c;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+}
+
+__global__ __launch_bounds__(256) void dense_stats_kernel(DenseP p) {
+  __shared__ float Kt[64 * DP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int64_t sh = blockIdx.y;
+  const int64_t s = sh / p.H;
+  const int h = (int)(sh % p.H), col = h * HD;
+  const int64_t row0 = s * p.L;
+  const int qi = (blockIdx.x * 4 + wave) * 16 + r;
+  // the lane's query as the B operand: Q[qi][4 t + g], t = 0..15
+  float qf[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) qf[t] = qi < p.L ? p.q[(row0 + qi) * p.ld_qkv + col + 4 * t + g] : 0.f;
+  float m_l = -INFINITY, l_l = 0.f;
+  const int kmax = p.causal ? (blockIdx.x * 4 + 4) * 16 : p.L;   // keys past the block's last query are masked
+  for (int kb = 0; kb < p.L && kb < kmax; kb += 64) {
+    __syncthreads();
+    stage64(Kt, p.k, p.ld_qkv, row0, kb, p.L, col);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc = mfma_f32(Kt[(kt * 16 + r) * DP + 4 * t + g], qf[t], acc);
+      float sc[4], tm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kb + kt * 16 + 4 * g + j;
+        sc[j] = dense_mask_ok(p, qi, key) ? p.scale * acc[j] : -INFINITY;
+        tm = fmaxf(tm, sc[j]);
+      }
+      const float mn = fmaxf(m_l, tm);
+      if (mn != -INFINITY) {
+        float add = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) add += __expf(sc[j] - mn);
+        l_l = l_l * __expf(m_l - mn) + add;
+        m_l = mn;
+      }
+    }
+  }
+  const float M = xrow4_max(m_l);
+  const float Lsum = xrow4_sum(M == -INFINITY ? 0.f : l_l * __expf(m_l - M));
+  // D = dO . O over the lane's 16 columns g*16 .. g*16+15, then across the 4 lanes of the query
+  float d = 0.f;
+  if (qi < p.L) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p.dout + (row0 + qi) * p.ld_dout + col + g * 16 + c);
+      const float4 b = *reinterpret_cast<const float4*>(p.o + (row0 + qi) * p.ld_o + col + g * 16 + c);
+      d += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    }
+  }
+  d = xrow4_sum(d);
+  if (g == 0 && qi < p.L) {
+    float* st = p.stats + ((sh * p.L) + qi) * 3;
+    st[0] = M;
+    st[1] = Lsum > 0.f ? 1.f / Lsum : 0.f;
+    st[2] = d;
+  }
+}
+
+__global__ __launch_bounds__(256) void dense_dkv_kernel(DenseP p) {
+  __shared__ float Qt[64 * DP], Ot[64 * DP];    // Ot holds dO
+  __shared__ float st[64 * 3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int64_t sh = blockIdx.y;
+  const int64_t s = sh / p.H;
+  const int h = (int)(sh % p.H), col = h * HD;
+  const int64_t row0 = s * p.L;
+  const int kt0 = (blockIdx.x * 4 + wave) * 16;
+  const int key = kt0 + r;
+  float kf[16], vf[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    kf[t] = key < p.L ? p.k[(row0 + key) * p.ld_qkv + col + 4 * t + g] : 0.f;
+    vf[t] = key < p.L ? p.v[(row0 + key) * p.ld_qkv + col + 4 * t + g] : 0.f;
+  }
+  f32x4 dV[4], dK[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { dV[e] = f32x4{0.f, 0.f, 0.f, 0.f}; dK[e] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int qstart = p.causal ? (blockIdx.x * 64) / 64 * 64 : 0;   // queries before the block see none of its keys
+  for (int qb = qstart; qb < p.L; qb += 64) {
+    __syncthreads();
+    stage64(Qt, p.q, p.ld_qkv, row0, qb, p.L, col);
+    stage64(Ot, p.dout, p.ld_dout, row0, qb, p.L, col);
+    for (int i = threadIdx.x; i < 64 * 3; i += 256) {
+      const int qq = qb + i / 3;
+      st[i] = qq < p.L ? p.stats[(sh * p.L + qq) * 3 + i % 3] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      f32x4 sa = f32x4{0.f, 0.f, 0.f, 0.f}, pa = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        sa = mfma_f32(Qt[(qs * 16 + r) * DP + 4 * t + g], kf[t], sa);   // S[q][key]
+        pa = mfma_f32(Ot[(qs * 16 + r) * DP + 4 * t + g], vf[t], pa);   // dP[q][key]
+      }
+      float P[4], dS[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ql = qs * 16 + 4 * g + j, qq = qb + ql;
+        const float* sq = st + ql * 3;
+        P[j] = dense_mask_ok(p, qq, key) ? __expf(p.scale * sa[j] - sq[0]) * sq[1] : 0.f;
+        dS[j] = P[j] * (pa[j] - sq[2]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ql = qs * 16 + 4 * g + j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dV[e] = mfma_f32(P[j], Ot[ql * DP + 16 * e + r], dV[e]);
+          dK[e] = mfma_f32(dS[j], Qt[ql * DP + 16 * e + r], dK[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kk = kt0 + 4 * g + j;
+    if (kk >= p.L) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      p.dv[(row0 + kk) * p.ld_dqkv + col + 16 * e + r] = dV[e][j];
+      p.dk[(row0 + kk) * p.ld_dqkv + col + 16 * e + r] = p.scale * dK[e][j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void dense_dq_kernel(DenseP p) {
+  __shared__ float Kt[64 * DP], Vt[64 * DP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int64_t sh = blockIdx.y;
+  const int64_t s = sh / p.H;
+  const int h = (int)(sh % p.H), col = h * HD;
+  const int64_t row0 = s * p.L;
+  const int qt0 = (blockIdx.x * 4 + wave) * 16;
+  const int qi = qt0 + r;
+  float qf[16], of[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    qf[t] = qi < p.L ? p.q[(row0 + qi) * p.ld_qkv + col + 4 * t + g] : 0.f;
+    of[t] = qi < p.L ? p.dout[(row0 + qi) * p.ld_dout + col + 4 * t + g] : 0.f;
+  }
+  float mq = 0.f, lq = 0.f, Dq = 0.f;
+  if (qi < p.L) {
+    const float* sq = p.stats + (sh * p.L + qi) * 3;
+    mq = sq[0]; lq = sq[1]; Dq = sq[2];
+  }
+  f32x4 dQ[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dQ[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kend = p.causal ? (blockIdx.x * 4 + 4) * 16 : p.L;
+  for (int kb = 0; kb < p.L && kb < kend; kb += 64) {
+    __syncthreads();
+    stage64(Kt, p.k, p.ld_qkv, row0, kb, p.L, col);
+    stage64(Vt, p.v, p.ld_qkv, row0, kb, p.L, col);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f32x4 sa = f32x4{0.f, 0.f, 0.f, 0.f}, pa = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        sa = mfma_f32(Kt[(ks * 16 + r) * DP + 4 * t + g], qf[t], sa);   // S^T[key][q]
+        pa = mfma_f32(Vt[(ks * 16 + r) * DP + 4 * t + g], of[t], pa);   // dP^T[key][q]
+      }
+      float dS[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = kb + ks * 16 + 4 * g + j;
+        dS[j] = dense_mask_ok(p, qi, kk) ? __expf(p.scale * sa[j] - mq) * lq * (pa[j] - Dq) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kl = ks * 16 + 4 * g + j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dQ[e] = mfma_f32(dS[j], Kt[kl * DP + 16 * e + r], dQ[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int qq = qt0 + 4 * g + j;
+    if (qq >= p.L) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p.dq[(row0 + qq) * p.ld_dqkv + col + 16 * e + r] = p.scale * dQ[e][j];
+  }
+}
+
 // ------------------------------------------------------------------------------ linear attention
 constexpr int LD = 32;     // head_dim
 constexpr int LCH = 32;    // tokens staged per chunk
@@ -448,4 +674,32 @@ extern "C" int catseg_linear_attention_backward(const CatsegLinAttnBwdArgs* p, v
     hipLaunchKernelGGL(lin_pad_reduce_kernel, dim3(1), dim3(256), 0, st, (const float*)p->workspace, npix, p->dk_pad,
                        p->dv_pad);
   return catseg_launch_status("linear_attention_backward");
+}
+
+extern "C" int64_t catseg_attention_backward_workspace(int64_t n_seq, int seq_len, int n_heads) {
+  return n_seq > 0 && seq_len > 0 && n_heads > 0 ? n_seq * n_heads * seq_len * 3 * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int catseg_attention_backward(const CatsegAttnBwdArgs* a, void* stream) {
+  CATSEG_CHECK(a && a->q && a->k && a->v && a->o && a->dout && a->dq && a->dk && a->dv, "attention_backward: null");
+  CATSEG_CHECK(a->head_dim == HD, "attention_backward: head_dim must be 64");
+  CATSEG_CHECK(a->n_seq > 0 && a->seq_len > 0 && a->n_heads > 0, "attention_backward: bad shape");
+  CATSEG_CHECK(a->ld_qkv % 4 == 0 && a->ld_o % 4 == 0 && a->ld_dout % 4 == 0 && a->ld_dqkv % 4 == 0,
+               "attention_backward: strides % 4");
+  CATSEG_CHECK(a->n_seq * a->n_heads < 65536, "attention_backward: at most 65535 (sequence, head) pairs");
+  const int64_t need = a->n_seq * a->n_heads * a->seq_len * 3 * (int64_t)sizeof(float);
+  CATSEG_CHECK(a->workspace && a->workspace_bytes >= need, "attention_backward: workspace too small");
+  DenseP p;
+  p.q = (const float*)a->q; p.k = (const float*)a->k; p.v = (const float*)a->v; p.ld_qkv = a->ld_qkv;
+  p.o = (const float*)a->o; p.ld_o = a->ld_o;
+  p.dout = (const float*)a->dout; p.ld_dout = a->ld_dout;
+  p.dq = (float*)a->dq; p.dk = (float*)a->dk; p.dv = (float*)a->dv; p.ld_dqkv = a->ld_dqkv;
+  p.stats = (float*)a->workspace;
+  p.n_seq = a->n_seq; p.L = a->seq_len; p.H = a->n_heads; p.scale = a->scale; p.causal = a->causal;
+  const dim3 grid((unsigned)((a->seq_len + 63) / 64), (unsigned)(a->n_seq * a->n_heads));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL(dense_dkv_kernel, grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL(dense_dq_kernel, grid, dim3(256), 0, st, p);
+  return catseg_launch_status("attention_backward");
 }

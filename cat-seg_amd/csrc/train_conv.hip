@@ -335,6 +335,54 @@ __global__ __launch_bounds__(256) void head_final_kernel(const float* __restrict
   dw[i] = s;
 }
 
+// ------------------------------------------------------------------------------ corr_embed input grad
+// dcorr[s][q] = sum_{tap, co} dX[s][q - off(tap)][co] w[co][tap]: the 7x7 conv's data gradient with a
+// single output channel (an MFMA tile would be 1/16 used).  One workgroup per slice; 32-channel chunks
+// of the slice's dX staged in LDS, the weights transposed to [tap][co] beside them.
+constexpr int CEC = 32, CEP = CEC + 4;
+__global__ __launch_bounds__(256) void corr_dgrad_kernel(const float* __restrict__ dX, const float* __restrict__ w,
+                                                         float* __restrict__ dcorr, int H, int W, int D, int k) {
+  extern __shared__ float sm[];
+  const int HW = H * W, taps = k * k, pad = k / 2;
+  float* xs = sm;                        // [HW][CEP]
+  float* wt = sm + HW * CEP;             // [taps][CEC]
+  const int64_t s = blockIdx.x;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < D; c0 += CEC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < HW * (CEC / 4); e += 256) {
+      const int p = e / (CEC / 4), c = (e % (CEC / 4)) * 4;
+      *reinterpret_cast<float4*>(xs + p * CEP + c) =
+          *reinterpret_cast<const float4*>(dX + (s * HW + p) * (int64_t)D + c0 + c);
+    }
+    for (int e = threadIdx.x; e < taps * CEC; e += 256) {
+      const int co = e / taps, t = e % taps;
+      wt[t * CEC + co] = w[(int64_t)(c0 + co) * taps + t];
+    }
+    __syncthreads();
+    int slot = 0;
+    for (int q = threadIdx.x; q < HW; q += 256, ++slot) {
+      const int y = q / W, x = q % W;
+      float a = 0.f;
+      for (int t = 0; t < taps; ++t) {
+        const int py = y - (t / k - pad), px = x - (t % k - pad);
+        if (py < 0 || py >= H || px < 0 || px >= W) continue;
+        const float* xr = xs + (py * W + px) * CEP;
+        const float* wr = wt + t * CEC;
+#pragma unroll
+        for (int c = 0; c < CEC; c += 4) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + c);
+          const float4 wv = *reinterpret_cast<const float4*>(wr + c);
+          a += xv.x * wv.x + xv.y * wv.y + xv.z * wv.z + xv.w * wv.w;
+        }
+      }
+      if (slot < 4) acc[slot] += a;
+    }
+  }
+  int slot = 0;
+  for (int q = threadIdx.x; q < HW && slot < 4; q += 256, ++slot) dcorr[s * HW + q] = acc[slot];
+}
+
 int head_grid(int64_t S, int H, int W, int C) {
   const int64_t items = S * H * W * (C / 4);
   const int64_t wg = (items + 256 * 16 - 1) / (256 * 16);
@@ -400,6 +448,26 @@ extern "C" int catseg_conv2d_wgrad(const CatsegConv2dArgs* a, void* stream) {
                        splits, n, (float*)a->dw, a->alpha, a->beta);
   }
   return catseg_launch_status("conv2d_wgrad");
+}
+
+extern "C" int catseg_corr_embed_backward_input(const float* dX, const float* weight, float* dcorr, int64_t S, int H,
+                                                int W, int D, int ksize, void* stream) {
+  CATSEG_CHECK(dX && weight && dcorr && S > 0 && H > 0 && W > 0 && ksize > 0 && ksize % 2 == 1,
+               "corr_embed_backward_input: bad args");
+  CATSEG_CHECK(D % CEC == 0, "corr_embed_backward_input: hidden must be a multiple of 32");
+  CATSEG_CHECK((int64_t)H * W <= 4 * 256, "corr_embed_backward_input: at most 1024 pixels per slice");
+  const size_t sh = ((size_t)H * W * CEP + (size_t)ksize * ksize * CEC) * sizeof(float);
+  CATSEG_CHECK(sh <= 160 * 1024, "corr_embed_backward_input: slice too large for LDS");
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_dgrad_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    configured = true;
+  }
+  CATSEG_CHECK(S < (1LL << 31), "corr_embed_backward_input: too many slices");
+  hipLaunchKernelGGL(corr_dgrad_kernel, dim3((unsigned)S), dim3(256), sh, (hipStream_t)stream, dX, weight, dcorr, H, W, D,
+                     ksize);
+  return catseg_launch_status("corr_embed_backward_input");
 }
 
 extern "C" int64_t catseg_head_conv_backward_workspace(int64_t S, int H, int W, int C) {

@@ -418,6 +418,15 @@ __global__ __launch_bounds__(256) void axpby_kernel(const float* __restrict__ x,
   }
   reinterpret_cast<float4*>(out)[i] = v;
 }
+// out[idx[r]][c] = in[r][c] (the EOT gather's backward, model_vpt.py:436)
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restrict__ in, int64_t ld_in,
+                                                           const int32_t* __restrict__ idx, int64_t rows, int64_t cols,
+                                                           float* __restrict__ out, int64_t ld_out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols, c = i % cols;
+  out[(int64_t)idx[r] * ld_out + c] = in[r * ld_in + c];
+}
 __global__ __launch_bounds__(256) void add_dev_scalar_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ s) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) x[i] += *s;
@@ -578,6 +587,14 @@ extern "C" int catseg_axpby(const float* x, const float* y, float* out, int64_t 
   CATSEG_CHECK(x && out && n > 0 && n % 4 == 0, "axpby: bad args (n % 4 == 0)");
   hipLaunchKernelGGL(axpby_kernel, dim3(blocks(n / 4)), dim3(256), 0, (hipStream_t)stream, x, y, out, n / 4, alpha, beta);
   return catseg_launch_status("axpby");
+}
+
+extern "C" int catseg_scatter_rows(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols,
+                                   float* out, int64_t ld_out, void* stream) {
+  CATSEG_CHECK(in && idx && out && rows > 0 && cols > 0 && ld_in >= cols && ld_out >= cols, "scatter_rows: bad args");
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(blocks(rows * cols)), dim3(256), 0, (hipStream_t)stream, in, ld_in, idx,
+                     rows, cols, out, ld_out);
+  return catseg_launch_status("scatter_rows");
 }
 
 extern "C" int catseg_add_dev_scalar(float* x, int64_t n, const float* s, void* stream) {

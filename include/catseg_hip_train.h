@@ -89,6 +89,10 @@ int catseg_l2normalize_backward(const float* x, int64_t ld_x, CatsegRowMap inmap
  * gradient sums.  catseg_add_dev_scalar — x[i] += *s (s a device scalar: the head conv's bias
  * without a host read, model.py:634). */
 int catseg_axpby(const float* x, const float* y, float* out, int64_t n, float alpha, float beta, void* stream);
+/* catseg_scatter_rows — out[idx[r]] = in[r] (fp32 rows): the backward of the text encoder's EOT gather
+ * (model_vpt.py:436, catseg_eot_gather). */
+int catseg_scatter_rows(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols, float* out,
+                        int64_t ld_out, void* stream);
 int catseg_add_dev_scalar(float* x, int64_t n, const float* s, void* stream);
 
 /* ---------------------------------------------------------------------------
@@ -132,6 +136,22 @@ typedef struct {
 } CatsegWinAttnBwdArgs;
 int catseg_window_attention_backward(const CatsegWinAttnBwdArgs* args, void* stream);
 
+/* catseg_attention_backward — dense softmax attention backward for catseg_attention mode 0 rows
+ * (the CLIP blocks' nn.MultiheadAttention, model_vpt.py:169-182,202-206; causal = the text encoder's
+ * triu mask, model_vpt.py:400-406): sequence s, token i at row s*seq_len + i; q/k/v the forward
+ * projections (scale not applied), o the forward output, dout = dL/do.  Writes dq, dk, dv.
+ * head_dim 64.  workspace >= catseg_attention_backward_workspace bytes (softmax statistics). */
+typedef struct {
+  const void* q; const void* k; const void* v; int64_t ld_qkv;
+  const void* o; int64_t ld_o;
+  const void* dout; int64_t ld_dout;
+  void* dq; void* dk; void* dv; int64_t ld_dqkv;
+  int64_t n_seq; int seq_len; int n_heads; int head_dim; float scale; int causal;
+  void* workspace; int64_t workspace_bytes;
+} CatsegAttnBwdArgs;
+int catseg_attention_backward(const CatsegAttnBwdArgs* args, void* stream);
+int64_t catseg_attention_backward_workspace(int64_t n_seq, int seq_len, int n_heads);
+
 /* catseg_linear_attention_backward — LinearAttention backward (model.py:256-286) for the rows of
  * catseg_linear_attention: dy = dL/d(attention output).  Writes dq, dk, dv; with n_pad > 0 also
  * dk_pad / dv_pad [heads*head_dim] = the gradients of the padding tokens' constant k / v projections
@@ -172,6 +192,12 @@ typedef struct {
 int catseg_conv2d_nhwc(const CatsegConv2dArgs* args, void* stream);
 int catseg_conv2d_wgrad(const CatsegConv2dArgs* args, void* stream);
 int64_t catseg_conv2d_wgrad_workspace(const CatsegConv2dArgs* args);
+
+/* catseg_corr_embed_backward_input — the data gradient of corr_embed's Conv2d(1, D, k, pad k/2)
+ * (model.py:613,654-659): dcorr[s][q] = sum_{tap, co} dX[s][q - tap][co] weight[co][tap]; dX rows
+ * [S*H*W][D], weight [D][k*k] (the Conv2d weight (D, 1, k, k)), dcorr [S][H*W].  D % 32 == 0. */
+int catseg_corr_embed_backward_input(const float* dX, const float* weight, float* dcorr, int64_t S, int H, int W,
+                                     int D, int ksize, void* stream);
 
 /* catseg_head_conv_backward — the head conv C -> 1 (3x3, model.py:634,679) backward: x the forward
  * input [S][H][W][C], dlogits [S][H][W]; dx [S][H][W][C] (overwritten), dw [9][C] (tap-major,

@@ -56,18 +56,50 @@ def head_keys(sd):
     return [k for k in sd if k.startswith(AGG) or k.startswith("upsample")]
 
 
-def compare_grads(got, ref, keys, tol=TOL):
-    worst = []
+def _rel(a, r):
+    return ((a.detach().double().cpu().reshape(r.shape) - r).abs().max() / (r.abs().max() + 1e-30)).item()
+
+
+def compare_grads(got, ref, keys, tol=TOL, ref32=None, report=None):
+    """Per parameter: max |got - ref| / max |ref| <= max(tol, 8 x the error of torch's own fp32
+    autograd of the same reference graph, ref32) — a gradient whose reference value is a heavily
+    cancelled sum is as sensitive to fp32 rounding in the reference's arithmetic as in ours.
+    The Swin `attn.k.bias` gradients are zero in exact arithmetic (a key bias adds q . b_k to every
+    score of a query row, which softmax cancels, model.py:86-114): they are checked against the
+    k weight's gradient scale instead (|got| <= 1e-5 max |d k.weight|)."""
+    rows = []
     for k in keys:
+        if ref[k] is None:          # a parameter off the graph (padding tokens at T == pad_len; the dense
+            # block's q / k projections, whose outputs the reference discards: zeros here)
+            assert got[k] is None or not got[k].abs().max().item(), f"{k}: gradient where the reference has none"
+            continue
         r = ref[k].double()
         gk = got[k]
         assert gk is not None, f"{k}: no gradient"
-        gk = gk.detach().double().cpu().reshape(r.shape)
-        e = ((gk - r).abs().max() / (r.abs().max() + 1e-30)).item()
-        worst.append((e, k))
-    worst.sort(reverse=True)
-    assert worst[0][0] <= tol, f"worst gradients (rel err, key): {worst[:5]}"
-    return worst
+        if ".swin_block." in k and k.endswith("attn.k.bias"):
+            wscale = ref[k[:-len("bias")] + "weight"].double().abs().max().item()
+            a = gk.detach().double().abs().max().item()
+            assert a <= 1e-5 * wscale, (k, a, wscale)
+            continue
+        e = _rel(gk, r)
+        e32 = _rel(ref32[k], r) if ref32 is not None else 0.0
+        rows.append((e, e32, k))
+    rows.sort(reverse=True)
+    if report is not None:
+        report.extend(rows)
+    bad = [x for x in rows if x[0] > max(tol, 8 * x[1])]
+    assert not bad, f"gradients off (rel err hip, rel err torch-fp32, key): {bad[:5]}; worst {rows[:3]}"
+    return rows
+
+
+def _write_report(name, rows):
+    d = os.environ.get("CATSEG_GRAD_REPORT")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"grad_{name}.txt"), "w") as f:
+            f.write("rel_err_hip\trel_err_torch_fp32\tparameter\n")
+            for e, e32, k in rows:
+                f.write(f"{e:.3e}\t{e32:.3e}\t{k}\n")
 
 
 CASES = {
@@ -92,15 +124,21 @@ def test_head_backward_matches_oracle_autograd(case):
     targets = torch.randint(0, T, (B, R, R), generator=gen, dtype=torch.int32)
     targets[:, :3] = 255
 
-    # reference: fp64 autograd through the oracle
-    sd64 = {k: v.double().requires_grad_(k in keys) for k, v in sd.items()}
-    ref_logits = ref_head(arch, sd64, feats, [h.permute(1, 0, 2) for h in hooks], text)
-    rl = ref_loss(ref_logits, targets)
-    rl.backward()
-    ref_grads = {k: sd64[k].grad for k in keys}
+    # reference: fp64 autograd through the oracle (and the same graph in torch fp32, the noise floor)
+    ref_grads = {}
+    for dt, store in ((torch.float64, ref_grads), (torch.float32, {})):
+        sdr = {k: v.detach().clone().to(dt).requires_grad_(k in keys) for k, v in sd.items()}
+        lg = ref_head(arch, sdr, feats.to(dt), [h.permute(1, 0, 2).to(dt) for h in hooks], text.to(dt))
+        l_ = ref_loss(lg, targets)
+        l_.backward()
+        store.update({k: sdr[k].grad for k in keys})
+        if dt == torch.float64:
+            ref_logits, rl = lg, l_
+        else:
+            ref32 = store
 
     # HIP: fp32 on the device, autograd Functions backed by the training kernels
-    P = {k: v.cuda().requires_grad_(k in keys) for k, v in sd.items()}
+    P = {k: v.detach().cuda().requires_grad_(k in keys) for k, v in sd.items()}
     logits = head_train_forward(arch, P, feats.reshape(B * L_, -1).float().cuda(),
                                 [h.reshape(B * L_, -1).float().cuda() for h in hooks], text.float().cuda())
     assert logits.shape == (B, T, R, R) and logits.requires_grad
@@ -108,7 +146,11 @@ def test_head_backward_matches_oracle_autograd(case):
     loss = ops.BCEOneHotLoss.apply(logits, targets.cuda(), 255)
     assert abs(loss.item() - rl.item()) <= 1e-5 * abs(rl.item())
     loss.backward()
-    compare_grads({k: P[k].grad for k in keys}, ref_grads, keys)
+    rows = []
+    try:
+        compare_grads({k: P[k].grad for k in keys}, ref_grads, keys, ref32=ref32, report=rows)
+    finally:
+        _write_report(case, rows)
 
 
 def test_head_backward_is_deterministic():
@@ -124,11 +166,65 @@ def test_head_backward_is_deterministic():
     targets = torch.randint(0, T, (B, 96, 96), generator=gen, dtype=torch.int32).cuda()
     runs = []
     for _ in range(2):
-        P = {k: v.cuda().requires_grad_(k in keys) for k, v in sd.items()}
+        P = {k: v.detach().cuda().requires_grad_(k in keys) for k, v in sd.items()}
         ops.BCEOneHotLoss.apply(head_train_forward(arch, P, feats, hooks, text), targets, 255).backward()
         runs.append({k: P[k].grad.clone() for k in keys})
     for k in keys:
         assert torch.equal(runs[0][k], runs[1][k]), k
+
+
+def test_clip_encoders_backward_matches_oracle_autograd():
+    """The CLIP image encoder (blocks, forward_dense, hooks, ln_post @ proj) and the causal text encoder
+    (EOT gather, ln_final @ text_projection, L2 norm) as autograd Functions, every transformer-block
+    parameter trained (CLIP_FINETUNE "full", cat_seg_model.py:70-71), vs fp64 autograd through the
+    oracle (model_vpt.py:202-240,288-314,421-438) on a random linear loss of every output."""
+    from cat_seg.engine import CatSegEngine
+    from cat_seg.training import clip_image_train_forward, clip_text_train_forward
+    from cat_seg.weights import CLIP
+    arch = TINY
+    sd = synthesize_state_dict(arch, seed=0)
+    keys = [k for k in sd if k.startswith(CLIP) and "transformer.resblocks" in k]
+    gen = torch.Generator().manual_seed(4)
+    B, T = 2, 7
+    ims = [torch.randint(0, 256, (3, 384, 384), generator=gen).float() for _ in range(B)]
+    toks = torch.zeros(T, arch.context_length, dtype=torch.long)
+    toks[:, 0] = 1
+    for t in range(T):
+        n = 3 + t % 4
+        toks[t, 1:n] = torch.randint(2, 400, (n - 1,), generator=gen)
+        toks[t, n] = arch.vocab_size - 1
+    L_ = arch.grid ** 2 + 1
+    rf = torch.randn(B, L_, arch.embed_dim, generator=gen, dtype=torch.float64)
+    rh = [torch.randn(B, L_, arch.vision_width, generator=gen, dtype=torch.float64) for _ in range(2)]
+    rt = torch.randn(T, arch.embed_dim, generator=gen, dtype=torch.float64)
+
+    refs = {}
+    for dt in (torch.float64, torch.float32):
+        sdr = {k: v.detach().clone().to(dt).requires_grad_(k in keys) for k, v in sd.items()}
+        clip_ims, _ = O.preprocess(arch, ims)
+        feats, hooks = O.encode_image_dense(arch, sdr, clip_ims.to(dt))
+        text = O.text_embeds(arch, sdr, toks)[:, 0]
+        loss = (feats * rf.to(dt)).sum() + (text * rt.to(dt)).sum()
+        for h, r in zip(hooks, rh):
+            loss = loss + (h.permute(1, 0, 2) * r.to(dt)).sum()
+        loss.backward()
+        refs[dt] = {k: sdr[k].grad for k in keys}
+
+    eng = CatSegEngine(arch, sd, dtype=torch.float32, device="cuda")
+    P = {k: v.detach().cuda().requires_grad_(k in keys) for k, v in sd.items()}
+    raw = torch.stack(ims).cuda()
+    sizes = torch.tensor([[384, 384]] * B, dtype=torch.int32, device="cuda")
+    feats, hooks = clip_image_train_forward(arch, P, eng, raw, sizes)
+    text = clip_text_train_forward(arch, P, eng, toks)
+    loss = (feats * rf.reshape(B * L_, -1).float().cuda()).sum() + (text * rt.float().cuda()).sum()
+    for h, r in zip(hooks, rh):
+        loss = loss + (h * r.reshape(B * L_, -1).float().cuda()).sum()
+    loss.backward()
+    rows = []
+    try:
+        compare_grads({k: P[k].grad for k in keys}, refs[torch.float64], keys, ref32=refs[torch.float32], report=rows)
+    finally:
+        _write_report("clip_encoders", rows)
 
 
 def test_catseg_train_step_backward_and_optimizer():
@@ -152,23 +248,34 @@ def test_catseg_train_step_backward_and_optimizer():
     assert loss.requires_grad
     loss.backward()
     named = dict(model.named_parameters())
-    keys = head_keys(named)
+    # CLIP_FINETUNE "attention": the head, the upsamplers and the CLIP q / v projections train
+    keys = [k for k, p in named.items() if p.requires_grad]
+    assert any("visual.transformer.resblocks.0.attn.q_proj_weight" in k for k in keys)
+    assert any(k.endswith("clip_model.transformer.resblocks.0.attn.v_proj_weight") for k in keys)
     assert all(named[k].grad is not None for k in keys)
-    assert all(named[k].grad is None for k in named if k.startswith("sem_seg_head.predictor.clip_model"))
+    assert all(named[k].grad is None for k in named if k not in keys)
 
-    # reference from the same images, every stage in fp64 (CLIP frozen: no_grad)
+    # reference from the same images, every stage in fp64 (CLIP q / v with grad), and torch fp32
     arch = model.arch
-    sd64 = {k: v.detach().cpu().double() for k, v in named.items()}
-    for k in keys:
-        sd64[k].requires_grad_(True)
-    with torch.no_grad():
+    refs = {}
+    for dt in (torch.float64, torch.float32):
+        sdr = {k: v.detach().cpu().clone().to(dt) for k, v in named.items()}
+        for k in keys:
+            sdr[k].requires_grad_(True)
         clip_ims, _ = O.preprocess(arch, ims)
-        feats, hooks = O.encode_image_dense(arch, sd64, clip_ims.double())
-        text = O.text_embeds(arch, sd64, toks)[:, 0]
-    rl = ref_loss(ref_head(arch, sd64, feats, hooks, text), torch.stack(sems).int())
-    assert abs(loss.item() - rl.item()) <= 1e-5 * abs(rl.item())
-    rl.backward()
-    compare_grads({k: named[k].grad for k in keys}, {k: sd64[k].grad for k in keys}, keys)
+        feats, hooks = O.encode_image_dense(arch, sdr, clip_ims.to(dt))
+        text = O.text_embeds(arch, sdr, toks)[:, 0]
+        rl = ref_loss(ref_head(arch, sdr, feats, hooks, text), torch.stack(sems).int())
+        rl.backward()
+        refs[dt] = ({k: sdr[k].grad for k in keys}, rl.item())
+    rl64 = refs[torch.float64][1]
+    assert abs(loss.item() - rl64) <= 1e-5 * abs(rl64)
+    rows = []
+    try:
+        compare_grads({k: named[k].grad for k in keys}, refs[torch.float64][0], keys, ref32=refs[torch.float32][0],
+                      report=rows)
+    finally:
+        _write_report("catseg_train_step", rows)
 
     # an optimizer step on the real parameters; eval then runs on the new weights
     before = model.engine.w.ce_b.clone()

@@ -229,6 +229,38 @@ def test_window_attention_backward(shift):
     close(dqkv[:, 2 * D:], vr.grad)
 
 
+@pytest.mark.parametrize("n_seq,L_,nh,causal", [(2, 577, 3, False), (5, 14, 2, True), (1, 77, 2, True),
+                                                 (3, 50, 1, False)])
+def test_dense_attention_backward(n_seq, L_, nh, causal):
+    """CLIP nn.MultiheadAttention core (model_vpt.py:202-206; causal triu -inf mask, model_vpt.py:400-406)."""
+    hd = 64
+    W = nh * hd
+    R = n_seq * L_
+    qkv = g(R, 3 * W, seed=40)
+    dout = g(R, W, seed=41)
+    qr, kr, vr = (qkv[:, i * W:(i + 1) * W].clone().requires_grad_(True) for i in range(3))
+
+    def heads(t):
+        return t.reshape(n_seq, L_, nh, hd).permute(0, 2, 1, 3)
+
+    s = (heads(qr) * hd ** -0.5) @ heads(kr).transpose(-2, -1)
+    if causal:
+        s = s + torch.full((L_, L_), float("-inf"), dtype=s.dtype).triu_(1)
+    o = (s.softmax(-1) @ heads(vr)).permute(0, 2, 1, 3).reshape(R, W)
+    o.backward(dout)
+    qkvd = dev(qkv)
+    od = torch.empty(R, W, device=DEV)
+    ops.attention(qkvd[:, :W], qkvd[:, W:2 * W], qkvd[:, 2 * W:], od, n_seq=n_seq, seq_len=L_, n_heads=nh,
+                  head_dim=hd, scale=hd ** -0.5, causal=causal)
+    close(od, o, 1e-5)
+    dqkv = torch.empty(R, 3 * W, device=DEV)
+    TO.attention_backward(qkvd, od, dev(dout), dqkv, n_seq=n_seq, seq_len=L_, n_heads=nh, head_dim=hd,
+                          scale=hd ** -0.5, causal=causal)
+    close(dqkv[:, :W], qr.grad)
+    close(dqkv[:, W:2 * W], kr.grad)
+    close(dqkv[:, 2 * W:], vr.grad)
+
+
 @pytest.mark.parametrize("T,n_pad", [(20, 236), (171, 85), (256, 0)])
 def test_linear_attention_backward(T, n_pad):
     B, HW, nh, D = 2, 9, 4, 128

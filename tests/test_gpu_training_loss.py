@@ -61,9 +61,10 @@ def test_catseg_training_forward_loss():
     model.train()
     losses = model(batch)
     assert set(losses) == {"loss_sem_seg"} and losses["loss_sem_seg"].dim() == 0
-    assert not losses["loss_sem_seg"].requires_grad
+    assert losses["loss_sem_seg"].requires_grad      # the head's HIP backward (tests/test_gpu_train_head.py)
     model.eval()
     eng = model.engine
+    model.sem_seg_head.predictor.get_text_embeds()      # the eval engine's class set (= the train tokens here)
     raw, sizes_dev, _ = model._batch(eng, [b["image"] for b in batch])
     with torch.no_grad():
         logits = eng.head_logits(raw, sizes_dev).cpu()
@@ -90,8 +91,9 @@ def test_train_eval_alternation_keeps_the_test_class_set():
     sem = torch.randint(0, len(train_tok), im.shape[-2:], generator=torch.Generator().manual_seed(3))
     model.train()
     loss = model([{"image": im, "sem_seg": sem}])["loss_sem_seg"].item()
-    eng = model.engine
-    assert eng.text_source().shape[0] == len(train_tok)
+    # the train-class logits from the training step's own fp32 engine
+    eng = model.train_engine
+    eng.set_text(eng.encode_text(torch.as_tensor(train_tok)))
     raw, sizes_dev, _ = model._batch(eng, [im])
     with torch.no_grad():
         train_logits = eng.head_logits(raw, sizes_dev).cpu()
