@@ -244,6 +244,9 @@ _SIGS = {
     "catseg_axpby": [vp, vp, vp, i64, f32, f32, vp],
     "catseg_add_dev_scalar": [vp, i64, vp, vp],
     "catseg_scatter_rows": [vp, i64, vp, i64, i64, vp, i64, vp],
+    "catseg_adamw_chunks": [vp, i32],
+    "catseg_adamw_chunk_table": [vp, i32, vp],
+    "catseg_adamw_step": [vp, vp, i64, f32, f32, f32, f32, vp, vp, i64, vp],
     "catseg_corr_embed_backward_input": [vp, vp, vp, i64, i32, i32, i32, i32, vp],
     "catseg_sum_classes": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
     "catseg_sum_pixels": [vp, i64, i64, i32, i64, i32, vp, i64, i32, vp],
@@ -289,7 +292,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = (C.c_char_p if name in ("catseg_last_error", "catseg_tuning_list") else
-                      C.c_int64 if name.endswith("_workspace") else C.c_int)
+                      C.c_int64 if name.endswith("_workspace") or name == "catseg_adamw_chunks" else C.c_int)
     _lib = lib
     return lib
 

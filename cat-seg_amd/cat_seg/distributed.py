@@ -98,6 +98,60 @@ def gather_logits_async(local: torch.Tensor, out: torch.Tensor, group=None):
     return dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
 
 
+def allreduce_gradients(params, group=None, bucket_mb: float = 64.0) -> int:
+    """Data-parallel gradient averaging of the training step (what DistributedDataParallel does for
+    train_net.py's `Trainer`, train_net.py:309-311 / detectron2 create_ddp_model): the `.grad` of every
+    parameter that has one, flattened into fp32 buckets of <= bucket_mb, one all_reduce(SUM) per bucket
+    (RCCL over xGMI on the GPU box; gloo stages device buckets through the host), divided by the world
+    size and copied back.  Buckets are filled in parameter order, so every rank reduces the same
+    buckets.  Returns the number of collectives issued (0 at world size 1)."""
+    rank, world = _world(group)
+    if world == 1:
+        return 0
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return 0
+    limit = max(1, int(bucket_mb * (1 << 20)) // 4)
+    buckets, cur, n = [], [], 0
+    for g in grads:
+        if cur and n + g.numel() > limit:
+            buckets.append(cur)
+            cur, n = [], 0
+        cur.append(g)
+        n += g.numel()
+    buckets.append(cur)
+    for b in buckets:
+        flat = torch.cat([g.reshape(-1).float() for g in b])
+        if flat.is_cuda and dist.get_backend(group) == "gloo":
+            h = flat.cpu()
+            dist.all_reduce(h, group=group)
+            flat.copy_(h)
+        else:
+            dist.all_reduce(flat, group=group)
+        flat.div_(world)
+        o = 0
+        for g in b:
+            g.copy_(flat[o:o + g.numel()].view_as(g))
+            o += g.numel()
+    return len(buckets)
+
+
+def create_ddp_model(model: torch.nn.Module, **kwargs) -> torch.nn.Module:
+    """detectron2 create_ddp_model as train_net.py's Trainer uses it: torch DistributedDataParallel around
+    the model when the world size is > 1 (gradients all-reduced in buckets during backward), else the
+    model itself.  The CAT-Seg parameters are plain nn.Parameters whose gradients come from the HIP
+    autograd Functions, so DDP's gradient hooks see them like any module's."""
+    _, world = _world(None)
+    if world == 1:
+        return model
+    from torch.nn.parallel import DistributedDataParallel
+    dev = next(model.parameters()).device
+    if dev.type == "cuda":
+        kwargs.setdefault("device_ids", [dev.index if dev.index is not None else torch.cuda.current_device()])
+    kwargs.setdefault("broadcast_buffers", False)
+    return DistributedDataParallel(model, **kwargs)
+
+
 def run_sharded(forward: Callable[[Sequence], torch.Tensor], items: Sequence, group=None) -> torch.Tensor:
     """Run `forward` on this rank's slice of `items` and all-gather the results.
 

@@ -207,6 +207,29 @@ int catseg_head_conv_backward(const float* x, const float* dlogits, const float*
                               int64_t S, int H, int W, int C, void* workspace, int64_t workspace_bytes, void* stream);
 int64_t catseg_head_conv_backward_workspace(int64_t S, int H, int W, int C);
 
+/* ---------------------------------------------------------------------------
+ * Optimizer: torch.optim.AdamW inside the reference's FullModelGradientClippingOptimizer
+ * (train_net.py:228-253), every parameter of every group in one multi-tensor pass.
+ * ------------------------------------------------------------------------- */
+/* One parameter tensor (fp32, contiguous, numel elements) and its group's hyper-parameters; an array
+ * of these lives in DEVICE memory.  bias_correction1/2 = 1 - beta^step of the step being taken. */
+typedef struct {
+  float* param; float* grad; float* exp_avg; float* exp_avg_sq;
+  int64_t numel;
+  float lr; float weight_decay; float bias_correction1; float bias_correction2;
+} CatsegAdamWTensor;
+/* The chunk table: 4096-element chunks over the tensors, entry = (tensor << 40) | chunk; host-side,
+ * computed once per parameter set (catseg_adamw_chunks gives its length). */
+int64_t catseg_adamw_chunks(const int64_t* numels, int n_tensors);
+int catseg_adamw_chunk_table(const int64_t* numels, int n_tensors, int64_t* table);
+/* catseg_adamw_step — with max_grad_norm > 0: total = ||all grads||_2 (fixed-order sum), coef =
+ * min(1, max_grad_norm / (total + 1e-6)), grads scaled in place (torch.nn.utils.clip_grad_norm_),
+ * norm_out[0] = total, norm_out[1] = coef (device floats; workspace >= n_chunks floats); then the AdamW
+ * update of torch.optim.AdamW (decoupled weight decay, lerp first moment, bias-corrected step). */
+int catseg_adamw_step(const CatsegAdamWTensor* tensors, const int64_t* chunk_table, int64_t n_chunks, float beta1,
+                      float beta2, float eps, float max_grad_norm, float* norm_out, void* workspace,
+                      int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -135,3 +135,39 @@ def test_gloo_world2_async_gather_ring():
 def test_world1_is_identity():
     x = torch.randn(3, 4)
     assert D.gather_logits(x, 3) is x
+
+
+def _grad_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gen = torch.Generator().manual_seed(100 + rank)
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in ((300, 7), (11,), (5, 5, 5), (4096,))]
+        for p in params:
+            p.grad = torch.randn(p.shape, generator=gen)
+        params[1].grad = None                        # a parameter without a gradient stays untouched
+        n = D.allreduce_gradients(params, bucket_mb=0.01)
+        torch.save({"n": n, "grads": [None if p.grad is None else p.grad for p in params]},
+                   os.path.join(out_dir, f"g{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_gradients_world2_gloo():
+    """Data-parallel gradient averaging (the DDP all-reduce of train_net.py:309-311): every rank ends
+    with the mean of the ranks' gradients, bucketed (three buckets at 10 KB), parameters without a
+    gradient untouched."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_grad_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"g{k}.pt"), weights_only=True) for k in range(2)]
+    assert r[0]["n"] == r[1]["n"] >= 2
+    for k in range(2):
+        expect = []
+        for rank in range(2):
+            gen = torch.Generator().manual_seed(100 + rank)
+            expect.append([torch.randn(s, generator=gen) for s in ((300, 7), (11,), (5, 5, 5), (4096,))])
+        for i in (0, 2, 3):
+            mean = (expect[0][i] + expect[1][i]) / 2
+            assert torch.allclose(r[k]["grads"][i], mean, atol=1e-6)
+        assert r[k]["grads"][1] is None
+    assert all(torch.equal(a, b) for a, b in zip(r[0]["grads"][:1], r[1]["grads"][:1]))

@@ -326,6 +326,44 @@ def test_conv2d_forward_dgrad_wgrad(cin, cout, k, relu):
         close(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, cin))
 
 
+@pytest.mark.parametrize("max_norm", [0.0, 0.01, 1e6])
+def test_adamw_matches_torch(max_norm):
+    """cat_seg.optim.AdamW (catseg_adamw_step) vs torch.optim.AdamW behind the reference's
+    FullModelGradientClippingOptimizer (train_net.py:228-253), 4 steps, three parameter groups."""
+    from cat_seg.optim import AdamW
+    gen = torch.Generator().manual_seed(50)
+    shapes = [(128, 256), (5000,), (3, 4, 5), (1,), (4097,)]
+    base = [torch.randn(*s, generator=gen) for s in shapes]
+    grads = [[torch.randn(*s, generator=gen) for s in shapes] for _ in range(4)]
+    mine = [b.clone().cuda().requires_grad_(True) for b in base]
+    ref = [b.clone().cuda().requires_grad_(True) for b in base]
+
+    def groups(ps):
+        return [{"params": ps[:2], "lr": 2e-4, "weight_decay": 1e-4}, {"params": ps[2:4], "lr": 2e-6,
+                "weight_decay": 0.0}, {"params": ps[4:], "lr": 1e-3, "weight_decay": 0.05}]
+
+    o1 = AdamW(groups(mine), 2e-4, max_grad_norm=max_norm)
+    o2 = torch.optim.AdamW(groups(ref), 2e-4)
+    for st in range(4):
+        for p, q, gr in zip(mine, ref, grads[st]):
+            p.grad = gr.cuda()
+            q.grad = gr.cuda()
+        o1.step()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(ref, max_norm)
+        o2.step()
+        for p, q in zip(mine, ref):
+            assert (p - q).abs().max().item() <= 1e-6 * q.abs().max().item() + 1e-7
+            assert (p.grad - q.grad).abs().max().item() <= 1e-6 * q.grad.abs().max().item()
+    if max_norm > 0:
+        tot = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g.cuda()) for g in grads[-1]]))
+        assert abs(o1.last_grad_norm[0].item() - tot.item()) <= 1e-5 * tot.item()
+    # the state layout is torch's: the two optimizers' state dicts load into each other
+    sd = o1.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+    o2.load_state_dict(sd)
+
+
 def test_head_conv_backward():
     S, H, W, C = 5, 32, 24, 32
     x = g(S, C, H, W, seed=32)

@@ -116,6 +116,24 @@ def test_clip_finetune_requires_grad_like_the_reference():
     assert not any(p.requires_grad for n, p in m.named_parameters() if "clip_model" in n)
 
 
+def test_build_optimizer_groups_and_adamw_chunk_table():
+    """cat_seg.optim.build_optimizer gives the same per-parameter groups as the restated reference rules;
+    the fused AdamW's chunk table covers every element once (host code)."""
+    from cat_seg.optim import AdamW, build_optimizer, chunk_table
+    cfg = tiny_cfg(**{"SOLVER.CLIP_GRADIENTS.ENABLED": "True", "SOLVER.CLIP_GRADIENTS.CLIP_TYPE": "full_model",
+                      "SOLVER.CLIP_GRADIENTS.CLIP_VALUE": "0.01", "SOLVER.BASE_LR": "0.0002"})
+    m = build_model(cfg)
+    opt = build_optimizer(cfg, m)
+    assert isinstance(opt, AdamW) and opt.max_grad_norm == 0.01
+    ref = build_optimizer_groups(m, base_lr=2e-4, wd=cfg.SOLVER.WEIGHT_DECAY, wd_norm=cfg.SOLVER.WEIGHT_DECAY_NORM,
+                                 wd_embed=cfg.SOLVER.WEIGHT_DECAY_EMBED, clip_mult=cfg.SOLVER.CLIP_MULTIPLIER)
+    assert len(opt.param_groups) == len(ref)
+    for a, b in zip(opt.param_groups, ref):
+        assert a["params"][0] is b["params"][0] and a["lr"] == b["lr"] and a["weight_decay"] == b["weight_decay"]
+    t = chunk_table([4096, 1, 8193])
+    assert t.tolist() == [0, 1 << 40, (2 << 40), (2 << 40) | 1, (2 << 40) | 2]
+
+
 def test_reference_build_optimizer_rules_apply():
     m = build_model(tiny_cfg())
     groups = build_optimizer_groups(m)
