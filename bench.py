@@ -148,8 +148,6 @@ def main():
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}")
     cfg = CONFIGS[args.config]
     cfg5 = args.config == 5
-    if cfg5 and world > 1:
-        raise SystemExit("--config 5 is a single-GPU measurement (the scaling runs use the headline config)")
     arch = cfg["arch"]
     B = args.batch or cfg["B"]
     T = args.classes or cfg["T"]
@@ -167,11 +165,15 @@ def main():
     raw = synthetic_batch(rank, B, S, dev)
     sizes = torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev)
     out = None if cfg5 else torch.empty(B, T, R, R, device=dev)
-    gsize = eng.SLIDE_OUT if cfg5 else 4 * arch.grid
+    gsize = 4 * arch.grid
+    rows = 5 * B if cfg5 else B          # gathered logit planes per rank (config 5: 4 tiles + global per image)
 
     def step():
-        if cfg5:      # crops + head + Fold merge -> 640² probabilities at the image size (sem_seg_postprocess)
-            return eng.forward_sliding(raw, sizes, [(S, S)] * B)[0]
+        if cfg5:
+            # crops + head + Fold merge -> 640² probabilities at the image size (sem_seg_postprocess is the
+            # identity at 640²); the crops' logits (5 per image, 96²) are what N > 1 all-gathers
+            _, crop_logits = eng.sliding_logits(raw, sizes, return_crops=True)
+            return crop_logits
         logits = eng.head_logits(raw, sizes)
         ops.postprocess(logits, out, crop=(min(logits.shape[-2], R), min(logits.shape[-1], R)))
         return logits
@@ -186,7 +188,7 @@ def main():
     overlap = world > 1 and backend == "nccl"
     nbuf = 2 if world > 1 else 1
     graphs, g_logits = [], []
-    gathered = ([torch.empty(world * B, T, gsize, gsize, device=dev) for _ in range(nbuf)]
+    gathered = ([torch.empty(world * rows, T, gsize, gsize, device=dev) for _ in range(nbuf)]
                 if world > 1 else None)
     works = [None] * nbuf
     torch.cuda.synchronize()
@@ -248,7 +250,7 @@ def main():
                     raw.copy_(synthetic_batch(r, B, S, dev))
                     lg = forward_once(last)
                     torch.cuda.synchronize()
-                    ok = ok and torch.equal(ref[r * B:(r + 1) * B], lg)
+                    ok = ok and torch.equal(ref[r * rows:(r + 1) * rows], lg)
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
             flag = flag.to(dev) if backend == "nccl" else flag
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -377,7 +379,10 @@ def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
         roof = {"bound": "hbm", "kernel": top, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), **common}
     # tflops: executed work / time; ref_tflops: the reference's count for the module / time
-    # (differs where the build skips padding rows, per-class guidance halves or ConvT maps)
+    # (differs where the build skips padding rows, per-class guidance halves or ConvT maps).
+    # Per family the floor: floor_ms = max(executed flops / the dtype's dense MFMA peak, algorithmic
+    # bytes / 8 TB/s) and floor_frac = floor_ms / ms (1.0 = at the roof); traffic_mb_per_launch from the
+    # newest same-config PMC summary (tools/pmc_traffic.py) where one exists for the family.
     kern = {}
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"]):
         e = {"launches": v["launches"], "ms": round(v["ms"], 3)}
@@ -387,6 +392,17 @@ def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
                 e["ref_tflops"] = round(v["ref_flops"] / (v["ms"] / 1e3) / 1e12, 2)
         if v["bytes"]:
             e["gbs"] = round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)
+        peak = (PEAK_FP8_TFLOPS if k == "gemm_fp8" else PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else
+                PEAK_F32_TFLOPS)
+        floor_s = max(v["flops"] / (peak * 1e12), v["bytes"] / (PEAK_HBM_GBS * 1e9))
+        e["gflop"] = round(v["flops"] / 1e9, 3)
+        e["algorithmic_mb"] = round(v["bytes"] / 1e6, 3)
+        e["floor_ms"] = round(floor_s * 1e3, 4)
+        e["floor_frac"] = round(floor_s * 1e3 / v["ms"], 4) if v["ms"] > 0 else None
+        e["floor_bound"] = "mfma" if v["flops"] / (peak * 1e12) >= v["bytes"] / (PEAK_HBM_GBS * 1e9) else "hbm"
+        t, _, _ = pmc_traffic(k, bench_config)
+        if t:
+            e["traffic_mb_per_launch"] = round(t / 1e6, 3)
         kern[k] = e
     return roof, kern
 

@@ -720,11 +720,13 @@ class CatSegEngine:
     # ------------------------------------------------------------------ sliding-window eval
     SLIDE_KERNEL, SLIDE_OVERLAP, SLIDE_OUT = 384, 0.333, 640      # cat_seg_model.py:158-160
 
-    def sliding_logits(self, raw: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+    def sliding_logits(self, raw: torch.Tensor, sizes: torch.Tensor, return_crops: bool = False):
         """TEST.SLIDING_WINDOW branch up to the merged probabilities (cat_seg_model.py:156-176,204-213),
         for every image of the batch: 640² resize, Unfold(384, stride 256) tiles + the 384² global
         crop through the head, then sigmoid / Fold / average.  raw (N,3,Hc,Wc) fp32 0-255 canvas,
-        sizes (N,2) int32 valid (h, w).  Returns fp32 probabilities (N, T0, 640, 640)."""
+        sizes (N,2) int32 valid (h, w).  Returns fp32 probabilities (N, T0, 640, 640), and with
+        return_crops also the crops' head logits (N*(nb²+1), T0, 96, 96) (what a batch-sharded run
+        all-gathers: 640² probabilities are 7x larger)."""
         k, res = self.SLIDE_KERNEL, self.SLIDE_OUT
         stride = int(k * (1 - self.SLIDE_OVERLAP))
         nb = (res - k) // stride + 1
@@ -735,7 +737,7 @@ class CatSegEngine:
         logits = self.head_logits(crops, csz)                      # (N*(nb²+1), T0, 96, 96)
         merged = torch.empty(N, logits.shape[1], res, res, device=self.device, dtype=_f32)
         ops.sliding_merge(logits, merged, kernel=k, stride=stride, out_res=res)
-        return merged
+        return (merged, logits) if return_crops else merged
 
     def forward_sliding(self, raw: torch.Tensor, sizes: torch.Tensor, out_hw) -> List[torch.Tensor]:
         """Sliding-window probabilities resized to out_hw[n] = (height, width) per image

@@ -39,6 +39,16 @@ def test_bench_two_ranks_gloo_on_one_gpu():
     assert line["value"] > 0 and line["steps"] == 3
 
 
+@pytest.mark.timeout(500)
+def test_bench_config5_two_ranks_gloo_on_one_gpu():
+    """Config 5 (sliding 640², fp8 ViT GEMMs) batch-sharded over 2 ranks: every rank all-gathers the
+    crops' head logits (5 planes per image), rank 0 re-runs both ranks' images bit for bit."""
+    line = _bench("--config", "5", "--gpus", "2", "--batch", "1", "--classes", "64", "--steps", "2", "--warmup", "1",
+                  "--cpu-images", "0", "--no-roofline", "--backend", "gloo")
+    assert line["n_gpus"] == 2 and line["gather_matches_1gpu"] is True
+    assert line["config"]["bench_config"] == 5 and line["config"]["global_batch"] == 2
+
+
 @pytest.mark.timeout(400)
 def test_bench_one_gpu_line_contract():
     line = _bench("--steps", "2", "--warmup", "1", "--cpu-images", "0")
@@ -49,3 +59,7 @@ def test_bench_one_gpu_line_contract():
     assert line["metric"].startswith("images/sec @ ViT-L/14 336², 150 classes, bs=8")
     r = line["roofline"]
     assert r["bound"] in ("mfma", "hbm") and 0 < r["frac"] < 1 and r["lib_sha16"]
+    # every kernel family carries its floor (max of MFMA time and byte time) and the fraction reached
+    for k, e in line["kernels"].items():
+        assert e["floor_ms"] >= 0 and e["floor_bound"] in ("mfma", "hbm"), k
+        assert e["floor_frac"] is None or 0 <= e["floor_frac"] <= 1.5, (k, e)

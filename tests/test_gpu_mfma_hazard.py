@@ -1,5 +1,5 @@
 """The gfx950 MFMA operand cases the shipped kernels rely on, on the device:
-tools/probe_mfma_overlap.hip (built by `make -C cat-seg_amd/csrc`) compares every case with the same
+tools/probe_mfma_overlap.hip (built by `make -C cat-seg_amd/csrc probe`, which __graft_entry__.build() runs) compares every case with the same
 products on disjoint, generously padded registers, bit for bit, alone and beside partner waves that
 saturate the matrix pipe.  Every K=32 case -- destination partially over srcA / srcB / srcC, the
 chained-srcC LDS write-after-read pattern -- and the K=16 cases without a pending srcC dependency must
@@ -19,7 +19,7 @@ PROBE = os.path.join(ROOT, "tools", "bin", "probe_mfma_overlap")
 
 def test_mfma_operand_cases_the_kernels_use():
     if not os.path.exists(PROBE):
-        pytest.fail("tools/bin/probe_mfma_overlap missing: build with make -C cat-seg_amd/csrc")
+        pytest.fail("tools/bin/probe_mfma_overlap missing: build with make -C cat-seg_amd/csrc probe")
     out = subprocess.run([PROBE, "4"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     rows = re.findall(r"^(plain|hammer)\s+(.+?)\s+mismatching words (\d+) of (\d+)$", out.stdout, re.M)
