@@ -153,3 +153,23 @@ def test_reference_build_optimizer_rules_apply():
     before = copy.deepcopy(dict(m.named_parameters())[agg + "head.bias"].detach())
     opt.step()
     assert not torch.equal(dict(m.named_parameters())[agg + "head.bias"].detach(), before)
+
+
+def test_custom_ops_are_registered_with_meta_kernels():
+    """torch.ops.catseg.* exist and their fake kernels give the output shape / dtype on meta tensors
+    (no GPU: the dispatcher routes meta inputs to the registered fake implementation)."""
+    from cat_seg import custom_ops  # noqa: F401
+    C = torch.ops.catseg
+    A = torch.empty(300, 256, device="meta", dtype=torch.bfloat16)
+    W = torch.empty(128, 256, device="meta", dtype=torch.bfloat16)
+    out = C.gemm(A, W, None, 0, None, 0)
+    assert out.shape == (300, 128) and out.dtype == torch.float32 and out.device.type == "meta"
+    ln = C.layernorm(torch.empty(7, 64, device="meta"), torch.empty(64, device="meta"),
+                     torch.empty(64, device="meta"), 1e-5, 1)
+    assert ln.dtype == torch.bfloat16 and ln.shape == (7, 64)
+    pp = C.postprocess(torch.empty(2, 5, 96, 96, device="meta"), 336, 300, 96, 96)
+    assert pp.shape == (2, 5, 336, 300)
+    att = C.attention(torch.empty(154, 384, device="meta"), 2, 77, 2, True, 0, 0, 0, 0, 0)
+    assert att.shape == (154, 128)
+    mm = C.mm(torch.empty(10, 20, device="meta"), torch.empty(10, 30, device="meta"), True, False)
+    assert mm.shape == (20, 30)
