@@ -32,7 +32,7 @@ def test_catseg_forward_matches_golden(dtype):
     tol = 1e-3 if dtype == "f32" else 2e-2
     assert err.max().item() < tol, err.max().item()
     # every image vs the oracle (the reference returns image 0 only; the batched boundary returns all)
-    sd = model.state_dict()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}   # the oracle runs on the host
     text = O.text_embeds(model.arch, sd, torch.from_numpy(g["tokens"]))
     ref = O.catseg_forward(model.arch, sd, [{"image": im} for im in imgs], text, all_images=True)
     for r, o in zip(ref, out):
