@@ -237,9 +237,10 @@ _SIGS = {
     "catseg_layernorm_backward_workspace": [i64, i64],
     "catseg_act_forward": [vp, vp, i64, i32, vp],
     "catseg_act_backward": [vp, vp, vp, i64, i32, vp],
-    "catseg_groupnorm_stats_rows": [vp, i64, i64, i32, i32, f32, vp, vp, vp],
+    "catseg_groupnorm_stats_rows": [vp, i64, i64, i32, i32, f32, vp, vp, vp, i64, vp],
+    "catseg_groupnorm_stats_rows_workspace": [i64, i64, i32, i32],
     "catseg_groupnorm_relu_backward": [vp, vp, vp, i64, i64, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, i64, vp],
-    "catseg_groupnorm_relu_backward_workspace": [i64, i32],
+    "catseg_groupnorm_relu_backward_workspace": [i64, i64, i32],
     "catseg_l2normalize_backward": [vp, i64, RowMap, vp, i64, vp, i64, RowMap, i32, i64, i64, f32, vp],
     "catseg_axpby": [vp, vp, vp, i64, f32, f32, vp],
     "catseg_add_dev_scalar": [vp, i64, vp, vp],

@@ -105,19 +105,20 @@ def act_backward(u, dy, act, out=None):
 
 def groupnorm_stats_rows(x, S, HW, C_, cpg, mean, rstd, eps=1e-5):
     _chk(x, mean, rstd)
+    ws = _ws(L.load().catseg_groupnorm_stats_rows_workspace(S, HW, C_, cpg), x.device)
     with _rec("groupnorm_stats_rows", 0, 4 * x.numel()):
         call("catseg_groupnorm_stats_rows", x.data_ptr(), S, HW, C_, cpg, eps, mean.data_ptr(), rstd.data_ptr(),
-             _stream())
+             None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel() * 4, _stream())
     return mean, rstd
 
 
 def groupnorm_relu_backward(x, dy, dx, *, S, HW, C_, cpg, mean, rstd, gamma, beta, dgamma, dbeta, acc_param=False):
     _chk(x, dy, dx, mean, rstd, gamma, beta, dgamma, dbeta)
-    ws = _ws(L.load().catseg_groupnorm_relu_backward_workspace(S, C_), x.device)
-    with _rec("groupnorm_relu_backward", 0, 4 * x.numel() * 5):
+    ws = _ws(L.load().catseg_groupnorm_relu_backward_workspace(S, HW, C_), x.device)
+    with _rec("groupnorm_relu_backward", 0, 4 * x.numel() * 5):   # x, dy read twice, dx written
         call("catseg_groupnorm_relu_backward", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), S, HW, C_, cpg,
              mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
-             int(acc_param), ws.data_ptr(), ws.numel() * 4, _stream())
+             int(acc_param), None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel() * 4, _stream())
     return dx
 
 

@@ -178,29 +178,90 @@ int gemm_ex_splits(int64_t M, int64_t N, int64_t K) {
   return s < 1 ? 1 : (int)s;
 }
 
-// column sums: partial[chunk][c] over rows [chunk*CR, (chunk+1)*CR)
-constexpr int CR = 1024;
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t ld, int64_t rows,
-                                                             int64_t cols, float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + c;
-  const int64_t r0 = (int64_t)blockIdx.y * CR;
-  const int64_t r1 = r0 + CR < rows ? r0 + CR : rows;
-  float s = 0.f;
-  if (col < cols)
-    for (int64_t rr = r0 + q; rr < r1; rr += 4) s += x[rr * ld + col];
-  red[q][c] = s;
-  __syncthreads();
-  if (q == 0 && col < cols) part[(int64_t)blockIdx.y * cols + col] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+// column sums.  The rows are cut into `chunks` ranges of cr rows; one 256-thread workgroup per (column
+// block, chunk): QW consecutive column vectors (V floats: 16-byte loads when the layout allows) x
+// 256/QW row lanes, so a wave reads whole row segments; the row lanes reduce by a fixed tree and
+// write part[chunk][col].  The final pass sums the chunks per column with 16 lanes and a fixed tree.
+// chunks and cr depend on (rows, cols) only: deterministic.
+constexpr int COLSUM_MAX_CHUNKS = 2048;
+struct ColsumPlan {
+  int v, qw, gx;
+  int64_t chunks, cr;
+};
+ColsumPlan colsum_plan(int64_t rows, int64_t cols, int64_t ld, uintptr_t x) {
+  ColsumPlan p;
+  p.v = (cols % 4 == 0 && ld % 4 == 0 && x % 16 == 0) ? 4 : 1;
+  const int64_t nv = cols / p.v;
+  int qw = 1;
+  while (qw < nv && qw < 64) qw <<= 1;
+  p.qw = qw;
+  p.gx = (int)((nv + qw - 1) / qw);
+  int64_t ch = (rows + 63) / 64;
+  const int64_t cap = (COLSUM_MAX_CHUNKS + p.gx - 1) / p.gx;
+  if (ch > cap) ch = cap;
+  if (ch < 1) ch = 1;
+  p.cr = (rows + ch - 1) / ch;
+  p.chunks = (rows + p.cr - 1) / p.cr;
+  return p;
 }
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int64_t cols,
+
+template <int V>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t ld, int64_t rows,
+                                                             int64_t cols, int qw, int64_t cr, float* __restrict__ part) {
+  __shared__ float red[V][256];
+  const int qi = threadIdx.x & (qw - 1), rl = threadIdx.x / qw, nrl = 256 / qw;
+  const int64_t vec = (int64_t)blockIdx.x * qw + qi;
+  const int64_t r0 = (int64_t)blockIdx.y * cr;
+  const int64_t r1 = r0 + cr < rows ? r0 + cr : rows;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  if (vec * V < cols) {
+    if constexpr (V == 4) {
+      const float4* xv = reinterpret_cast<const float4*>(x) + vec;
+      const int64_t ldv = ld / 4;
+#pragma unroll 4
+      for (int64_t r = r0 + rl; r < r1; r += nrl) {
+        const float4 t = xv[r * ldv];
+        acc[0] += t.x; acc[1] += t.y; acc[2] += t.z; acc[3] += t.w;
+      }
+    } else {
+#pragma unroll 4
+      for (int64_t r = r0 + rl; r < r1; r += nrl) acc[0] += x[r * ld + vec];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[j][threadIdx.x] = acc[j];
+  __syncthreads();
+  for (int off = 128; off >= qw; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < qw && vec * V < cols) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) part[(int64_t)blockIdx.y * cols + vec * V + j] = red[j][threadIdx.x];
+  }
+}
+
+// out[c] = alpha * sum_z part[z][c] (+ beta * out[c]); 16 columns x 16 chunk lanes per workgroup
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int64_t chunks, int64_t cols,
                                                            float* __restrict__ out, float alpha, int beta) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[256];
+  const int ci = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int64_t c = (int64_t)blockIdx.x * 16 + ci;
   float s = 0.f;
-  for (int z = 0; z < chunks; ++z) s += part[(int64_t)z * cols + c];
-  out[c] = alpha * s + (beta ? out[c] : 0.f);
+  if (c < cols)
+    for (int64_t z = zl; z < chunks; z += 16) s += part[z * cols + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off >= 16; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 16 && c < cols) out[c] = alpha * red[threadIdx.x] + (beta ? out[c] : 0.f);
 }
 
 }  // namespace
@@ -255,19 +316,23 @@ extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
 
 extern "C" int64_t catseg_colsum_workspace(int64_t rows, int64_t cols) {
   if (rows <= 0 || cols <= 0) return 0;
-  return ((rows + CR - 1) / CR) * cols * (int64_t)sizeof(float);
+  // the larger of the 16-byte-load plan and the scalar plan (the launch picks one by ld / alignment)
+  const int64_t a = colsum_plan(rows, cols, cols, 0).chunks, b = colsum_plan(rows, cols, cols, 1).chunks;
+  return (a > b ? a : b) * cols * (int64_t)sizeof(float);
 }
 
 extern "C" int catseg_colsum(const float* x, int64_t ld, int64_t rows, int64_t cols, float* out, float alpha, int beta,
                              void* workspace, int64_t workspace_bytes, void* stream) {
   CATSEG_CHECK(x && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
-  const int64_t chunks = (rows + CR - 1) / CR;
-  CATSEG_CHECK(workspace && workspace_bytes >= chunks * cols * (int64_t)sizeof(float), "colsum: workspace too small");
-  CATSEG_CHECK(chunks < 65536, "colsum: too many rows");
+  const ColsumPlan p = colsum_plan(rows, cols, ld, (uintptr_t)x);
+  CATSEG_CHECK(workspace && workspace_bytes >= p.chunks * cols * (int64_t)sizeof(float), "colsum: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)chunks), dim3(256), 0, st, x, ld,
-                     rows, cols, (float*)workspace);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st,
-                     (const float*)workspace, (int)chunks, cols, out, alpha, beta);
+  const dim3 grid((unsigned)p.gx, (unsigned)p.chunks);
+  if (p.v == 4)
+    hipLaunchKernelGGL(colsum_partial_kernel<4>, grid, dim3(256), 0, st, x, ld, rows, cols, p.qw, p.cr, (float*)workspace);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, st, x, ld, rows, cols, p.qw, p.cr, (float*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 15) / 16)), dim3(256), 0, st, (const float*)workspace,
+                     p.chunks, cols, out, alpha, beta);
   return catseg_launch_status("colsum");
 }

@@ -139,104 +139,235 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------- GroupNorm
-// block sum over 256 threads (fixed order: DPP rows, then the 4 waves in order)
-DEV float block_sum(float v, float* sh) {
-  v = wave_sum(v);
-  const int wave = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[wave] = v;
-  __syncthreads();
-  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+// NHWC slices x[s][p][c] (S slices of HW pixels x C channels), groups of cpg consecutive channels.
+// The slice is cut into chunks of GN_PPC(C) pixels; one 256-thread workgroup per (chunk, slice),
+// thread t owns channel quad t % (C/4) (a float4) and pixels t / (C/4) + k * (1024 / C), k < 16,
+// so every load is a coalesced float4 and a chunk is 16 float4 per thread, held in registers.
+// Partials reduce across the threads of one quad by a fixed binary tree (strides 128 .. C/4),
+// chunks combine in chunk order: deterministic, grid a function of the shape only.
+// Requires C/4 a power of two <= 256 and cpg % 4 == 0 (the decoder: C 32 / 64 / 128, cpg 16).
+constexpr int GN_K = 16;                       // float4 per thread per chunk
+DEV int gn_ppc(int C) { return GN_K * 1024 / C; }
+int gn_chunks(int64_t HW, int C) { return (int)((HW + GN_K * 1024 / C - 1) / (GN_K * 1024 / C)); }
+bool gn_shape_ok(int C, int cpg) {
+  const int nq = C / 4;
+  return C % 4 == 0 && nq > 0 && nq <= 256 && (nq & (nq - 1)) == 0 && cpg % 4 == 0 && C % cpg == 0;
 }
 
-// one workgroup per (slice, group): mean and rstd over HW x cpg values (biased variance, two passes)
-__global__ __launch_bounds__(256) void gn_stats_kernel(const float* __restrict__ x, int64_t HW, int C, int cpg, int G,
-                                                       float eps, float* __restrict__ mean, float* __restrict__ rstd) {
-  __shared__ float sh[4];
-  const int64_t s = blockIdx.x / G;
-  const int g = blockIdx.x % G;
-  const float* base = x + s * HW * C + (int64_t)g * cpg;
-  const int64_t n = HW * cpg;
+// in-place tree over red[NV][256]: afterwards red[v][q], q < nq, holds quad q's sum (fixed order)
+template <int NV>
+DEV void quad_tree(float (*red)[256], int nq) {
+  for (int off = 128; off >= nq; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) red[v][threadIdx.x] += red[v][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+}
+
+// statistics, pass 1: per (slice, chunk, group) {sum, M2 about the chunk's own group mean}
+__global__ __launch_bounds__(256) void gn_stats_chunk_kernel(const float* __restrict__ x, int64_t HW, int C, int cpg,
+                                                             float* __restrict__ part) {
+  __shared__ float red[1][256];
+  __shared__ float gmean[256];
+  const int nq = C >> 2, G = C / cpg, qpg = cpg >> 2;
+  const int q = threadIdx.x & (nq - 1), pl = threadIdx.x / nq, ppi = 256 / nq;
+  const int64_t s = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * gn_ppc(C);
+  const int64_t pend = p0 + gn_ppc(C) < HW ? p0 + gn_ppc(C) : HW;
+  const float4* xs = reinterpret_cast<const float4*>(x + s * HW * C) + q;
+  float4 v[GN_K];
   float acc = 0.f;
-  for (int64_t e = threadIdx.x; e < n; e += 256) acc += base[(e / cpg) * C + e % cpg];
-  const float mu = block_sum(acc, sh) / (float)n;
-  acc = 0.f;
-  for (int64_t e = threadIdx.x; e < n; e += 256) {
-    const float d = base[(e / cpg) * C + e % cpg] - mu;
-    acc += d * d;
+#pragma unroll
+  for (int k = 0; k < GN_K; ++k) {
+    const int64_t p = p0 + pl + (int64_t)k * ppi;
+    v[k] = p < pend ? xs[p * nq] : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc += ((v[k].x + v[k].y) + v[k].z) + v[k].w;
   }
-  const float var = block_sum(acc, sh) / (float)n;
-  if (threadIdx.x == 0) {
-    mean[blockIdx.x] = mu;
-    rstd[blockIdx.x] = 1.f / sqrtf(var + eps);
-  }
-}
-
-// GroupNorm+ReLU backward, pass 1: per (slice, channel) sums of dyr and dyr * xhat, one workgroup per
-// (slice, group); thread t owns channel t % cpg of the group (cpg divides 256).
-__global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                            int64_t HW, int C, int cpg, int G,
-                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                            float* __restrict__ sums) {
-  __shared__ float r1[256], r2[256];
-  const int64_t s = blockIdx.x / G;
-  const int g = blockIdx.x % G;
-  const int c = threadIdx.x % cpg, pr = threadIdx.x / cpg, np = 256 / cpg;
-  const int ch = g * cpg + c;
-  const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x], ga = gamma[ch], be = beta[ch];
-  float s1 = 0.f, s2 = 0.f;
-  for (int64_t p = pr; p < HW; p += np) {
-    const int64_t off = (s * HW + p) * C + ch;
-    const float xh = (x[off] - mu) * rs;
-    const float d = (ga * xh + be) > 0.f ? dy[off] : 0.f;
-    s1 += d;
-    s2 += d * xh;
-  }
-  r1[threadIdx.x] = s1;
-  r2[threadIdx.x] = s2;
+  red[0][threadIdx.x] = acc;
   __syncthreads();
-  if (threadIdx.x < cpg) {
-    float a = 0.f, b = 0.f;
-    for (int q = 0; q < np; ++q) { a += r1[q * cpg + threadIdx.x]; b += r2[q * cpg + threadIdx.x]; }
-    sums[(s * C + ch) * 2 + 0] = a;
-    sums[(s * C + ch) * 2 + 1] = b;
+  quad_tree<1>(red, nq);
+  const float cnt = (float)((pend - p0) * cpg);
+  if ((int)threadIdx.x < G) {
+    float t = 0.f;
+    for (int j = 0; j < qpg; ++j) t += red[0][threadIdx.x * qpg + j];
+    gmean[threadIdx.x] = t / cnt;
+    part[((s * gridDim.x + blockIdx.x) * G + threadIdx.x) * 2 + 0] = t;
+  }
+  __syncthreads();
+  const float mu = gmean[(q * 4) / cpg];
+  acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < GN_K; ++k) {
+    const int64_t p = p0 + pl + (int64_t)k * ppi;
+    if (p < pend) {
+      const float a = v[k].x - mu, b = v[k].y - mu, c = v[k].z - mu, d = v[k].w - mu;
+      acc += ((a * a + b * b) + c * c) + d * d;
+    }
+  }
+  red[0][threadIdx.x] = acc;
+  __syncthreads();
+  quad_tree<1>(red, nq);
+  if ((int)threadIdx.x < G) {
+    float t = 0.f;
+    for (int j = 0; j < qpg; ++j) t += red[0][threadIdx.x * qpg + j];
+    part[((s * gridDim.x + blockIdx.x) * G + threadIdx.x) * 2 + 1] = t;
   }
 }
 
-// pass 2: dx = rstd * (dyr * gamma - (A_g + xhat * B_g) / n), A_g = sum_c gamma_c S1_c, B_g = sum_c gamma_c S2_c
-__global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                           float* __restrict__ dx, int64_t S, int64_t HW, int C, int cpg,
-                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                           const float* __restrict__ sums) {
+// statistics, pass 2: one thread per (slice, group) combines its chunks in order (Chan et al.'s
+// pairwise mean / M2 update) -> mean, rstd (biased variance, as nn.GroupNorm)
+__global__ __launch_bounds__(256) void gn_stats_final_kernel(const float* __restrict__ part, int64_t S, int64_t HW,
+                                                             int C, int cpg, int nch, float eps, float* __restrict__ mean,
+                                                             float* __restrict__ rstd) {
+  const int G = C / cpg;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= S * HW * C) return;
-  const int ch = (int)(i % C);
-  const int64_t s = i / (HW * C);
-  const int g = ch / cpg;
-  const int64_t sg = s * (C / cpg) + g;
+  if (i >= S * G) return;
+  const int64_t s = i / G;
+  const int g = (int)(i % G);
+  const int ppc = gn_ppc(C);
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int k = 0; k < nch; ++k) {
+    const int64_t px = (k + 1) * (int64_t)ppc < HW ? ppc : HW - (int64_t)k * ppc;
+    const float nb = (float)(px * cpg);
+    const float* pp = part + ((s * nch + k) * G + g) * 2;
+    const float mb = pp[0] / nb;
+    const float nn = n + nb;
+    const float dl = mb - mu;
+    mu += dl * (nb / nn);
+    m2 += pp[1] + dl * dl * (n * nb / nn);
+    n = nn;
+  }
+  mean[i] = mu;
+  rstd[i] = 1.f / sqrtf(m2 / n + eps);
+}
+
+// GroupNorm+ReLU backward, pass 1: per (slice, chunk, channel) S1 = sum dyr, S2 = sum dyr * xhat,
+// dyr = dy where the ReLU passed (gamma * xhat + beta > 0)
+__global__ __launch_bounds__(256) void gn_bwd_chunk_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                                  int64_t HW, int C, int cpg,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ beta, float* __restrict__ part) {
+  __shared__ float red[8][256];
+  const int nq = C >> 2, G = C / cpg;
+  const int q = threadIdx.x & (nq - 1), pl = threadIdx.x / nq, ppi = 256 / nq;
+  const int64_t s = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * gn_ppc(C);
+  const int64_t pend = p0 + gn_ppc(C) < HW ? p0 + gn_ppc(C) : HW;
+  const int64_t sg = s * G + (q * 4) / cpg;
+  const float mu = mean[sg], rs = rstd[sg];
+  const float4 ga = reinterpret_cast<const float4*>(gamma)[q], be = reinterpret_cast<const float4*>(beta)[q];
+  const float4* xs = reinterpret_cast<const float4*>(x + s * HW * C) + q;
+  const float4* ds = reinterpret_cast<const float4*>(dy + s * HW * C) + q;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = 0; k < GN_K; ++k) {
+    const int64_t p = p0 + pl + (int64_t)k * ppi;
+    if (p < pend) {
+      const float4 xv = xs[p * nq], dv = ds[p * nq];
+      const float xh[4] = {(xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs};
+      const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (gg[j] * xh[j] + bb[j]) > 0.f ? dd[j] : 0.f;
+        a[j] += d;
+        b[j] += d * xh[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { red[j][threadIdx.x] = a[j]; red[4 + j][threadIdx.x] = b[j]; }
+  __syncthreads();
+  quad_tree<8>(red, nq);
+  if ((int)threadIdx.x < nq) {
+    float* out = part + ((s * gridDim.x + blockIdx.x) * C + threadIdx.x * 4) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { out[2 * j] = red[j][threadIdx.x]; out[2 * j + 1] = red[4 + j][threadIdx.x]; }
+  }
+}
+
+// pass 2: per (slice, channel) totals over the chunks, in chunk order -> sums[s][c][2]
+__global__ __launch_bounds__(256) void gn_bwd_chan_kernel(const float* __restrict__ part, int64_t S, int C, int nch,
+                                                          float* __restrict__ sums) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= S * C) return;
+  const int64_t s = i / C;
+  const int c = (int)(i % C);
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nch; ++k) {
+    const float* pp = part + ((s * nch + k) * C + c) * 2;
+    a += pp[0];
+    b += pp[1];
+  }
+  sums[i * 2 + 0] = a;
+  sums[i * 2 + 1] = b;
+}
+
+// pass 3: dx = rstd * (dyr * gamma - (A_g + xhat * B_g) / n), A_g = sum_c gamma_c S1_c, B_g = sum_c gamma_c S2_c
+// (A_g, B_g formed once per thread, channels in ascending order)
+__global__ __launch_bounds__(256) void gn_bwd_chunk_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                                 float* __restrict__ dx, int64_t HW, int C, int cpg,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta,
+                                                                 const float* __restrict__ sums) {
+  const int nq = C >> 2, G = C / cpg;
+  const int q = threadIdx.x & (nq - 1), pl = threadIdx.x / nq, ppi = 256 / nq;
+  const int64_t s = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * gn_ppc(C);
+  const int64_t pend = p0 + gn_ppc(C) < HW ? p0 + gn_ppc(C) : HW;
+  const int g = (q * 4) / cpg;
+  const int64_t sg = s * G + g;
   float A = 0.f, Bv = 0.f;
   for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
     A += gamma[c] * sums[(s * C + c) * 2 + 0];
     Bv += gamma[c] * sums[(s * C + c) * 2 + 1];
   }
-  const float n = (float)(HW * cpg);
-  const float mu = mean[sg], rs = rstd[sg], ga = gamma[ch];
-  const float xh = (x[i] - mu) * rs;
-  const float d = (ga * xh + beta[ch]) > 0.f ? dy[i] : 0.f;
-  dx[i] = rs * (d * ga - (A + xh * Bv) / n);
+  const float inv_n = 1.f / (float)(HW * cpg);
+  const float mu = mean[sg], rs = rstd[sg];
+  const float4 ga = reinterpret_cast<const float4*>(gamma)[q], be = reinterpret_cast<const float4*>(beta)[q];
+  const float gg[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {be.x, be.y, be.z, be.w};
+  const float4* xs = reinterpret_cast<const float4*>(x + s * HW * C) + q;
+  const float4* ds = reinterpret_cast<const float4*>(dy + s * HW * C) + q;
+  float4* os = reinterpret_cast<float4*>(dx + s * HW * C) + q;
+#pragma unroll 4
+  for (int k = 0; k < GN_K; ++k) {
+    const int64_t p = p0 + pl + (int64_t)k * ppi;
+    if (p < pend) {
+      const float4 xv = xs[p * nq], dv = ds[p * nq];
+      const float xx[4] = {xv.x, xv.y, xv.z, xv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (xx[j] - mu) * rs;
+        const float d = (gg[j] * xh + bb[j]) > 0.f ? dd[j] : 0.f;
+        o[j] = rs * (d * gg[j] - (A + xh * Bv) * inv_n);
+      }
+      os[p * nq] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
 }
 
-// pass 3: dgamma[c] = sum_s S2[s][c], dbeta[c] = sum_s S1[s][c]
+// pass 4: dgamma[c] = sum_s S2[s][c], dbeta[c] = sum_s S1[s][c]; one workgroup per channel,
+// thread t takes slices t, t + 256, ..., then a fixed tree over the 256 threads
 __global__ __launch_bounds__(256) void gn_param_kernel(const float* __restrict__ sums, int64_t S, int C,
                                                        float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[2][256];
+  const int c = blockIdx.x;
   float a = 0.f, b = 0.f;
-  for (int64_t s = 0; s < S; ++s) { a += sums[(s * C + c) * 2 + 0]; b += sums[(s * C + c) * 2 + 1]; }
-  dgamma[c] = acc ? dgamma[c] + b : b;
-  dbeta[c] = acc ? dbeta[c] + a : a;
+  for (int64_t s = threadIdx.x; s < S; s += 256) { a += sums[(s * C + c) * 2 + 0]; b += sums[(s * C + c) * 2 + 1]; }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  quad_tree<2>(red, 1);
+  if (threadIdx.x == 0) {
+    dgamma[c] = acc ? dgamma[c] + red[1][0] : red[1][0];
+    dbeta[c] = acc ? dbeta[c] + red[0][0] : red[0][0];
+  }
 }
 
 // ---------------------------------------------------------------------------------- reductions
@@ -489,17 +620,31 @@ extern "C" int catseg_act_backward(const float* u, const float* dy, float* du, i
   return catseg_launch_status("act_backward");
 }
 
+extern "C" int64_t catseg_groupnorm_stats_rows_workspace(int64_t S, int64_t HW, int C, int cpg) {
+  if (S <= 0 || HW <= 0 || C <= 0 || cpg <= 0 || !gn_shape_ok(C, cpg)) return 0;
+  return S * gn_chunks(HW, C) * (C / cpg) * 2 * (int64_t)sizeof(float);
+}
+
 extern "C" int catseg_groupnorm_stats_rows(const float* x, int64_t S, int64_t HW, int C, int cpg, float eps, float* mean,
-                                           float* rstd, void* stream) {
-  CATSEG_CHECK(x && mean && rstd && S > 0 && HW > 0 && cpg > 0 && C % cpg == 0, "groupnorm_stats_rows: bad args");
-  CATSEG_CHECK(S * (C / cpg) < (1LL << 31), "groupnorm_stats_rows: too many groups");
-  hipLaunchKernelGGL(gn_stats_kernel, dim3((unsigned)(S * (C / cpg))), dim3(256), 0, (hipStream_t)stream, x, HW, C, cpg,
-                     C / cpg, eps, mean, rstd);
+                                           float* rstd, void* workspace, int64_t workspace_bytes, void* stream) {
+  CATSEG_CHECK(x && mean && rstd && S > 0 && HW > 0 && cpg > 0, "groupnorm_stats_rows: bad args");
+  CATSEG_CHECK(gn_shape_ok(C, cpg), "groupnorm_stats_rows: needs C/4 a power of two <= 256 and cpg % 4 == 0");
+  CATSEG_CHECK(((uintptr_t)x % 16) == 0, "groupnorm_stats_rows: x must be 16-byte aligned");
+  const int nch = gn_chunks(HW, C);
+  CATSEG_CHECK(S < 65536 && nch < (1 << 30), "groupnorm_stats_rows: too many slices");
+  CATSEG_CHECK(workspace && workspace_bytes >= S * nch * (C / cpg) * 2 * (int64_t)sizeof(float),
+               "groupnorm_stats_rows: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(gn_stats_chunk_kernel, dim3((unsigned)nch, (unsigned)S), dim3(256), 0, st, x, HW, C, cpg, part);
+  hipLaunchKernelGGL(gn_stats_final_kernel, dim3(blocks(S * (C / cpg))), dim3(256), 0, st, (const float*)part, S, HW, C,
+                     cpg, nch, eps, mean, rstd);
   return catseg_launch_status("groupnorm_stats_rows");
 }
 
-extern "C" int64_t catseg_groupnorm_relu_backward_workspace(int64_t S, int C) {
-  return S > 0 && C > 0 ? S * C * 2 * (int64_t)sizeof(float) : 0;
+extern "C" int64_t catseg_groupnorm_relu_backward_workspace(int64_t S, int64_t HW, int C) {
+  if (S <= 0 || HW <= 0 || C <= 0 || C % 4 != 0) return 0;
+  return (S * gn_chunks(HW, C) * C * 2 + S * C * 2) * (int64_t)sizeof(float);
 }
 
 extern "C" int catseg_groupnorm_relu_backward(const float* x, const float* dy, float* dx, int64_t S, int64_t HW, int C,
@@ -507,17 +652,25 @@ extern "C" int catseg_groupnorm_relu_backward(const float* x, const float* dy, f
                                               const float* beta, float* dgamma, float* dbeta, int acc_param,
                                               void* workspace, int64_t workspace_bytes, void* stream) {
   CATSEG_CHECK(x && dy && dx && mean && rstd && gamma && beta && dgamma && dbeta, "groupnorm_relu_backward: null pointer");
-  CATSEG_CHECK(S > 0 && HW > 0 && cpg > 0 && C % cpg == 0 && 256 % cpg == 0, "groupnorm_relu_backward: bad shape");
-  CATSEG_CHECK(workspace && workspace_bytes >= S * C * 2 * (int64_t)sizeof(float), "groupnorm_relu_backward: workspace");
+  CATSEG_CHECK(S > 0 && HW > 0 && cpg > 0, "groupnorm_relu_backward: bad shape");
+  CATSEG_CHECK(gn_shape_ok(C, cpg), "groupnorm_relu_backward: needs C/4 a power of two <= 256 and cpg % 4 == 0");
+  CATSEG_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
+                   ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0,
+               "groupnorm_relu_backward: x, dy, dx, gamma, beta must be 16-byte aligned");
+  const int nch = gn_chunks(HW, C);
+  CATSEG_CHECK(S < 65536, "groupnorm_relu_backward: too many slices");
+  CATSEG_CHECK(workspace && workspace_bytes >= (S * nch * C * 2 + S * C * 2) * (int64_t)sizeof(float),
+               "groupnorm_relu_backward: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  float* sums = (float*)workspace;
-  const int G = C / cpg;
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3((unsigned)(S * G)), dim3(256), 0, st, x, dy, HW, C, cpg, G, mean, rstd,
-                     gamma, beta, sums);
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(blocks(S * HW * C)), dim3(256), 0, st, x, dy, dx, S, HW, C, cpg, mean,
-                     rstd, gamma, beta, (const float*)sums);
-  hipLaunchKernelGGL(gn_param_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (const float*)sums, S, C,
-                     dgamma, dbeta, acc_param);
+  float* part = (float*)workspace;
+  float* sums = part + S * nch * C * 2;
+  const dim3 grid((unsigned)nch, (unsigned)S);
+  hipLaunchKernelGGL(gn_bwd_chunk_reduce_kernel, grid, dim3(256), 0, st, x, dy, HW, C, cpg, mean, rstd, gamma, beta, part);
+  hipLaunchKernelGGL(gn_bwd_chan_kernel, dim3(blocks(S * C)), dim3(256), 0, st, (const float*)part, S, C, nch, sums);
+  hipLaunchKernelGGL(gn_bwd_chunk_apply_kernel, grid, dim3(256), 0, st, x, dy, dx, HW, C, cpg, mean, rstd, gamma, beta,
+                     (const float*)sums);
+  hipLaunchKernelGGL(gn_param_kernel, dim3((unsigned)C), dim3(256), 0, st, (const float*)sums, S, C, dgamma, dbeta,
+                     acc_param);
   return catseg_launch_status("groupnorm_relu_backward");
 }
 

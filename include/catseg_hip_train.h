@@ -66,18 +66,23 @@ int catseg_act_forward(const float* u, float* a, int64_t n, int act, void* strea
 int catseg_act_backward(const float* u, const float* dy, float* du, int64_t n, int act, void* stream);
 
 /* catseg_groupnorm_stats_rows — nn.GroupNorm statistics (model.py:529,532) of an NHWC map
- * x[S][HW][C], groups of cpg channels: mean / rstd [S][C/cpg] (biased variance, eps). */
+ * x[S][HW][C], groups of cpg channels: mean / rstd [S][C/cpg] (biased variance, eps).  Pixel chunks
+ * of 16384/C pixels reduce {sum, M2} in registers, chunks combine in order (pairwise update).
+ * C/4 a power of two <= 256, cpg % 4 == 0, x 16-byte aligned.
+ * workspace >= catseg_groupnorm_stats_rows_workspace(S, HW, C, cpg) bytes. */
 int catseg_groupnorm_stats_rows(const float* x, int64_t S, int64_t HW, int C, int cpg, float eps, float* mean,
-                                float* rstd, void* stream);
+                                float* rstd, void* workspace, int64_t workspace_bytes, void* stream);
+int64_t catseg_groupnorm_stats_rows_workspace(int64_t S, int64_t HW, int C, int cpg);
 
 /* catseg_groupnorm_relu_backward — backward of y = relu(GroupNorm(x)) (model.py:529-533) given
- * dy = dL/dy: dx (overwritten), dgamma / dbeta (+= when acc_param).  256 % cpg == 0.
- * workspace >= catseg_groupnorm_relu_backward_workspace(S, C) bytes. */
+ * dy = dL/dy: dx (overwritten), dgamma / dbeta (+= when acc_param).  C/4 a power of two <= 256,
+ * cpg % 4 == 0, x / dy / dx / gamma / beta 16-byte aligned.
+ * workspace >= catseg_groupnorm_relu_backward_workspace(S, HW, C) bytes. */
 int catseg_groupnorm_relu_backward(const float* x, const float* dy, float* dx, int64_t S, int64_t HW, int C, int cpg,
                                    const float* mean, const float* rstd, const float* gamma, const float* beta,
                                    float* dgamma, float* dbeta, int acc_param, void* workspace,
                                    int64_t workspace_bytes, void* stream);
-int64_t catseg_groupnorm_relu_backward_workspace(int64_t S, int C);
+int64_t catseg_groupnorm_relu_backward_workspace(int64_t S, int64_t HW, int C);
 
 /* catseg_l2normalize_backward — F.normalize backward (model.py:649-650, cat_seg_predictor.py:216):
  * dx[outmap(r)] (+)= (dy[r] - y (y . dy[r])) / max(|x|, eps), x = x[inmap(r)], y = x / max(|x|, eps). */

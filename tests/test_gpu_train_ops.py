@@ -56,11 +56,18 @@ def test_gemm_ex_layouts(M, N, K):
             close(out, 0.5 * ref + 3.0)
 
 
-def test_colsum():
-    x = g(5000, 132, seed=3)
-    out = torch.ones(132, device=DEV)
-    TO.colsum(dev(x), out, beta=1, alpha=2.0)
-    close(out, 2 * x.sum(0) + 1)
+@pytest.mark.parametrize("rows,cols,ld", [(5000, 132, 132),      # 16-byte loads, 33 vectors in a 64-wide block
+                                          (5000, 130, 130),      # scalar path (cols % 4 != 0)
+                                          (3001, 96, 100),       # strided rows, vectors
+                                          (300000, 32, 32),      # 2048 chunks, 8 vectors x 32 row lanes
+                                          (77, 3072, 3072),      # 12 column blocks, one chunk per 64 rows
+                                          (9, 1, 1)])
+def test_colsum(rows, cols, ld):
+    x = g(rows, ld, seed=3)
+    out = torch.ones(cols, device=DEV)
+    TO.colsum(dev(x), out, rows=rows, cols=cols, ld=ld, beta=1, alpha=2.0)
+    ref = x[:, :cols].double().sum(0)
+    close(out, 2 * ref.float() + 1)
 
 
 @pytest.mark.parametrize("cols", [128, 768])
@@ -92,8 +99,11 @@ def test_act_forward_backward(act, fn):
     close(TO.act_backward(dev(u), dev(dy), act), ur.grad, 1e-6)
 
 
-def test_groupnorm_relu_stats_and_backward():
-    S, H, W, C, cpg = 6, 12, 10, 64, 16
+@pytest.mark.parametrize("S,H,W,C,cpg", [(6, 12, 10, 64, 16),    # one pixel chunk
+                                         (3, 40, 37, 32, 16),    # 3 chunks of 512 pixels, the last ragged
+                                         (2, 24, 24, 128, 16),   # 4.5 chunks of 128 pixels
+                                         (4, 9, 7, 16, 4)])      # one group of 4 channels per quad
+def test_groupnorm_relu_stats_and_backward(S, H, W, C, cpg):
     x = g(S, C, H, W, seed=10) * 2 + 0.5
     gm = 1 + 0.2 * g(C, seed=11)
     bt = 0.3 * g(C, seed=12)

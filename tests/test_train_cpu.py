@@ -46,7 +46,7 @@ def test_train_entry_points_validate_on_the_host():
     # workspace queries are pure host arithmetic
     assert lib.catseg_gemm_ex_workspace(384, 128, 400000) > 0
     assert lib.catseg_gemm_ex_workspace(400000, 128, 384) == 0
-    assert lib.catseg_colsum_workspace(5000, 128) == 5 * 128 * 4
+    assert lib.catseg_colsum_workspace(5000, 128) == 79 * 128 * 4            # 79 chunks of 64 rows
 
 
 REF_NORM_TYPES = (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d, torch.nn.BatchNorm3d, torch.nn.SyncBatchNorm,
