@@ -24,7 +24,7 @@ import torch
 from torch import nn
 from torch.nn.modules.module import _IncompatibleKeys
 
-from . import ops
+from . import custom_ops, ops
 from .arch import CatSegArch, arch_from_cfg
 from .engine import CatSegEngine
 from .modeling.heads.cat_seg_head import CATSegHead  # noqa: F401  (registers the head)
@@ -98,6 +98,7 @@ class CATSeg(nn.Module):
         self._train_engine: Optional[CatSegEngine] = None
         self._engine_key = self._train_engine_key = None
         self.input_format = "RGB"          # read by SemanticSegmentorWithTTA / DefaultPredictor
+        self._op_handle = custom_ops.register_model(self)   # catseg::head_logits (torch.compile path)
 
     @classmethod
     def from_config(cls, cfg):
@@ -217,11 +218,41 @@ class CATSeg(nn.Module):
         sizes_dev = torch.tensor(sizes, dtype=torch.int32).to(dev, non_blocking=True)
         return (raw if on_dev else raw.to(dev, non_blocking=True)), sizes_dev, sizes
 
+    def _forward_traced(self, batched_inputs: List[dict]):
+        """The eval forward as dynamo traces it (torch.compile): the canvas staging in torch ops, the
+        network as the one registered operator catseg::head_logits (custom_ops), the resize through
+        catseg::postprocess; same kernels and results as the eager branch below."""
+        handle = self._op_handle
+        n_classes, res = custom_ops.head_meta(handle)
+        images = [x["image"] for x in batched_inputs]
+        d = max(self.size_divisibility, 1)
+        H = max(int(i.shape[-2]) for i in images)
+        W = max(int(i.shape[-1]) for i in images)
+        H, W = -(-H // d) * d, -(-W // d) * d
+        dev = self._engine_device()
+        raw = torch.zeros(len(images), 3, H, W, dtype=torch.float32, device=dev)
+        for k, im in enumerate(images):
+            raw[k, :, : im.shape[-2], : im.shape[-1]] = im.to(dev, torch.float32)
+        sizes = [(int(i.shape[-2]), int(i.shape[-1])) for i in images]
+        sizes_dev = torch.tensor(sizes, dtype=torch.int32, device=dev)
+        logits = torch.ops.catseg.head_logits(raw, sizes_dev, handle, n_classes, res)
+        n = len(batched_inputs) if self.return_all_images else 1
+        results = []
+        for i in range(n):
+            ih, iw = sizes[i]
+            h = int(batched_inputs[i].get("height", ih))
+            w = int(batched_inputs[i].get("width", iw))
+            out = torch.ops.catseg.postprocess(logits[i:i + 1], h, w, min(res, ih), min(res, iw))
+            results.append({"sem_seg": out[0]})
+        return results
+
     def forward(self, batched_inputs: List[dict]):
         if self.training:
             return self._training_loss(batched_inputs)
         if self.sliding_window:
             return self._forward_sliding(batched_inputs)
+        if torch.compiler.is_compiling():
+            return self._forward_traced(batched_inputs)
         with torch.no_grad():
             eng = self.engine
             self.sem_seg_head.predictor.get_text_embeds()

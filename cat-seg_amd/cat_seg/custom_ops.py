@@ -14,10 +14,15 @@ need the dispatcher); these are the registered surface for code that composes th
   catseg::postprocess      sigmoid + bilinear resize (catseg_postprocess; cat_seg_model.py:222-228)
   catseg::linear           y = act(x W^T + b) with a registered backward (catseg_gemm forward,
                            catseg_gemm_ex / catseg_colsum backward): the training kernels through autograd
+  catseg::head_logits      the whole eval forward of a registered CATSeg model up to the logits
+                           (CLIP dense encode + Aggregator, cat_seg_model.py:155-188): one opaque operator,
+                           so `torch.compile(model, fullgraph=True)` traces CATSeg.forward with no break
 """
 from __future__ import annotations
 
-from typing import Optional
+import itertools
+import weakref
+from typing import Optional, Tuple
 
 import torch
 
@@ -184,3 +189,53 @@ def _(u, dy, act):
 
 
 linear.register_autograd(_linear_backward, setup_context=_linear_setup)
+
+
+# ------------------------------------------------------------------------------------- whole-model forward
+# CATSeg models register themselves here (an int handle, so the operator's schema stays plain); the op
+# runs the model's engine eagerly, the fake kernel only needs the output geometry.
+_MODELS: "dict[int, weakref.ref]" = {}
+_next_handle = itertools.count(1)
+
+
+def register_model(model) -> int:
+    h = next(_next_handle)
+    _MODELS[h] = weakref.ref(model)
+    return h
+
+
+def _model(handle: int):
+    m = _MODELS.get(handle)
+    m = m() if m is not None else None
+    if m is None:
+        raise RuntimeError(f"catseg: no live CATSeg model with handle {handle}")
+    return m
+
+
+@torch._dynamo.assume_constant_result
+def head_meta(handle: int) -> Tuple[int, int]:
+    """(T0, logit resolution) of a registered model, with its engine built and its test-class text
+    embeddings cached: run eagerly when dynamo traces CATSeg.forward (a constant of the graph)."""
+    m = _model(handle)
+    eng = m.engine
+    m.sem_seg_head.predictor.get_text_embeds()
+    return int(eng.n_classes), int(4 * m.arch.grid)
+
+
+@torch.library.custom_op("catseg::head_logits", mutates_args=())
+def head_logits(raw: torch.Tensor, sizes: torch.Tensor, handle: int, n_classes: int, res: int) -> torch.Tensor:
+    """fp32 logits (B, T0, res, res) of the registered model's eval forward (CatSegEngine.head_logits)
+    for the zero-padded image canvas raw (B, 3, H, W) fp32 and the per-image sizes (B, 2) int32."""
+    m = _model(handle)
+    eng = m.engine
+    m.sem_seg_head.predictor.get_text_embeds()
+    out = eng.head_logits(raw.contiguous(), sizes.contiguous())
+    if tuple(out.shape) != (raw.shape[0], n_classes, res, res):
+        raise RuntimeError(f"catseg::head_logits: logits {tuple(out.shape)} != the traced geometry "
+                           f"{(raw.shape[0], n_classes, res, res)} (class set changed after tracing?)")
+    return out.clone()
+
+
+@head_logits.register_fake
+def _(raw, sizes, handle, n_classes, res):
+    return raw.new_empty((raw.shape[0], n_classes, res, res))

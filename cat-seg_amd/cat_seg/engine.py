@@ -373,6 +373,13 @@ class CatSegEngine:
         """The class-embedding tensor the current set_text() call was given (None before any)."""
         return None if self._text is None else self._text.src
 
+    @property
+    def n_classes(self) -> int:
+        """T0, the class count of the current set_text() (the logits' channel count)."""
+        if self._text is None:
+            raise RuntimeError("set_text() / encode_text() must run first")
+        return int(self._text.T)
+
     def set_text(self, text: torch.Tensor):
         """Cache the per-class-set terms (the predictor's eval cache, cat_seg_predictor.py:191-192,221-222).
         text: (T, C_o) or (T, 1, C_o) L2-normalized class embeddings."""

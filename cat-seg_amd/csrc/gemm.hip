@@ -785,6 +785,10 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 1 && v == 19) return launch3<TO, 128, 128, 2, 4, 2, 64, false, 1>(g, st);
   if (epi == 2 && v == 19) return launch3<TO, 128, 128, 2, 4, 2, 64, false, 2>(g, st);
   if (epi == 1 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 1>(g, st);
+  if (epi == 1 && v == 21) return launch3<TO, 160, 128, 2, 4, 3, 64, false, 1>(g, st);
+  if (epi == 2 && v == 21) return launch3<TO, 160, 128, 2, 4, 3, 64, false, 2>(g, st);
+  if (epi == 1 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 1>(g, st);
+  if (epi == 2 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 2>(g, st);
   if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
   // forced tiles (gemm_variant, tests / tools/micro_gemm.py): the automatic candidates only
   switch (v) {

@@ -66,3 +66,33 @@ def test_compile_fullgraph_through_custom_ops():
     eager = block(x)
     compiled = torch.compile(block, fullgraph=True, backend="aot_eager")(x)
     assert torch.equal(compiled, eager)
+
+
+def test_compile_catseg_forward_fullgraph():
+    """torch.compile(CATSeg, fullgraph=True) traces the eval forward with no graph break: the canvas
+    staging as torch ops, the network as catseg::head_logits, the resize as catseg::postprocess; the
+    compiled forward returns the eager forward's probabilities bit for bit (same kernels)."""
+    import os
+    import numpy as np
+    from cat_seg import build_model
+    from conftest import ROOT
+    from test_boundary_cpu import tiny_cfg
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "e2e_tiny_eval.npz")))
+    model = build_model(tiny_cfg()).cuda().eval()
+    model.sem_seg_head.predictor.set_class_tokens(g["tokens"])
+    im = torch.from_numpy(g["image0"])
+    inputs = [{"image": im, "height": 200, "width": 300}, {"image": im[:, :40, :48]}]
+    eager = model(inputs)
+    torch._dynamo.reset()
+    compiled = torch.compile(model, fullgraph=True, backend="aot_eager")
+    got = compiled(inputs)
+    assert len(got) == len(eager) == 2
+    for a, b in zip(eager, got):
+        assert a["sem_seg"].shape == b["sem_seg"].shape
+        assert torch.equal(a["sem_seg"], b["sem_seg"])
+    # the traced graph holds the two registered operators, not the engine's ctypes calls
+    from torch._dynamo.testing import CompileCounterWithBackend
+    cnt = CompileCounterWithBackend("aot_eager")
+    torch._dynamo.reset()
+    torch.compile(model, fullgraph=True, backend=cnt)(inputs)
+    assert cnt.frame_count == 1
