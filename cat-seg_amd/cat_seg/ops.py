@@ -31,8 +31,8 @@ class _rec:
     (class padding rows, guidance halves recomputed per class and the
     ConvTranspose maps are algorithmic work the build skips); defaults to flops."""
 
-    def __init__(self, kernel, flops=0, nbytes=0, ref_flops=None):
-        self.kernel, self.flops, self.nbytes = kernel, flops, nbytes
+    def __init__(self, kernel, flops=0, nbytes=0, ref_flops=None, shape=None):
+        self.kernel, self.flops, self.nbytes, self.shape = kernel, flops, nbytes, shape
         self.ref_flops = flops if ref_flops is None else ref_flops
 
     def __enter__(self):
@@ -49,7 +49,7 @@ class _rec:
             if exc[0] is None:
                 self.e1.record(torch.cuda.current_stream())
                 PROFILE.append({"kernel": self.kernel, "flops": self.flops, "ref_flops": self.ref_flops,
-                                "bytes": self.nbytes, "start": self.e0, "end": self.e1})
+                                "bytes": self.nbytes, "start": self.e0, "end": self.e1, "shape": self.shape})
         return False
 
 
@@ -113,7 +113,8 @@ def gemm(A, W, out, *, M=None, K=None, bias=None, act=L.ACT_NONE, alpha=1.0,
         a.cvt_k, a.cvt_hin, a.cvt_win, a.cvt_cout = store
     a.dtype_a, a.dtype_out = _dt(A), _dt(out)
     kname = "gemm_bf16" if a.dtype_a == L.BF16 else "gemm_f32"
-    with _rec(kname, 2 * M * N * K, A.element_size() * (M * K + N * K) + out.element_size() * M * N):
+    with _rec(kname, 2 * M * N * K, A.element_size() * (M * K + N * K) + out.element_size() * M * N,
+              shape=(M, N, K)):
         call("catseg_gemm", a, _stream())
     return out
 

@@ -44,7 +44,8 @@ def gemm_ex(A, a_sm, a_sk, B, b_sk, b_sn, out, *, M, N, K, ldc=None, alpha=1.0, 
     ws = _ws(L.load().catseg_gemm_ex_workspace(M, N, K), out.device)
     if ws is not None:
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
-    with _rec(flops_name, 2 * M * N * K, 4 * (M * K + K * N + M * N)):
+    with _rec(flops_name, 2 * M * N * K, 4 * (M * K + K * N + M * N),
+              shape=(M, N, K, "m" if a_sm == 1 else "k", "n" if b_sn == 1 else "k")):
         call("catseg_gemm_ex", a, _stream())
     return out
 

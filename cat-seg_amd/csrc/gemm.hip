@@ -210,11 +210,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
       rw[i] = (w_ok[i] && k < K) ? ld16(w_ptr[i] + k) : make_uint4(0, 0, 0, 0);
     }
   };
+  // fp32: rows 8..15 of every 16-row group hold each 4-float chunk rotated by two (halves swapped),
+  // so the 16 rows x 2 k of a ds_read_b32 lane group (bank = (36 row + k) mod 32) fall on 32
+  // distinct banks instead of two rows per bank; the read index is k ^ 2 on those rows
+  auto rot = [](uint4 u, int row) {
+    if constexpr (sizeof(TA) == 4) return ((row >> 3) & 1) ? make_uint4(u.z, u.w, u.x, u.y) : u;
+    else return u;
+  };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], ra[i]);
+    for (int i = 0; i < A_CH; ++i) st16(&sA[buf][a_lrow[i] * LDR + a_col[i]], rot(ra[i], a_lrow[i]));
 #pragma unroll
-    for (int i = 0; i < W_CH; ++i) st16(&sW[buf][w_lrow[i] * LDR + w_col[i]], rw[i]);
+    for (int i = 0; i < W_CH; ++i) st16(&sW[buf][w_lrow[i] * LDR + w_col[i]], rot(rw[i], w_lrow[i]));
   };
 
   f32x4 acc[FN][FM];
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
         for (int j = 0; j < FM; ++j) acc[i][j] = mfma_bf16(afrag, bfrag[j], acc[i][j]);
       }
     } else {
-      const int r = lane & 15, kq = lane >> 4;
+      const int r = lane & 15, kq = (lane >> 4) ^ (((lane >> 3) & 1) << 1);   // rot() above
 #pragma unroll
       for (int s = 0; s < BK / 4; ++s) {
         float bv[FM];

@@ -70,14 +70,18 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
     rb = (ci < cin && n < cout) ? *reinterpret_cast<const float4*>(w + ((int64_t)tap * cin + ci) * a.ld_w + n)
                                 : make_float4(0, 0, 0, 0);
   };
+  // A image [k][pixel] with the pixel index XOR-swizzled by bits 2-3 of k (element (k, m) at
+  // k * CLA + (m ^ swz(k))): the transposing stores (lanes 8 pixels x 4 k-quads) hit 32 distinct
+  // banks per 32-lane group instead of 8; fragment reads stay conflict-free (swz uniform per read)
+  auto swz = [](int k) { return ((k >> 2) & 3) << 3; };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if constexpr (VEC) {
-        float* d = &As[buf][a_k[i] * CLA + a_m[i]];
+        float* d = &As[buf][a_k[i] * CLA + (a_m[i] ^ swz(a_k[i]))];
         d[0] = ra[i].x; d[CLA] = ra[i].y; d[2 * CLA] = ra[i].z; d[3 * CLA] = ra[i].w;
       } else {
-        As[buf][a_k[i] * CLA + a_m[i]] = rs[i];
+        As[buf][a_k[i] * CLA + (a_m[i] ^ swz(a_k[i]))] = rs[i];
       }
     }
     *reinterpret_cast<float4*>(&Bs[buf][(tid >> 4) * CLB + (tid & 15) * 4]) = rb;
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
     for (int kk = 0; kk < CBK; kk += 4) {
       float av[2], bv[4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + wave * 32 + 16 * j + r];
+      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * 32 + 16 * j + r) ^ swz(kk))];
 #pragma unroll
       for (int i = 0; i < 4; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
 #pragma unroll
@@ -171,6 +175,18 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
     a_dy[i] = tap / ks - pad;
     a_dx[i] = tap % ks - pad;
   }
+  // the (slice, row, column) of each A pixel, divided out once and advanced by CBK pixels per slab
+  // (no 64-bit division in the loop: it was most of this kernel's VALU)
+  int64_t c_s[NA];
+  int c_y[NA], c_x[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int64_t p0 = kb + a_kk[i];
+    c_s[i] = p0 / HWp;
+    const int64_t rem = p0 % HWp;
+    c_y[i] = (int)(rem / W);
+    c_x[i] = (int)(rem % W);
+  }
   float4 ra[VEC ? 2 : 1];
   float rs[VEC ? 1 : 8];
   float4 rb;
@@ -178,25 +194,28 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int64_t pix = k0 + a_kk[i];
-      bool ok = a_ok[i] && pix < ke;
-      const int64_t pp = ok ? pix : 0;
-      const int64_t s = pp / HWp, rem = pp % HWp;
-      const int sy = (int)(rem / W) + a_dy[i], sx = (int)(rem % W) + a_dx[i];
-      ok = ok && sy >= 0 && sy < H && sx >= 0 && sx < W;
-      const float* p = x + (s * HWp + (int64_t)sy * W + sx) * a.ld_x + a_ci[i];
+      const int sy = c_y[i] + a_dy[i], sx = c_x[i] + a_dx[i];
+      const bool ok = a_ok[i] && pix < ke && sy >= 0 && sy < H && sx >= 0 && sx < W;
+      const float* p = x + (c_s[i] * HWp + (int64_t)sy * W + sx) * a.ld_x + a_ci[i];
       if constexpr (VEC) ra[i] = ok ? *reinterpret_cast<const float4*>(p) : make_float4(0, 0, 0, 0);
       else rs[i] = ok ? *p : 0.f;
+      c_x[i] += CBK;
+      while (c_x[i] >= W) {
+        c_x[i] -= W;
+        if (++c_y[i] == H) { c_y[i] = 0; ++c_s[i]; }
+      }
     }
     const int kr = tid >> 4, n4 = (tid & 15) * 4;
     const int64_t pix = k0 + kr;
     const int n = n0 + n4;
     rb = (pix < ke && n < cout) ? *reinterpret_cast<const float4*>(dy + pix * a.ld_y + n) : make_float4(0, 0, 0, 0);
   };
+  auto swz = [](int k) { return ((k >> 2) & 3) << 3; };   // the [k][m] swizzle of conv_fwd_kernel
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      if constexpr (VEC) *reinterpret_cast<float4*>(&As[buf][a_kk[i] * CLA + a_mm[i]]) = ra[i];
-      else As[buf][a_kk[i] * CLA + a_mm[i]] = rs[i];
+      if constexpr (VEC) *reinterpret_cast<float4*>(&As[buf][a_kk[i] * CLA + (a_mm[i] ^ swz(a_kk[i]))]) = ra[i];
+      else As[buf][a_kk[i] * CLA + (a_mm[i] ^ swz(a_kk[i]))] = rs[i];
     }
     *reinterpret_cast<float4*>(&Bs[buf][(tid >> 4) * CLB + (tid & 15) * 4]) = rb;
   };
@@ -219,7 +238,7 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
     for (int kk = 0; kk < CBK; kk += 4) {
       float av[2], bv[4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + wave * 32 + 16 * j + r];
+      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * 32 + 16 * j + r) ^ swz(kk))];
 #pragma unroll
       for (int i = 0; i < 4; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
 #pragma unroll

@@ -68,23 +68,30 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
       }
     }
   };
+  // LDS image [k][m] / [k][n] with the m (n) index XOR-swizzled by bits 2-3 of k:  element (k, m) at
+  // k * LP + (m ^ swz(k)).  The k-contiguous operand's transposing stores (lanes: 8 m x 4 k-quads)
+  // then hit 32 distinct banks per 32-lane group instead of 8 (4-way), and a fragment read (16 m x
+  // lanes g = k & 3) keeps its 16 + 16 banks (swz is uniform over the 4 k of a read).
+  auto swz = [](int k) { return ((k >> 2) & 3) << 3; };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + i * TNT;
       if constexpr (AM) {
-        *reinterpret_cast<float4*>(&As[buf][(c >> 5) * LP + (c & 31) * 4]) = ra[i];
+        const int k = c >> 5;
+        *reinterpret_cast<float4*>(&As[buf][k * LP + (((c & 31) * 4) ^ swz(k))]) = ra[i];
       } else {
-        const int m = c >> 2, k4 = (c & 3) * 4;
-        As[buf][(k4 + 0) * LP + m] = ra[i].x; As[buf][(k4 + 1) * LP + m] = ra[i].y;
-        As[buf][(k4 + 2) * LP + m] = ra[i].z; As[buf][(k4 + 3) * LP + m] = ra[i].w;
+        const int m = c >> 2, k4 = (c & 3) * 4, mm = m ^ swz(k4);
+        As[buf][(k4 + 0) * LP + mm] = ra[i].x; As[buf][(k4 + 1) * LP + mm] = ra[i].y;
+        As[buf][(k4 + 2) * LP + mm] = ra[i].z; As[buf][(k4 + 3) * LP + mm] = ra[i].w;
       }
       if constexpr (BNC) {
-        *reinterpret_cast<float4*>(&Bs[buf][(c >> 5) * LP + (c & 31) * 4]) = rb[i];
+        const int k = c >> 5;
+        *reinterpret_cast<float4*>(&Bs[buf][k * LP + (((c & 31) * 4) ^ swz(k))]) = rb[i];
       } else {
-        const int n = c >> 2, k4 = (c & 3) * 4;
-        Bs[buf][(k4 + 0) * LP + n] = rb[i].x; Bs[buf][(k4 + 1) * LP + n] = rb[i].y;
-        Bs[buf][(k4 + 2) * LP + n] = rb[i].z; Bs[buf][(k4 + 3) * LP + n] = rb[i].w;
+        const int n = c >> 2, k4 = (c & 3) * 4, nn = n ^ swz(k4);
+        Bs[buf][(k4 + 0) * LP + nn] = rb[i].x; Bs[buf][(k4 + 1) * LP + nn] = rb[i].y;
+        Bs[buf][(k4 + 2) * LP + nn] = rb[i].z; Bs[buf][(k4 + 3) * LP + nn] = rb[i].w;
       }
     }
   };
@@ -113,9 +120,9 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
     for (int kk = 0; kk < TBK; kk += 4) {
       float av[4], bv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) av[j] = as[(kk + g) * LP + wm + 16 * j + r];
+      for (int j = 0; j < 4; ++j) av[j] = as[(kk + g) * LP + ((wm + 16 * j + r) ^ swz(kk))];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = bs[(kk + g) * LP + wn + 16 * i + r];
+      for (int i = 0; i < 4; ++i) bv[i] = bs[(kk + g) * LP + ((wn + 16 * i + r) ^ swz(kk))];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -147,34 +154,54 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
   }
 }
 
-// C[m][n] = alpha * sum_s part[s][m][n] + beta * C[m][n], s in order
+// C[m][n] = alpha * sum_s part[s][m][n] + beta * C[m][n]: 16 float4 outputs x 16 split lanes per
+// workgroup (lane z takes splits z, z + 16, ...), then a fixed tree over the lanes
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, int64_t M,
                                                             int64_t N, float* __restrict__ C, int64_t ldc, float alpha,
                                                             int beta) {
-  const int64_t n4 = N / 4;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * n4) return;
-  const int64_t m = i / n4, n = (i % n4) * 4;
+  __shared__ float4 red[256];
+  const int64_t n4 = N / 4, total = M * n4;
+  const int ci = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + ci;
   float4 s = make_float4(0, 0, 0, 0);
-  for (int z = 0; z < splits; ++z) {
-    const float4 v = *reinterpret_cast<const float4*>(part + ((int64_t)z * M + m) * N + n);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  if (i < total) {
+    const float4* p4 = reinterpret_cast<const float4*>(part) + i;
+#pragma unroll 4
+    for (int z = zl; z < splits; z += 16) {
+      const float4 v = p4[(int64_t)z * total];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
   }
-  float4* p = reinterpret_cast<float4*>(C + m * ldc + n);
-  s.x *= alpha; s.y *= alpha; s.z *= alpha; s.w *= alpha;
-  if (beta) { const float4 o = *p; s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w; }
-  *p = s;
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off >= 16; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      const float4 o = red[threadIdx.x + off];
+      float4& r = red[threadIdx.x];
+      r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 16 && i < total) {
+    const int64_t m = i / n4, n = (i % n4) * 4;
+    float4 v = red[threadIdx.x];
+    float4* p = reinterpret_cast<float4*>(C + m * ldc + n);
+    v.x *= alpha; v.y *= alpha; v.z *= alpha; v.w *= alpha;
+    if (beta) { const float4 o = *p; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+    *p = v;
+  }
 }
 
-// Split count: fill ~2 rounds of 256 CUs with tiles x splits, each split at least 16 k-slabs.
+// Split count: fill ~4 workgroups per CU (1024) with tiles x splits, each split at least 16
+// k-slabs (256 k), at most 512 splits (a 128 x 128 weight gradient over 394k rows: 512 x 770 k).
 // Depends on the shape only (never the device), so results are reproducible across parts.
 int gemm_ex_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
   if (tiles >= 512) return 1;
-  int64_t s = (512 + tiles - 1) / tiles;
+  int64_t s = (1024 + tiles - 1) / tiles;
   const int64_t kmax = K / (TBK * 16);
   if (s > kmax) s = kmax;
-  if (s > 64) s = 64;
+  if (s > 512) s = 512;
   return s < 1 ? 1 : (int)s;
 }
 
@@ -253,8 +280,10 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   const int ci = threadIdx.x & 15, zl = threadIdx.x >> 4;
   const int64_t c = (int64_t)blockIdx.x * 16 + ci;
   float s = 0.f;
-  if (c < cols)
+  if (c < cols) {
+#pragma unroll 8
     for (int64_t z = zl; z < chunks; z += 16) s += part[z * cols + c];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   for (int off = 128; off >= 16; off >>= 1) {
@@ -308,7 +337,7 @@ extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
 #undef GEX
   if (splits > 1) {
     const int64_t n = g->M * (g->N / 4);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, splits, g->M,
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, part, splits, g->M,
                        g->N, (float*)g->C, g->ldc, g->alpha, g->beta);
   }
   return catseg_launch_status("gemm_ex");

@@ -85,16 +85,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     part[(int64_t)blockIdx.x * 2 * cols + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
 }
 
-// dgamma / dbeta = sum of the per-workgroup partials, in workgroup order
+// dgamma / dbeta = sum of the per-workgroup partials: 16 columns x 16 partial lanes per workgroup
+// (lane z takes partials z, z + 16, ...), then a fixed tree over the lanes
 __global__ __launch_bounds__(256) void ln_param_final_kernel(const float* __restrict__ part, int nwg, int cols,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                              int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 2 * cols) return;
+  __shared__ float red[256];
+  const int ci = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + ci;
   float s = 0.f;
-  for (int w = 0; w < nwg; ++w) s += part[(int64_t)w * 2 * cols + c];
-  float* o = c < cols ? dgamma + c : dbeta + (c - cols);
-  *o = acc ? *o + s : s;
+  if (c < 2 * cols) {
+#pragma unroll 8
+    for (int w = zl; w < nwg; w += 16) s += part[(int64_t)w * 2 * cols + c];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off >= 16; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 16 && c < 2 * cols) {
+    float* o = c < cols ? dgamma + c : dbeta + (c - cols);
+    *o = acc ? *o + red[threadIdx.x] : red[threadIdx.x];
+  }
 }
 
 // ---------------------------------------------------------------------------------- activations
@@ -381,6 +394,7 @@ __global__ __launch_bounds__(256) void sum_classes_kernel(const float* __restric
   const int c = (int)(i % c4n) * 4;
   const int64_t bp = i / c4n, b = bp / HW, p = bp % HW;
   float4 s = make_float4(0, 0, 0, 0);
+#pragma unroll 8
   for (int t = 0; t < T; ++t) {
     const float4 v = *reinterpret_cast<const float4*>(x + ((b * T + t) * HW + p) * ld_x + c);
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -401,6 +415,7 @@ __global__ __launch_bounds__(256) void sum_pixels_kernel(const float* __restrict
   if (c < C)
     for (int64_t b = 0; b < B; ++b) {
       const float* base = x + (b * T + t) * HW * ld_x + c;
+#pragma unroll 8
       for (int64_t p = q; p < HW; p += 4) s += base[p * ld_x];
     }
   red[q][threadIdx.x & 63] = s;
@@ -601,7 +616,7 @@ extern "C" int catseg_layernorm_backward(const float* x, int64_t ld_x, const flo
   }
 #undef LNB
   if (dgamma)
-    hipLaunchKernelGGL(ln_param_final_kernel, dim3((unsigned)((2 * cols + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(ln_param_final_kernel, dim3((unsigned)((2 * cols + 15) / 16)), dim3(256), 0, st,
                        (const float*)part, grid, (int)cols, dgamma, dbeta, acc_param);
   return catseg_launch_status("layernorm_backward");
 }

@@ -82,14 +82,23 @@ def main():
         ops.PROFILE = []
         step()
         torch.cuda.synchronize()
-        fam = {}
+        fam, shp = {}, {}
         for r in ops.PROFILE:
             ms = r["start"].elapsed_time(r["end"])
             f = fam.setdefault(r["kernel"], [0.0, 0, 0.0])
             f[0] += ms
             f[1] += 1
             f[2] += r["flops"]
+            if r.get("shape") is not None:
+                g = shp.setdefault((r["kernel"],) + tuple(r["shape"]), [0.0, 0, 0.0])
+                g[0] += ms
+                g[1] += 1
+                g[2] += r["flops"]
         ops.PROFILE = None
+        # the GEMM launches by shape (M, N, K[, A / B contiguous dimension]): where the GEMM time goes
+        out["gemm_shapes"] = [{"kernel": k[0], "shape": list(k[1:]), "ms": round(v[0], 3), "launches": v[1],
+                               "tflops": round(v[2] / (v[0] * 1e9), 1) if v[0] > 0 else None}
+                              for k, v in sorted(shp.items(), key=lambda kv: -kv[1][0])[:40]]
         tot = sum(v[0] for v in fam.values())
         out["kernels_ms"] = {k: {"ms": round(v[0], 3), "launches": v[1],
                                  "tflops": round(v[2] / (v[0] * 1e9), 1) if v[0] > 0 and v[2] else None}
