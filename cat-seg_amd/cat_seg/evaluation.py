@@ -68,17 +68,35 @@ def coco_rle_encode(mask: np.ndarray) -> dict:
         edges = np.flatnonzero(flat[1:] != flat[:-1]) + 1
         runs = np.diff(np.concatenate(([0], edges, [flat.size])))
         cnts = ([0] if flat[0] else []) + runs.tolist()
-    out = []
-    for i, c in enumerate(cnts):
-        x = int(c) - (int(cnts[i - 2]) if i > 2 else 0)
-        while True:
-            g = x & 0x1F
-            x >>= 5
-            more = (x != -1) if (g & 0x10) else (x != 0)
-            out.append(chr((g | 0x20 if more else g) + 48))
-            if not more:
-                break
-    return {"size": [int(h), int(w)], "counts": "".join(out)}
+    # rleToString, vectorised: x_i = c_i - c_{i-2} (i > 2), n_i = the fewest 5-bit groups whose
+    # two's complement holds x_i (the loop "until the rest is the last group's sign extension")
+    c = np.asarray(cnts, dtype=np.int64)
+    x = c.copy()
+    if c.size > 3:
+        x[3:] -= c[1:-2]
+    n = np.ones_like(x)
+    for k in range(1, 7):
+        lim = 1 << (5 * k - 1)
+        n += (x >= lim) | (x < -lim)
+    ks = np.arange(int(n.max()))
+    groups = (x[:, None] >> (5 * ks)[None, :]) & 0x1F
+    more = ks[None, :] < (n[:, None] - 1)
+    chars = groups + 48 + np.where(more, 0x20, 0)
+    out = chars[ks[None, :] < n[:, None]].astype(np.uint8).tobytes().decode("ascii")
+    return {"size": [int(h), int(w)], "counts": out}
+
+
+_OBJ_GROUP = []
+
+
+def _object_group():
+    """A gloo process group over all ranks for object collectives (created once, collectively);
+    None (the default group) when the default backend is gloo already."""
+    if dist.get_backend() == "gloo":
+        return None
+    if not _OBJ_GROUP:
+        _OBJ_GROUP.append(dist.new_group(backend="gloo"))
+    return _OBJ_GROUP[0]
 
 
 def reduce_confusion(conf: torch.Tensor) -> torch.Tensor:
@@ -213,7 +231,9 @@ class SemSegEvaluator:
         (plain_train_net.py:139-140)."""
         if self._distributed and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             parts = [None] * dist.get_world_size()
-            dist.all_gather_object(parts, self._predictions)
+            # Python objects go through a gloo group (as detectron2's comm.all_gather does), never
+            # pickled into device buffers of the RCCL group
+            dist.all_gather_object(parts, self._predictions, group=_object_group())
             return [r for part in parts for r in part]
         return list(self._predictions)
 

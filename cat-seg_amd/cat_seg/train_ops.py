@@ -280,7 +280,7 @@ def conv2d(x, w, y, *, S, H, W, cin, cout, ksize=3, bias=None, act=L.ACT_NONE, a
     _chk(x, w, y, bias)
     a = _conv_args(x, w, y, S=S, H=H, W=W, cin=cin, cout=cout, ksize=ksize, bias=bias, act=act, alpha=alpha,
                    beta=beta, ld_x=ld_x, ld_y=ld_y)
-    with _rec("conv2d", 2 * S * H * W * cout * cin * ksize * ksize):
+    with _rec("conv2d", 2 * S * H * W * cout * cin * ksize * ksize, shape=(S * H * W, cin, cout, ksize)):
         call("catseg_conv2d_nhwc", a, _stream())
     return y
 
@@ -293,7 +293,7 @@ def conv2d_wgrad(x, dy, dw, *, S, H, W, cin, cout, ksize=3, alpha=1.0, beta=0, l
     ws = _ws(L.load().catseg_conv2d_wgrad_workspace(C.byref(a)), x.device)
     if ws is not None:
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
-    with _rec("conv2d_wgrad", 2 * S * H * W * cout * cin * ksize * ksize):
+    with _rec("conv2d_wgrad", 2 * S * H * W * cout * cin * ksize * ksize, shape=(S * H * W, cin, cout, ksize)):
         call("catseg_conv2d_wgrad", a, _stream())
     return dw
 

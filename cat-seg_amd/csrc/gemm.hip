@@ -162,8 +162,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
                                                   const TA* __restrict__ W, int64_t ldw,
                                                   int64_t M, int64_t N, int64_t K, EpiArgs e) {
   constexpr int VN = Vec16<TA>::N;           // elements per 16-byte chunk
-  constexpr int CPR = BK / VN;               // chunks per tile row
-  constexpr int LDR = BK + Lds<TA>::PAD;     // LDS row stride (elements)
+  // fp32 K-tile 16 (bf16: 32): 37 KB of LDS per 128 x 128 workgroup, four workgroups per CU
+  constexpr int BKT = sizeof(TA) == 4 ? 16 : BK;
+  constexpr int CPR = BKT / VN;              // chunks per tile row
+  constexpr int LDR = BKT + Lds<TA>::PAD;    // LDS row stride (elements)
   constexpr int A_CH = BM * CPR / NT;        // chunks per thread
   constexpr int W_CH = BN * CPR / NT;
   static_assert(A_CH >= 1 && W_CH >= 1, "tile too small");
@@ -230,13 +232,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int ktiles = (int)((K + BK - 1) / BK);
+  const int ktiles = (int)((K + BKT - 1) / BKT);
   gload(0);
   sstore(0);
   __syncthreads();
   for (int kt = 0; kt < ktiles; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BK);
+    if (kt + 1 < ktiles) gload((int64_t)(kt + 1) * BKT);
     const TA* As = sA[buf];
     const TA* Ws = sW[buf];
     if constexpr (sizeof(TA) == 2) {
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const TA* __restrict__ A, int6
     } else {
       const int r = lane & 15, kq = (lane >> 4) ^ (((lane >> 3) & 1) << 1);   // rot() above
 #pragma unroll
-      for (int s = 0; s < BK / 4; ++s) {
+      for (int s = 0; s < BKT / 4; ++s) {
         float bv[FM];
 #pragma unroll
         for (int j = 0; j < FM; ++j) bv[j] = As[(wm + 16 * j + r) * LDR + 4 * s + kq];
@@ -852,7 +854,11 @@ void launch_tiles(const CatsegGemmArgs* g, hipStream_t st) {
     else if (t128 < 512) launch2<TO, 64, 128>(g, st);     // fill 256 CUs x 2 slots
     else launch2<TO, 128, 128>(g, st);
   } else {
-    if (g->N <= 64) launch<TA, TO, 128, 64>(g, st);
+    // fp32: 64 x 64 tiles when 128 x 128 would leave most CUs idle (the CLIP GEMMs of the training
+    // step at M = 4 x 577 / 171 x 12 rows: 68-114 tiles)
+    const int64_t t128 = ((g->M + 127) / 128) * ((g->N + 127) / 128);
+    if (t128 < 256) launch<TA, TO, 64, 64>(g, st);
+    else if (g->N <= 64) launch<TA, TO, 128, 64>(g, st);
     else launch<TA, TO, 128, 128>(g, st);
   }
 }

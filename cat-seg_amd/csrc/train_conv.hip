@@ -17,18 +17,25 @@
 
 namespace {
 
-constexpr int CBM = 128, CBN = 64, CBK = 16, CNT = 256;
-constexpr int CLA = CBM + 16, CLB = CBN + 16;   // LDS pitches
+constexpr int CBK = 16, CNT = 256;
+// Tiles (pixels or (tap, ci) rows x output channels): 128 x 64 (four waves of 32 x 64) for cout > 32,
+// 256 x 32 (four waves of 64 x 32) for cout <= 32, so the 32-channel decoder convs spend no MFMA on
+// zero weight columns; either way a wave issues 8 MFMAs per 4-deep k-step.
+// [k][m] images: element (k, m) at k * pitch + (m ^ swz(k)): the transposing stores (8 m x 4 k-quads
+// per 32-lane group) hit 32 distinct banks, fragment reads (16 m x 2 k per group) stay conflict-free
+DEV int swz(int k) { return ((k >> 2) & 3) << 3; }
 
-template <bool VEC>
+template <bool VEC, int BMT, int BNT>
 __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int tiles_n) {
+  constexpr int CLA = BMT + 16, CLB = BNT + 16;
+  constexpr int WM = BMT / 4, FM = WM / 16, FN = BNT / 16;
   __shared__ __attribute__((aligned(16))) float As[2][CBK * CLA];
   __shared__ __attribute__((aligned(16))) float Bs[2][CBK * CLB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t m0 = (int64_t)(lin / tiles_n) * CBM;
-  const int n0 = (lin % tiles_n) * CBN;
+  const int64_t m0 = (int64_t)(lin / tiles_n) * BMT;
+  const int n0 = (lin % tiles_n) * BNT;
   const float* x = (const float*)a.x;
   const float* w = (const float*)a.w;
   const int H = a.H, W = a.W, cin = a.cin, cout = a.cout, ks = a.ksize, pad = a.pad;
@@ -36,8 +43,8 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
   const int nkc = (cin + CBK - 1) / CBK;
   const int nslab = ks * ks * nkc;
 
-  // per-thread A rows (fixed over K): VEC 2 chunks of 4 channels, else 8 scalars
-  constexpr int NA = VEC ? 2 : 8;
+  // per-thread A rows (fixed over K): VEC chunks of 4 channels, else scalars
+  constexpr int NA = VEC ? BMT / 64 : BMT / 16;
   int64_t a_base[NA]; int a_y[NA], a_x[NA], a_k[NA], a_m[NA]; bool a_ok[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -51,9 +58,11 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
     a_y[i] = (int)(rem / W); a_x[i] = (int)(rem % W);
     a_base[i] = s * HWp;
   }
-  float4 ra[VEC ? 2 : 1];
-  float rs[VEC ? 1 : 8];
+  float4 ra[VEC ? NA : 1];
+  float rs[VEC ? 1 : NA];
   float4 rb;
+  constexpr int BQ = BNT / 4;                 // float4 per weight row of the tile
+  const bool b_on = tid < CBK * BQ;
   auto gload = [&](int slab) {
     const int tap = slab / nkc, ci0 = (slab % nkc) * CBK;
     const int dy = tap / ks - pad, dx = tap % ks - pad;
@@ -65,15 +74,11 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
       if constexpr (VEC) ra[i] = ok ? *reinterpret_cast<const float4*>(p) : make_float4(0, 0, 0, 0);
       else rs[i] = ok ? *p : 0.f;
     }
-    const int kr = tid >> 4, n4 = (tid & 15) * 4;
+    const int kr = tid / BQ, n4 = (tid % BQ) * 4;
     const int ci = ci0 + kr, n = n0 + n4;
-    rb = (ci < cin && n < cout) ? *reinterpret_cast<const float4*>(w + ((int64_t)tap * cin + ci) * a.ld_w + n)
-                                : make_float4(0, 0, 0, 0);
+    rb = (b_on && ci < cin && n < cout) ? *reinterpret_cast<const float4*>(w + ((int64_t)tap * cin + ci) * a.ld_w + n)
+                                        : make_float4(0, 0, 0, 0);
   };
-  // A image [k][pixel] with the pixel index XOR-swizzled by bits 2-3 of k (element (k, m) at
-  // k * CLA + (m ^ swz(k))): the transposing stores (lanes 8 pixels x 4 k-quads) hit 32 distinct
-  // banks per 32-lane group instead of 8; fragment reads stay conflict-free (swz uniform per read)
-  auto swz = [](int k) { return ((k >> 2) & 3) << 3; };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -84,14 +89,14 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
         As[buf][a_k[i] * CLA + (a_m[i] ^ swz(a_k[i]))] = rs[i];
       }
     }
-    *reinterpret_cast<float4*>(&Bs[buf][(tid >> 4) * CLB + (tid & 15) * 4]) = rb;
+    if (b_on) *reinterpret_cast<float4*>(&Bs[buf][(tid / BQ) * CLB + (tid % BQ) * 4]) = rb;
   };
 
-  f32x4 acc[4][2];
+  f32x4 acc[FN][FM];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   gload(0);
   sstore(0);
   __syncthreads();
@@ -100,22 +105,22 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
     if (sl + 1 < nslab) gload(sl + 1);
 #pragma unroll
     for (int kk = 0; kk < CBK; kk += 4) {
-      float av[2], bv[4];
+      float av[FM], bv[FN];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * 32 + 16 * j + r) ^ swz(kk))];
+      for (int j = 0; j < FM; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * WM + 16 * j + r) ^ swz(kk))];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
+      for (int i = 0; i < FN; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
     }
     if (sl + 1 < nslab) sstore(buf ^ 1);
     __syncthreads();
   }
   float* y = (float*)a.y;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < FN; ++i) {
     const int n = n0 + 16 * i + 4 * g;
     if (n >= cout) continue;
     float bias[4] = {0.f, 0.f, 0.f, 0.f};
@@ -124,8 +129,8 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
       for (int u = 0; u < 4; ++u) bias[u] = a.bias[n + u];
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t m = m0 + wave * 32 + 16 * j + r;
+    for (int j = 0; j < FM; ++j) {
+      const int64_t m = m0 + wave * WM + 16 * j + r;
       if (m >= M) continue;
       float* p = y + m * a.ld_y + n;
       float v[4];
@@ -142,16 +147,18 @@ __global__ __launch_bounds__(CNT) void conv_fwd_kernel(CatsegConv2dArgs a, int t
   }
 }
 
-template <bool VEC>
+template <bool VEC, int BMT, int BNT>
 __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int tiles_n, int64_t k_chunk,
                                                          float* __restrict__ part) {
+  constexpr int CLA = BMT + 16, CLB = BNT + 16;
+  constexpr int WM = BMT / 4, FM = WM / 16, FN = BNT / 16;
   __shared__ __attribute__((aligned(16))) float As[2][CBK * CLA];
   __shared__ __attribute__((aligned(16))) float Bs[2][CBK * CLB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (lin / tiles_n) * CBM;
-  const int n0 = (lin % tiles_n) * CBN;
+  const int m0 = (lin / tiles_n) * BMT;
+  const int n0 = (lin % tiles_n) * BNT;
   const float* x = (const float*)a.x;
   const float* dy = (const float*)a.y;
   const int H = a.H, W = a.W, cin = a.cin, cout = a.cout, ks = a.ksize, pad = a.pad;
@@ -160,14 +167,15 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
   const int64_t kb = (int64_t)blockIdx.y * k_chunk;
   const int64_t ke = kb + k_chunk < K ? kb + k_chunk : K;
 
-  // per-thread A columns (tap, ci) fixed over K
-  constexpr int NA = VEC ? 2 : 8;
+  // per-thread A columns (tap, ci) fixed over K; pixel row a_kk of the 16-pixel slab
+  constexpr int AQ = VEC ? BMT / 4 : BMT;     // A items per slab row
+  constexpr int NA = CBK * AQ / CNT;
   int a_kk[NA], a_mm[NA], a_dy[NA], a_dx[NA], a_ci[NA]; bool a_ok[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int c = tid + i * CNT;
-    a_kk[i] = VEC ? c >> 5 : c >> 7;
-    a_mm[i] = VEC ? (c & 31) * 4 : c & 127;
+    a_kk[i] = c / AQ;
+    a_mm[i] = VEC ? (c % AQ) * 4 : c % AQ;
     const int m = m0 + a_mm[i];
     a_ok[i] = m < M;
     const int tap = a_ok[i] ? m / cin : 0;
@@ -187,9 +195,11 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
     c_y[i] = (int)(rem / W);
     c_x[i] = (int)(rem % W);
   }
-  float4 ra[VEC ? 2 : 1];
-  float rs[VEC ? 1 : 8];
+  float4 ra[VEC ? NA : 1];
+  float rs[VEC ? 1 : NA];
   float4 rb;
+  constexpr int BQ = BNT / 4;
+  const bool b_on = tid < CBK * BQ;
   auto gload = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -205,26 +215,26 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
         if (++c_y[i] == H) { c_y[i] = 0; ++c_s[i]; }
       }
     }
-    const int kr = tid >> 4, n4 = (tid & 15) * 4;
+    const int kr = tid / BQ, n4 = (tid % BQ) * 4;
     const int64_t pix = k0 + kr;
     const int n = n0 + n4;
-    rb = (pix < ke && n < cout) ? *reinterpret_cast<const float4*>(dy + pix * a.ld_y + n) : make_float4(0, 0, 0, 0);
+    rb = (b_on && pix < ke && n < cout) ? *reinterpret_cast<const float4*>(dy + pix * a.ld_y + n)
+                                        : make_float4(0, 0, 0, 0);
   };
-  auto swz = [](int k) { return ((k >> 2) & 3) << 3; };   // the [k][m] swizzle of conv_fwd_kernel
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if constexpr (VEC) *reinterpret_cast<float4*>(&As[buf][a_kk[i] * CLA + (a_mm[i] ^ swz(a_kk[i]))]) = ra[i];
       else As[buf][a_kk[i] * CLA + (a_mm[i] ^ swz(a_kk[i]))] = rs[i];
     }
-    *reinterpret_cast<float4*>(&Bs[buf][(tid >> 4) * CLB + (tid & 15) * 4]) = rb;
+    if (b_on) *reinterpret_cast<float4*>(&Bs[buf][(tid / BQ) * CLB + (tid % BQ) * 4]) = rb;
   };
 
-  f32x4 acc[4][2];
+  f32x4 acc[FN][FM];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = ke > kb ? (int)((ke - kb + CBK - 1) / CBK) : 0;
   if (nk > 0) {
     gload(kb);
@@ -236,27 +246,27 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
     if (kt + 1 < nk) gload(kb + (int64_t)(kt + 1) * CBK);
 #pragma unroll
     for (int kk = 0; kk < CBK; kk += 4) {
-      float av[2], bv[4];
+      float av[FM], bv[FN];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * 32 + 16 * j + r) ^ swz(kk))];
+      for (int j = 0; j < FM; ++j) av[j] = As[buf][(kk + g) * CLA + ((wave * WM + 16 * j + r) ^ swz(kk))];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
+      for (int i = 0; i < FN; ++i) bv[i] = Bs[buf][(kk + g) * CLB + 16 * i + r];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
   float* dst = part ? part + (int64_t)blockIdx.y * M * cout : (float*)a.dw;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < FN; ++i) {
     const int n = n0 + 16 * i + 4 * g;
     if (n >= cout) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = m0 + wave * 32 + 16 * j + r;
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wave * WM + 16 * j + r;
       if (m >= M) continue;
       float* p = dst + (int64_t)m * cout + n;
       float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -269,18 +279,34 @@ __global__ __launch_bounds__(CNT) void conv_wgrad_kernel(CatsegConv2dArgs a, int
   }
 }
 
+// dw[i] = alpha * sum_z part[z][i] + beta * dw[i]: 16 outputs x 16 split lanes per workgroup, fixed tree
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int64_t n,
                                                            float* __restrict__ dw, float alpha, int beta) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+  __shared__ float red[256];
+  const int ci = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + ci;
   float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += part[(int64_t)z * n + i];
-  dw[i] = alpha * s + (beta ? dw[i] : 0.f);
+  if (i < n) {
+#pragma unroll 8
+    for (int z = zl; z < splits; z += 16) s += part[(int64_t)z * n + i];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off >= 16; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 16 && i < n) dw[i] = alpha * red[threadIdx.x] + (beta ? dw[i] : 0.f);
 }
+
+// the tile for an output-channel count
+struct ConvTile { int bm, bn; };
+ConvTile conv_tile(int cout) { return cout <= 32 ? ConvTile{256, 32} : ConvTile{128, 64}; }
 
 int wgrad_splits(const CatsegConv2dArgs* a) {
   const int64_t M = (int64_t)a->ksize * a->ksize * a->cin;
-  const int64_t tiles = ((M + CBM - 1) / CBM) * ((a->cout + CBN - 1) / CBN);
+  const ConvTile t = conv_tile(a->cout);
+  const int64_t tiles = ((M + t.bm - 1) / t.bm) * ((a->cout + t.bn - 1) / t.bn);
   const int64_t K = a->S * a->H * a->W;
   int64_t s = (1024 + tiles - 1) / tiles;
   const int64_t kmax = K / (CBK * 64);
@@ -426,13 +452,19 @@ extern "C" int catseg_conv2d_nhwc(const CatsegConv2dArgs* a, void* stream) {
   CATSEG_CHECK(a->w && a->ld_w >= a->cout && a->ld_w % 4 == 0 && ((uintptr_t)a->w % 16) == 0, "conv2d: bad weight");
   CATSEG_CHECK(a->act == ACT_NONE || a->act == ACT_RELU, "conv2d: act must be none or relu");
   const int64_t M = a->S * a->H * a->W;
-  const int64_t tm = (M + CBM - 1) / CBM, tn = (a->cout + CBN - 1) / CBN;
+  const ConvTile t = conv_tile(a->cout);
+  const int64_t tm = (M + t.bm - 1) / t.bm, tn = (a->cout + t.bn - 1) / t.bn;
   CATSEG_CHECK(tm * tn < (1LL << 31), "conv2d: too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  if (a->cin % 4 == 0)
-    hipLaunchKernelGGL((conv_fwd_kernel<true>), dim3((unsigned)(tm * tn)), dim3(CNT), 0, st, *a, (int)tn);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<false>), dim3((unsigned)(tm * tn)), dim3(CNT), 0, st, *a, (int)tn);
+  const dim3 grid((unsigned)(tm * tn));
+  const bool vec = a->cin % 4 == 0;
+  if (t.bn == 32) {
+    if (vec) hipLaunchKernelGGL((conv_fwd_kernel<true, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn);
+    else hipLaunchKernelGGL((conv_fwd_kernel<false, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn);
+  } else {
+    if (vec) hipLaunchKernelGGL((conv_fwd_kernel<true, 128, 64>), grid, dim3(CNT), 0, st, *a, (int)tn);
+    else hipLaunchKernelGGL((conv_fwd_kernel<false, 128, 64>), grid, dim3(CNT), 0, st, *a, (int)tn);
+  }
   return catseg_launch_status("conv2d_nhwc");
 }
 
@@ -447,7 +479,8 @@ extern "C" int catseg_conv2d_wgrad(const CatsegConv2dArgs* a, void* stream) {
   CATSEG_CHECK(a->dw && ((uintptr_t)a->dw % 16) == 0, "conv2d_wgrad: dw missing / unaligned");
   const int64_t M = (int64_t)a->ksize * a->ksize * a->cin;
   CATSEG_CHECK(M < (1LL << 30), "conv2d_wgrad: weight too large");
-  const int64_t tm = (M + CBM - 1) / CBM, tn = (a->cout + CBN - 1) / CBN;
+  const ConvTile t = conv_tile(a->cout);
+  const int64_t tm = (M + t.bm - 1) / t.bm, tn = (a->cout + t.bn - 1) / t.bn;
   const int splits = wgrad_splits(a);
   const int64_t need = splits > 1 ? (int64_t)splits * M * a->cout * (int64_t)sizeof(float) : 0;
   if (splits > 1) CATSEG_CHECK(a->workspace && a->workspace_bytes >= need, "conv2d_wgrad: workspace too small");
@@ -457,13 +490,17 @@ extern "C" int catseg_conv2d_wgrad(const CatsegConv2dArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   float* part = splits > 1 ? (float*)a->workspace : nullptr;
   dim3 grid((unsigned)(tm * tn), (unsigned)splits);
-  if (a->cin % 4 == 0)
-    hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
-  else
-    hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+  const bool vec = a->cin % 4 == 0;
+  if (t.bn == 32) {
+    if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<true, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<false, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+  } else {
+    if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<true, 128, 64>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<false, 128, 64>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+  }
   if (splits > 1) {
     const int64_t n = M * a->cout;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const float*)part,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, (const float*)part,
                        splits, n, (float*)a->dw, a->alpha, a->beta);
   }
   return catseg_launch_status("conv2d_wgrad");

@@ -304,10 +304,12 @@ def test_linear_attention_backward(T, n_pad):
         close(dvp, vp.grad)
 
 
-@pytest.mark.parametrize("cin,cout,k,relu", [(96, 64, 3, False), (64, 32, 3, True), (1, 128, 7, False),
-                                             (128, 16, 3, True), (20, 8, 3, False)])
-def test_conv2d_forward_dgrad_wgrad(cin, cout, k, relu):
-    S, H, W = 3, 24, 20
+@pytest.mark.parametrize("cin,cout,k,relu,S", [(96, 64, 3, False, 3), (64, 32, 3, True, 3), (1, 128, 7, False, 3),
+                                               (128, 16, 3, True, 3), (20, 8, 3, False, 3),
+                                               (32, 32, 3, True, 24),     # weight gradient split over 11 pixel ranges
+                                               (96, 64, 3, False, 40)])   # 256 x 32 and 128 x 64 tiles, split-K
+def test_conv2d_forward_dgrad_wgrad(cin, cout, k, relu, S):
+    H, W = 24, 20
     x = g(S, cin, H, W, seed=28)
     w = g(cout, cin, k, k, seed=29) / math.sqrt(cin * k * k)
     b = g(cout, seed=30)
