@@ -192,14 +192,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// Split count: fill ~4 workgroups per CU (1024) with tiles x splits, each split at least 16
-// k-slabs (256 k), at most 512 splits (a 128 x 128 weight gradient over 394k rows: 512 x 770 k).
-// Depends on the shape only (never the device), so results are reproducible across parts.
+// Split count: only when the tiles alone leave CUs idle (< 256 tiles), then ~4 workgroups per CU
+// (1024) of tiles x splits, each split at least 8 k-slabs (128 k), at most 512 splits.  Measured on
+// the training step's shapes (tools/micro_gemm_ex_splits.py): 456 tiles x 3 splits of K 768 took
+// 192 us against 119 unsplit (the partials' traffic), 16 tiles of K 2052 25 us at 16 splits against
+// 34 at 8.  Depends on the shape only (never the device), so results are reproducible across parts.
+int g_gemm_ex_splits = 0;   // tuning: > 0 forces the split count (capped by K / 16 and 512)
 int gemm_ex_splits(int64_t M, int64_t N, int64_t K) {
+  if (g_gemm_ex_splits > 0) {
+    int64_t f = g_gemm_ex_splits, kmax = (K + TBK - 1) / TBK;
+    if (f > kmax) f = kmax;
+    return (int)(f > 512 ? 512 : f);
+  }
   const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
-  if (tiles >= 512) return 1;
+  if (tiles >= 256) return 1;
   int64_t s = (1024 + tiles - 1) / tiles;
-  const int64_t kmax = K / (TBK * 16);
+  const int64_t kmax = K / (TBK * 8);
   if (s > kmax) s = kmax;
   if (s > 512) s = 512;
   return s < 1 ? 1 : (int)s;
@@ -294,6 +302,8 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 }
 
 }  // namespace
+
+CATSEG_KNOB(g_gemm_ex_splits, "gemm_ex_splits");
 
 extern "C" int64_t catseg_gemm_ex_workspace(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
