@@ -115,18 +115,21 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
       const float mn = fmaxf(m_l, tm);
       float add = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) add += expf(sc[j] - mn);
-      l_l = l_l * expf(m_l - mn) + add;
+      for (int j = 0; j < 4; ++j) add += __expf(sc[j] - mn);
+      l_l = l_l * __expf(m_l - mn) + add;
       m_l = mn;
     }
     const float M = xrow4_max(m_l);
-    const float Lsum = xrow4_sum(l_l * expf(m_l - M));
+    const float Lsum = xrow4_sum(l_l * __expf(m_l - M));
     if (g == 0) { mst[qi] = M; lst[qi] = 1.f / Lsum; }
   }
   __syncthreads();
 
-  // ---- pass A: waves own key tiles; dV = P^T dO, dK = scale dS^T Q ----
-  for (int kt = wave; kt < NT; kt += 4) {
+  // ---- passes A and B as one list of 2 NT items dealt round-robin over the waves (item < NT: pass A
+  // for key tile item, else pass B for query tile item - NT): with NT = 9 the longest wave does 3 A +
+  // 2 B items instead of 3 A + 3 B when each pass is dealt on its own ----
+  // pass A: the wave owns a key tile; dV = P^T dO, dK = scale dS^T Q
+  auto pass_a = [&](int kt) {
     f32x4 dV[2], dK[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) { dV[e] = f32x4{0.f, 0.f, 0.f, 0.f}; dK[e] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
       for (int j = 0; j < 4; ++j) {
         const int qj = qt * 16 + 4 * g + j;
         const float sc = scale * sa[j] + ((masked && reg[qj] != rk) ? -100.f : 0.f);
-        P[j] = expf(sc - mst[qj]) * lst[qj];
+        P[j] = __expf(sc - mst[qj]) * lst[qj];
         dS[j] = P[j] * (pa[j] - Dst[qj]);
       }
 #pragma unroll
@@ -169,10 +172,10 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
         dk[row * a.ld_dqkv + col + 16 * e + r] = scale * dK[e][j];
       }
     }
-  }
+  };
 
-  // ---- pass B: waves own query tiles; dQ = scale dS K ----
-  for (int qt = wave; qt < NT; qt += 4) {
+  // pass B: the wave owns a query tile; dQ = scale dS K
+  auto pass_b = [&](int qt) {
     f32x4 dQ[2];
     dQ[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     dQ[1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
       for (int j = 0; j < 4; ++j) {
         const int kj = kt * 16 + 4 * g + j;
         const float sc = scale * sa[j] + ((masked && reg[kj] != rq) ? -100.f : 0.f);
-        dS[j] = expf(sc - mq) * lq * (pa[j] - Dq);
+        dS[j] = __expf(sc - mq) * lq * (pa[j] - Dq);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -207,6 +210,11 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(CatsegWinAttnBwdArgs 
 #pragma unroll
       for (int e = 0; e < 2; ++e) dq[row * a.ld_dqkv + col + 16 * e + r] = scale * dQ[e][j];
     }
+  };
+
+  for (int it = wave; it < 2 * NT; it += 4) {
+    if (it < NT) pass_a(it);
+    else pass_b(it - NT);
   }
 }
 
@@ -441,8 +449,8 @@ constexpr int LD = 32;     // head_dim
 constexpr int LCH = 32;    // tokens staged per chunk
 constexpr int KVP = 33;    // LDS pitch of the 32x32 states
 
-DEV float phi(float x) { return x > 0.f ? x + 1.f : expf(x); }       // elu(x) + 1
-DEV float dphi(float x) { return x > 0.f ? 1.f : expf(x); }
+DEV float phi(float x) { return x > 0.f ? x + 1.f : __expf(x); }       // elu(x) + 1
+DEV float dphi(float x) { return x > 0.f ? 1.f : __expf(x); }
 
 struct LinWave {
   float kv[LD * KVP];     // KV (phase 1-2), then dKV (phase 3)
