@@ -10,6 +10,8 @@
 #   bash tools/gpu.sh TAG pmc [HEAD]               FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic.json
 #   bash tools/gpu.sh TAG sq [SCRIPT]              SQ stall / mix / LDS / MFMA-busy passes -> summary.txt, mfma_util.txt
 #   bash tools/gpu.sh TAG final [HEAD]             tests + smoke + headline (with CPU leg) + configs + trace + pmc + sq
+#   bash tools/gpu.sh TAG final1                    the first half of final: tests + smoke + headline + configs
+#   bash tools/gpu.sh TAG final2 [HEAD]             the second half: trace + pmc + sq + the training step
 #   bash tools/gpu.sh TAG micro SCRIPT [ARGS...]   one tools/micro_*.py run
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
@@ -81,5 +83,7 @@ case "$CMD" in
   sq) sq "$@" ;;
   micro) micro "$@" ;;
   final) tests && smoke && bench && configs && trace && pmc "$@" && sq ;;
+  final1) tests && smoke && bench --cpu-images -1 && configs ;;
+  final2) trace && pmc "$@" && sq && train ;;
   *) echo "unknown command $CMD" >&2; exit 2 ;;
 esac
