@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--finetune", default="attention", choices=["attention", "none", "full"])
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--image", type=int, default=384,
+                    help="training crop (the reference's INPUT.CROP.SIZE (384, 384) for B/16 and L/14; the "
+                         "CLIP encoder sees it resized to its resolution, cat_seg_model.py:136-146)")
     a = ap.parse_args()
 
     cfg = get_cfg()
@@ -49,7 +52,7 @@ def main():
     toks = np.load(os.path.join(ROOT, "tests", "golden", "class_tokens.npz"))["ade847"][:a.classes]
     model.sem_seg_head.predictor.set_class_tokens(torch.from_numpy(toks.astype(np.int64)))
     opt = build_optimizer(cfg, model)
-    S = model.clip_resolution[0]
+    S = a.image
     gen = torch.Generator().manual_seed(0)
     batch = [{"image": torch.randint(0, 256, (3, S, S), generator=gen, dtype=torch.uint8),
               "sem_seg": torch.randint(0, a.classes, (S, S), generator=gen)} for _ in range(a.batch)]
@@ -74,9 +77,9 @@ def main():
     out = {"metric": "training images/sec (forward + backward + AdamW step)", "value": a.batch / dt,
            "unit": "images/sec", "ms_per_step": dt * 1e3, "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
            "dtype": "f32", "data": "synthetic images / labels, random-init weights",
-           "loss": float(loss), "grad_norm": float(opt.last_grad_norm[0]),
+           "loss": float(loss.detach()), "grad_norm": float(opt.last_grad_norm[0]),
            "peak_mem_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
-           "config": {"clip": a.clip, "resolution": S, "classes": a.classes, "batch": a.batch, "pooling": [2, 2],
+           "config": {"clip": a.clip, "resolution": S, "clip_resolution": model.clip_resolution[0], "classes": a.classes, "batch": a.batch, "pooling": [2, 2],
                       "clip_finetune": a.finetune, "optimizer": "AdamW (HIP) + full-model clip 0.01"}}
     if a.profile:
         ops.PROFILE = []
