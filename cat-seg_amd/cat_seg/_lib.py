@@ -129,6 +129,7 @@ class GemmExArgs(C.Structure):
         ("C", vp), ("ldc", i64),
         ("alpha", f32), ("beta", i32),
         ("workspace", vp), ("workspace_bytes", i64),
+        ("act_u", vp), ("ld_u", i64), ("act", i32),
     ]
 
 

@@ -31,17 +31,21 @@ def _chk(*ts):
             assert t.dtype == _f32 and t.is_cuda, f"fp32 device tensor expected, got {t.dtype} on {t.device}"
 
 
-def gemm_ex(A, a_sm, a_sk, B, b_sk, b_sn, out, *, M, N, K, ldc=None, alpha=1.0, beta=0, flops_name="gemm_ex"):
-    """out[m][n] = alpha * sum_k A[m*a_sm + k*a_sk] * B[k*b_sk + n*b_sn] + beta * out (catseg_gemm_ex).
+def gemm_ex(A, a_sm, a_sk, B, b_sk, b_sn, out, *, M, N, K, ldc=None, alpha=1.0, beta=0, flops_name="gemm_ex",
+            act_u=None, act=L.ACT_NONE):
+    """out[m][n] = alpha * sum_k A[m*a_sm + k*a_sk] * B[k*b_sk + n*b_sn] + beta * out (catseg_gemm_ex);
+    with act: out = alpha * (A B) * act'(act_u) (the activation backward fused, beta 0).
     A / B / out may be views: their data_ptr() is the element (0, 0)."""
-    _chk(A, B, out)
+    _chk(A, B, out, act_u)
     a = L.GemmExArgs()
     a.A, a.a_sm, a.a_sk = A.data_ptr(), a_sm, a_sk
     a.B, a.b_sk, a.b_sn = B.data_ptr(), b_sk, b_sn
     a.M, a.N, a.K = M, N, K
     a.C, a.ldc = out.data_ptr(), ldc if ldc is not None else out.stride(-2)
     a.alpha, a.beta = alpha, int(beta)
-    ws = _ws(L.load().catseg_gemm_ex_workspace(M, N, K), out.device)
+    if act != L.ACT_NONE:
+        a.act_u, a.ld_u, a.act = act_u.data_ptr(), act_u.stride(-2), int(act)
+    ws = None if act != L.ACT_NONE else _ws(L.load().catseg_gemm_ex_workspace(M, N, K), out.device)
     if ws is not None:
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
     with _rec(flops_name, 2 * M * N * K, 4 * (M * K + K * N + M * N),
@@ -50,14 +54,15 @@ def gemm_ex(A, a_sm, a_sk, B, b_sk, b_sn, out, *, M, N, K, ldc=None, alpha=1.0, 
     return out
 
 
-def mm(A, B, out=None, *, beta=0, alpha=1.0):
-    """out = alpha * A @ B (+ out): A (M, K), B (K, N) strided 2-D views with a unit stride each."""
+def mm(A, B, out=None, *, beta=0, alpha=1.0, act_u=None, act=L.ACT_NONE):
+    """out = alpha * A @ B (+ out): A (M, K), B (K, N) strided 2-D views with a unit stride each;
+    act: out = (A @ B) * act'(act_u), the activation's backward fused into the GEMM's epilogue."""
     M, K = A.shape
     N = B.shape[1]
     if out is None:
         out = torch.empty(M, N, device=A.device, dtype=_f32)
     return gemm_ex(A, A.stride(0), A.stride(1), B, B.stride(0), B.stride(1), out, M=M, N=N, K=K, alpha=alpha,
-                   beta=beta)
+                   beta=beta, act_u=act_u, act=act)
 
 
 def colsum(x, out, *, rows=None, cols=None, ld=None, alpha=1.0, beta=0):

@@ -393,11 +393,10 @@ class SwinBlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         # MLP: out = x1 + fc2(GELU(fc1(LN2(x1))))
         dw2, db2 = _mm_t(dout, a), _colsum(dout)
-        da = TO.mm(dout, w2.detach())
-        du = TO.act_backward(u, da, L.ACT_GELU, out=da)
+        du = TO.mm(dout, w2.detach(), act_u=u, act=L.ACT_GELU)      # GELU backward in the epilogue
         dw1, db1 = _mm_t(du, h2), _colsum(du)
         dh2 = TO.mm(du, w1.detach())
-        del da, du
+        del du
         dx1 = dout.clone()
         dn2w, dn2b = _empty(D, like=X), _empty(D, like=X)
         TO.layernorm_backward(x1, n2w.detach(), dh2, dx1, acc_dx=True, dgamma=dn2w, dbeta=dn2b)
@@ -506,11 +505,10 @@ class ClassLayerFn(torch.autograd.Function):
             dyo = dout
         # MLP: yo = y + MLP.2(ReLU(MLP.0(LN2(y))))
         dw2, db2 = _mm_t(dyo, a), _colsum(dyo)
-        da = TO.mm(dyo, w2.detach())
-        du = TO.act_backward(u, da, L.ACT_RELU, out=da)
+        du = TO.mm(dyo, w2.detach(), act_u=u, act=L.ACT_RELU)
         dw0, db0 = _mm_t(du, h2), _colsum(du)
         dh2 = TO.mm(du, w0.detach())
-        del da, du
+        del du
         dy = dyo.clone()
         dn2w, dn2b = _empty(D, like=Xp), _empty(D, like=Xp)
         TO.layernorm_backward(y, n2w.detach(), dh2, dy, acc_dx=True, dgamma=dn2w, dbeta=dn2b)
@@ -731,14 +729,13 @@ class ClipBlockFn(torch.autograd.Function):
             g[14] = _mm_t(dout, a)
         if ni[15]:
             g[15] = _colsum(dout)
-        da = TO.mm(dout, pw.detach())
-        du = TO.act_backward(u, da, L.ACT_QUICKGELU, out=da)
+        du = TO.mm(dout, pw.detach(), act_u=u, act=L.ACT_QUICKGELU)
         if ni[12]:
             g[12] = _mm_t(du, h2)
         if ni[13]:
             g[13] = _colsum(du)
         dh2 = TO.mm(du, fcw.detach())
-        del da, du
+        del du
         dx1 = dout.clone()
         g[10], g[11] = _ln_bwd(x1, ln2w, dh2, dx1, ni[10] or ni[11])
         if ni[8]:
@@ -756,10 +753,11 @@ class ClipBlockFn(torch.autograd.Function):
                 g[i] = _mm_t(dqkv[:, j * W:(j + 1) * W], h)
         if ni[7]:
             g[7] = _colsum(dqkv)
-        dh = TO.mm(dqkv, torch.cat([qw.detach(), kw.detach(), vw.detach()], 0).contiguous())
-        dx = dx1
-        g[2], g[3] = _ln_bwd(x, ln1w, dh, dx, ni[2] or ni[3])
-        g[0] = dx
+        if ni[0] or ni[2] or ni[3]:    # not for the first block of a frozen embedding: nothing reads dx there
+            dh = TO.mm(dqkv, torch.cat([qw.detach(), kw.detach(), vw.detach()], 0).contiguous())
+            dx = dx1
+            g[2], g[3] = _ln_bwd(x, ln1w, dh, dx, ni[2] or ni[3])
+            g[0] = dx if ni[0] else None
         return tuple(g)
 
 
@@ -803,14 +801,13 @@ class ClipDenseBlockFn(torch.autograd.Function):
             g[14] = _mm_t(dout, a)
         if ni[15]:
             g[15] = _colsum(dout)
-        da = TO.mm(dout, pw.detach())
-        du = TO.act_backward(u, da, L.ACT_QUICKGELU, out=da)
+        du = TO.mm(dout, pw.detach(), act_u=u, act=L.ACT_QUICKGELU)
         if ni[12]:
             g[12] = _mm_t(du, h2)
         if ni[13]:
             g[13] = _colsum(du)
         dh2 = TO.mm(du, fcw.detach())
-        del da, du
+        del du
         dvo = dout.clone()
         g[10], g[11] = _ln_bwd(vo, ln2w, dh2, dvo, ni[10] or ni[11])
         if ni[8]:

@@ -302,13 +302,24 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // the tile for an output-channel count
 struct ConvTile { int bm, bn; };
 ConvTile conv_tile(int cout) { return cout <= 32 ? ConvTile{256, 32} : ConvTile{128, 64}; }
+// weight gradient: M = taps x cin rows; 192-row tiles where they waste fewer rows than 256 (M = 576:
+// 3 full tiles instead of 2 + a quarter-used one; M = 288: 2 tiles at 75 % instead of 56 %)
+ConvTile wgrad_tile(int64_t M, int cout) {
+  if (cout > 32) return ConvTile{128, 64};
+  const int64_t t256 = (M + 255) / 256, t192 = (M + 191) / 192;
+  return t192 * 192 < t256 * 256 ? ConvTile{192, 32} : ConvTile{256, 32};
+}
 
 int wgrad_splits(const CatsegConv2dArgs* a) {
   const int64_t M = (int64_t)a->ksize * a->ksize * a->cin;
-  const ConvTile t = conv_tile(a->cout);
+  const ConvTile t = wgrad_tile(M, a->cout);
   const int64_t tiles = ((M + t.bm - 1) / t.bm) * ((a->cout + t.bn - 1) / t.bn);
   const int64_t K = a->S * a->H * a->W;
-  int64_t s = (1024 + tiles - 1) / tiles;
+  // one round of resident workgroups: LDS per workgroup 2 x 16 x (bm + 16 + bn + 16) floats
+  // (256 x 32: 41 KB -> 3 per CU; 128 x 64: 29 KB -> 5 per CU); floor, so no tail round
+  const int64_t lds = 2LL * CBK * (t.bm + 16 + t.bn + 16) * 4;
+  const int64_t slots = 256 * ((160 * 1024) / lds);
+  int64_t s = slots / tiles;
   const int64_t kmax = K / (CBK * 64);
   if (s > kmax) s = kmax;
   if (s > 512) s = 512;
@@ -479,7 +490,7 @@ extern "C" int catseg_conv2d_wgrad(const CatsegConv2dArgs* a, void* stream) {
   CATSEG_CHECK(a->dw && ((uintptr_t)a->dw % 16) == 0, "conv2d_wgrad: dw missing / unaligned");
   const int64_t M = (int64_t)a->ksize * a->ksize * a->cin;
   CATSEG_CHECK(M < (1LL << 30), "conv2d_wgrad: weight too large");
-  const ConvTile t = conv_tile(a->cout);
+  const ConvTile t = wgrad_tile(M, a->cout);
   const int64_t tm = (M + t.bm - 1) / t.bm, tn = (a->cout + t.bn - 1) / t.bn;
   const int splits = wgrad_splits(a);
   const int64_t need = splits > 1 ? (int64_t)splits * M * a->cout * (int64_t)sizeof(float) : 0;
@@ -491,7 +502,10 @@ extern "C" int catseg_conv2d_wgrad(const CatsegConv2dArgs* a, void* stream) {
   float* part = splits > 1 ? (float*)a->workspace : nullptr;
   dim3 grid((unsigned)(tm * tn), (unsigned)splits);
   const bool vec = a->cin % 4 == 0;
-  if (t.bn == 32) {
+  if (t.bm == 192) {
+    if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<true, 192, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<false, 192, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
+  } else if (t.bn == 32) {
     if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<true, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
     else hipLaunchKernelGGL((conv_wgrad_kernel<false, 256, 32>), grid, dim3(CNT), 0, st, *a, (int)tn, kc, part);
   } else {

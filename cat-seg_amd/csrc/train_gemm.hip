@@ -21,6 +21,32 @@
 namespace {
 
 constexpr int TBM = 128, TBN = 128, TBK = 16, TNT = 256;
+
+// d act / d u in the GEMM epilogue.  GELU' = Phi(u) + u phi(u) with erf by Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7) sharing its exp(-u^2 / 2) with phi: one exp + one rcp per value, where
+// ocml erff + expf cost ~40 VALU (the epilogue runs once per output, outside the MFMA loop).
+DEV float act_grad(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? 1.f : 0.f;
+    case ACT_GELU: {
+      const float z = fabsf(v) * 0.70710678118654752f;
+      const float e = __expf(-z * z);                     // exp(-u^2 / 2)
+      const float t = __frcp_rn(fmaf(0.3275911f, z, 1.f));
+      float p = fmaf(1.061405429f, t, -1.453152027f);
+      p = fmaf(p, t, 1.421413741f);
+      p = fmaf(p, t, -0.284496736f);
+      p = fmaf(p, t, 0.254829592f);
+      const float erf_z = copysignf(1.f - p * t * e, v);
+      return fmaf(0.5f, erf_z, 0.5f) + v * 0.39894228040143268f * e;
+    }
+    case ACT_QUICKGELU: {
+      const float s = __frcp_rn(1.f + __expf(-1.702f * v));
+      return s + 1.702f * v * s * (1.f - s);
+    }
+    default: return 1.f;
+  }
+}
+
 constexpr int LP = TBM + 16;  // LDS row (one k) of a tile: 144 floats, the 4 k rows of a fragment read on
                                // disjoint 16-bank groups
 
@@ -31,7 +57,8 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
                                                       const float* __restrict__ B, int64_t b_sk, int64_t b_sn,
                                                       int64_t M, int64_t N, int64_t K, int64_t k_chunk,
                                                       float* __restrict__ C, int64_t ldc, float alpha, int beta,
-                                                      float* __restrict__ part, int tiles_n) {
+                                                      float* __restrict__ part, int tiles_n,
+                                                      const float* __restrict__ act_u, int64_t ld_u, int act) {
   __shared__ __attribute__((aligned(16))) float As[2][TBK * LP];
   __shared__ __attribute__((aligned(16))) float Bs[2][TBK * LP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -147,6 +174,10 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
       float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       if (!part) {
         v.x *= alpha; v.y *= alpha; v.z *= alpha; v.w *= alpha;
+        if (act) {
+          const float4 u = *reinterpret_cast<const float4*>(act_u + m * ld_u + n);
+          v.x *= act_grad(u.x, act); v.y *= act_grad(u.y, act); v.z *= act_grad(u.z, act); v.w *= act_grad(u.w, act);
+        }
         if (beta) { const float4 o = *p; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
       }
       *p = v;
@@ -206,7 +237,7 @@ int gemm_ex_splits(int64_t M, int64_t N, int64_t K) {
   }
   const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
   if (tiles >= 256) return 1;
-  int64_t s = (1024 + tiles - 1) / tiles;
+  int64_t s = 1024 / tiles;                 // floor: tiles x splits <= 1024 resident slots (no tail round)
   const int64_t kmax = K / (TBK * 8);
   if (s > kmax) s = kmax;
   if (s > 512) s = 512;
@@ -329,7 +360,13 @@ extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
                "gemm_ex: A, B, C must be 16-byte aligned");
   const int64_t tm = (g->M + TBM - 1) / TBM, tn = (g->N + TBN - 1) / TBN;
   CATSEG_CHECK(tm * tn < (1LL << 31), "gemm_ex: too many tiles");
-  const int splits = gemm_ex_splits(g->M, g->N, g->K);
+  const int act = g->act;
+  CATSEG_CHECK(act == ACT_NONE || act == ACT_RELU || act == ACT_GELU || act == ACT_QUICKGELU, "gemm_ex: bad act");
+  if (act) {
+    CATSEG_CHECK(g->act_u && g->ld_u >= g->N && g->ld_u % 4 == 0 && ((uintptr_t)g->act_u % 16) == 0 && !g->beta,
+                 "gemm_ex: the act epilogue needs 16-byte aligned act_u rows (ld_u % 4 == 0) and beta == 0");
+  }
+  const int splits = act ? 1 : gemm_ex_splits(g->M, g->N, g->K);   // the epilogue runs unsplit
   const int64_t ws_need = splits > 1 ? (int64_t)splits * g->M * g->N * (int64_t)sizeof(float) : 0;
   if (splits > 1) CATSEG_CHECK(g->workspace && g->workspace_bytes >= ws_need, "gemm_ex: workspace too small");
   int64_t kc = (g->K + splits - 1) / splits;
@@ -339,7 +376,7 @@ extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
   dim3 grid((unsigned)(tm * tn), (unsigned)splits);
 #define GEX(a_, b_) hipLaunchKernelGGL((gemm_ex_kernel<a_, b_>), grid, dim3(TNT), 0, st, (const float*)g->A, g->a_sm, \
                                        g->a_sk, (const float*)g->B, g->b_sk, g->b_sn, g->M, g->N, g->K, kc, (float*)g->C, \
-                                       g->ldc, g->alpha, g->beta, part, (int)tn)
+                                       g->ldc, g->alpha, g->beta, part, (int)tn, (const float*)g->act_u, g->ld_u, act)
   if (AM && BNC) GEX(true, true);
   else if (AM) GEX(true, false);
   else if (BNC) GEX(false, true);

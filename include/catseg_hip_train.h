@@ -37,6 +37,10 @@ typedef struct {
   void* C; int64_t ldc;
   float alpha; int beta;
   void* workspace; int64_t workspace_bytes;
+  /* optional activation-backward epilogue (act != CATSEG_ACT_NONE; beta must be 0): C[m][n] =
+   * alpha * sum_k A B * act'(act_u[m*ld_u + n]) -- the MLP's dU = (dY . W2) * act'(U) in one pass
+   * (act_u may be C itself: each element is read before it is written by the same lane) */
+  const void* act_u; int64_t ld_u; int act;
 } CatsegGemmExArgs;
 int catseg_gemm_ex(const CatsegGemmExArgs* args, void* stream);
 int64_t catseg_gemm_ex_workspace(int64_t M, int64_t N, int64_t K);

@@ -56,6 +56,22 @@ def test_gemm_ex_layouts(M, N, K):
             close(out, 0.5 * ref + 3.0)
 
 
+@pytest.mark.parametrize("act,fn", [(L.ACT_GELU, F.gelu), (L.ACT_RELU, F.relu),
+                                    (L.ACT_QUICKGELU, lambda t: t * torch.sigmoid(1.702 * t))])
+def test_gemm_ex_activation_backward_epilogue(act, fn):
+    """dU = (dY . W2) * act'(U) in the GEMM's epilogue (the MLP backward's fused form) vs fp64 autograd,
+    in place (the epilogue writes over U) and into a fresh buffer."""
+    M, N, K = 1000, 512, 128
+    dY, W2, U = g(M, K, seed=40), g(K, N, seed=41) / math.sqrt(K), g(M, N, seed=42, scale=2)
+    ur = U.clone().requires_grad_(True)
+    fn(ur).backward(dY @ W2)
+    out = TO.mm(dev(dY), dev(W2), act_u=dev(U), act=act)
+    close(out, ur.grad)
+    Ud = dev(U)
+    TO.mm(dev(dY), dev(W2), out=Ud, act_u=Ud, act=act)
+    close(Ud, ur.grad)
+
+
 @pytest.mark.parametrize("rows,cols,ld", [(5000, 132, 132),      # 16-byte loads, 33 vectors in a 64-wide block
                                           (5000, 130, 130),      # scalar path (cols % 4 != 0)
                                           (3001, 96, 100),       # strided rows, vectors
@@ -306,6 +322,7 @@ def test_linear_attention_backward(T, n_pad):
 
 @pytest.mark.parametrize("cin,cout,k,relu,S", [(96, 64, 3, False, 3), (64, 32, 3, True, 3), (1, 128, 7, False, 3),
                                                (128, 16, 3, True, 3), (20, 8, 3, False, 3),
+                                               (3, 16, 3, False, 3),      # scalar (cin % 4 != 0) 192-row weight tiles
                                                (32, 32, 3, True, 24),     # weight gradient split over 11 pixel ranges
                                                (96, 64, 3, False, 40)])   # 256 x 32 and 128 x 64 tiles, split-K
 def test_conv2d_forward_dgrad_wgrad(cin, cout, k, relu, S):
