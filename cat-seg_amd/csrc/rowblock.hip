@@ -21,6 +21,17 @@ namespace {
 constexpr int KD = 128;    // feature width of the rows
 constexpr int NT = 256;    // 4 waves
 
+// fp32 LDS images (row pitch 132 / 68 floats = 4 mod 32 dwords): rows with bit 3 set hold each
+// 4-float chunk rotated by two (halves swapped), and fragment reads use k-lane q ^ 2 there, so the
+// 16 rows x 2 k of a ds_read_b32 lane group fall on 32 distinct banks (rows r and r + 8 shared a
+// bank pair); bf16 images are untouched
+template <typename T>
+DEV uint4 rot_row(uint4 u, int row) {
+  if constexpr (sizeof(T) == 4) return ((row >> 3) & 1) ? make_uint4(u.z, u.w, u.x, u.y) : u;
+  else return u;
+}
+DEV int rot_q(int q, int r) { return q ^ (((r >> 3) & 1) << 1); }
+
 template <typename T> struct RB;
 template <> struct RB<bf16> { static constexpr int BM = 128, PAD = 8, HC = 128; };
 template <> struct RB<float> { static constexpr int BM = 64, PAD = 4, HC = 64; };
@@ -58,7 +69,7 @@ DEV void load_rows(const T* __restrict__ X, int64_t ldx, int64_t m0, int64_t M, 
 #pragma unroll
       for (int j = 0; j < VN; ++j) e[j] = from_f<T>(v[j] * rstd * gg[j] + bb[j]);
     }
-    st16(&sX[r * ld + c], u);
+    st16(&sX[r * ld + c], rot_row<T>(u, r));
   }
 }
 
@@ -68,7 +79,7 @@ DEV void load_w(const T* __restrict__ W, int64_t ldw, int rows_valid, T* sW, int
   constexpr int VN = Vec16<T>::N, CPR = KD / VN;
   for (int i = threadIdx.x; i < ROWS * CPR; i += NT) {
     const int r = i / CPR, c = (i % CPR) * VN;
-    st16(&sW[r * ld + c], r < rows_valid ? ld16(W + (int64_t)r * ldw + c) : make_uint4(0, 0, 0, 0));
+    st16(&sW[r * ld + c], rot_row<T>(r < rows_valid ? ld16(W + (int64_t)r * ldw + c) : make_uint4(0, 0, 0, 0), r));
   }
 }
 
@@ -90,14 +101,15 @@ DEV void tile_mma(const T* sW, int ldw, const T* sA, int lda, int wn, int wm, f3
       }
     }
   } else {
+    const int qr = rot_q(q, r);
 #pragma unroll 4
     for (int s = 0; s < KD / 4; ++s) {
       float bv[FM];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) bv[j] = sA[(wm + 16 * j + r) * lda + 4 * s + q];
+      for (int j = 0; j < FM; ++j) bv[j] = sA[(wm + 16 * j + r) * lda + 4 * s + qr];
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
-        const float av = sW[(wn + 16 * i + r) * ldw + 4 * s + q];
+        const float av = sW[(wn + 16 * i + r) * ldw + 4 * s + qr];
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = mfma_f32(av, bv[j], acc[i][j]);
       }
@@ -205,6 +217,28 @@ __global__ __launch_bounds__(NT) void rows_gemm_kernel(const T* __restrict__ X, 
 
   const int wave = threadIdx.x >> 6;
   const int64_t m0 = (int64_t)blockIdx.x * BM;
+  if constexpr (sizeof(T) == 4) {
+    // fp32: one workgroup walks every BN-column block of its rows (grid.y = 1), so the rows are
+    // loaded and LayerNorm'd once instead of once per block (6x for the 384-wide q|k|v GEMM); the
+    // accumulator stage reuses the weight slab's LDS, the rows stay put
+    static_assert(BM * SLD * 4 <= WB, "fp32 stage must fit in the weight slab");
+    float* st4 = reinterpret_cast<float*>(smem + AB);
+    load_rows<T, BM>(X, ldx, m0, M, ln_g, ln_b, eps, sA, LD);
+    const int wm = (wave & 1) * WM, wn = (wave >> 1) * WN;
+    for (int n0 = 0; n0 < N; n0 += BN) {
+      load_w<T, BN>(W + (int64_t)n0 * KD, KD, min(BN, N - n0), sW, LD);
+      __syncthreads();
+      f32x4 acc[FN][FM];
+      zero(acc);
+      tile_mma<T, FN, FM>(sW, LD, sA, LD, wn, wm, acc);
+      __syncthreads();
+      stage_acc(st4, SLD, wn, wm, acc);
+      __syncthreads();
+      store_rows<T, BM, BN>(st4, SLD, m0, M, n0, e);
+      __syncthreads();
+    }
+    return;
+  }
   const int n0 = blockIdx.y * BN;
   load_rows<T, BM>(X, ldx, m0, M, ln_g, ln_b, eps, sA, LD);
   load_w<T, BN>(W + (int64_t)n0 * KD, KD, min(BN, N - n0), sW, LD);
@@ -257,7 +291,7 @@ __global__ __launch_bounds__(NT) void rows_mlp_kernel(const T* __restrict__ Y, i
       constexpr int VN = Vec16<T>::N, CPR = HC / VN;
       for (int i = threadIdx.x; i < KD * CPR; i += NT) {
         const int r = i / CPR, c = (i % CPR) * VN;
-        st16(&sW2[r * LDH + c], ld16(W2 + (int64_t)r * hidden + h0 + c));
+        st16(&sW2[r * LDH + c], rot_row<T>(ld16(W2 + (int64_t)r * hidden + h0 + c), r));
       }
     }
     __syncthreads();
@@ -275,6 +309,12 @@ __global__ __launch_bounds__(NT) void rows_mlp_kernel(const T* __restrict__ Y, i
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = apply_act(acc1[i][j][r] + bb[r], act);
+        if constexpr (sizeof(T) == 4) {
+          if ((col >> 3) & 1) {               // rot_row's layout for the fp32 hidden tile
+            const float t0 = v[0], t1 = v[1];
+            v[0] = v[2]; v[1] = v[3]; v[2] = t0; v[3] = t1;
+          }
+        }
         store4<T>(&sH[(wm + 16 * j + col) * LDH + hh], v);
       }
     }
@@ -295,7 +335,7 @@ __global__ __launch_bounds__(NT) void rows_mlp_kernel(const T* __restrict__ Y, i
         }
       }
     } else {
-      const int r = lane & 15, q = lane >> 4;
+      const int r = lane & 15, q = rot_q(lane >> 4, lane & 15);
 #pragma unroll 4
       for (int s = 0; s < HC / 4; ++s) {
         float bv[F2M];
@@ -373,7 +413,7 @@ extern "C" int catseg_rows_gemm(const void* x, int64_t ld_x, int64_t M, const fl
     hipLaunchKernelGGL(rows_gemm_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld_x, M, ln_gamma, ln_beta, eps,
                        (const bf16*)w, (int)N, e);
   } else {
-    dim3 grid((unsigned)((M + RB<float>::BM - 1) / RB<float>::BM), (unsigned)(N / 64));
+    dim3 grid((unsigned)((M + RB<float>::BM - 1) / RB<float>::BM), 1u);   // the kernel walks the N / 64 blocks
     hipLaunchKernelGGL(rows_gemm_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld_x, M, ln_gamma, ln_beta,
                        eps, (const float*)w, (int)N, e);
   }
