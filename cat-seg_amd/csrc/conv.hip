@@ -446,11 +446,20 @@ __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, 
       float v[8];
       load4<T>(src + c, v);
       load4<T>(src + c + 4, v + 4);
+      // weights / GroupNorm terms as 16-byte LDS broadcasts (a ds_read_b32 per element and term was
+      // the fp32 head's limit: 3 LDS reads per multiply-add)
+      const float4 w0 = *reinterpret_cast<const float4*>(wt + c), w1 = *reinterpret_cast<const float4*>(wt + c + 4);
+      const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      if (relu) {
+        const float4 a0 = *reinterpret_cast<const float4*>(ssc + c), a1 = *reinterpret_cast<const float4*>(ssc + c + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(ssh + c), b1 = *reinterpret_cast<const float4*>(ssh + c + 4);
+        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float u = fmaf(v[r], ssc[c + r], ssh[c + r]);
-        if (relu) u = fmaxf(u, 0.f);
-        acc = fmaf(u, wt[c + r], acc);
+        for (int r = 0; r < 8; ++r) acc = fmaf(fmaxf(fmaf(v[r], aa[r], bb[r]), 0.f), ww[r], acc);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc = fmaf(v[r], ww[r], acc);   // no GroupNorm: scale 1, shift 0
       }
     }
   }
@@ -458,6 +467,62 @@ __global__ void head_kernel(const T* x, int64_t B, int Tn, int H, int W, int C, 
   const int t = (int)(s % Tn);
   const int cls = classes ? classes[b * Tn + t] : t;
   out[(b * Tout + cls) * (int64_t)HW + pix] = acc;
+}
+
+// ---------------- head conv C -> 1, fp32 input: C/4 lanes per pixel ---------------------
+// The fp32 (training / config 2) head: lane l of a pixel's LPP = C/4 lanes loads channels 4l..4l+3 of
+// each tap, so one load instruction covers LPP-lane groups of whole 128-byte pixel rows (the
+// one-pixel-per-thread form touched 64 lines per instruction, 16 bytes each); the LPP partial sums
+// meet by xor shuffles.  GroupNorm + ReLU on load as head_kernel.
+template <int LPP>
+__global__ __launch_bounds__(256) void head_vec_kernel(const float* __restrict__ x, int Tn, int H, int W,
+                                                       const float* __restrict__ w, float bias,
+                                                       const float* mean, const float* rstd, const float* gamma,
+                                                       const float* beta, int cpg, const int32_t* classes, int Tout,
+                                                       float* __restrict__ out) {
+  constexpr int C = 4 * LPP, PPB = 256 / LPP;              // pixels per block pass
+  const int64_t s = blockIdx.y;
+  const int l = threadIdx.x % LPP, pl = threadIdx.x / LPP;
+  const int c = 4 * l;
+  float4 wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = *reinterpret_cast<const float4*>(w + t * C + c);
+  float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool gn = mean != nullptr;
+  if (gn) {
+    const int groups = C / cpg;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = rstd[s * groups + (c + r) / cpg] * gamma[c + r];
+      sc[r] = a;
+      sh[r] = beta[c + r] - mean[s * groups + (c + r) / cpg] * a;
+    }
+  }
+  const int HW = H * W;
+  const int64_t b = s / Tn;
+  const int t0 = (int)(s % Tn);
+  const int cls = classes ? classes[b * Tn + t0] : t0;
+  float* o = out + (b * Tout + cls) * (int64_t)HW;
+  const float* xs = x + s * (int64_t)HW * C + c;
+  for (int pix = blockIdx.x * PPB + pl; pix < HW; pix += gridDim.x * PPB) {
+    const int y = pix / W, xx = pix - y * W;
+    float acc = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yy = y + tap / 3 - 1, x2 = xx + tap % 3 - 1;
+      if (yy < 0 || yy >= H || x2 < 0 || x2 >= W) continue;
+      const float4 v = *reinterpret_cast<const float4*>(xs + ((int64_t)yy * W + x2) * C);
+      const float vv[4] = {v.x, v.y, v.z, v.w}, ww[4] = {wv[tap].x, wv[tap].y, wv[tap].z, wv[tap].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float u = gn ? fmaxf(fmaf(vv[r], sc[r], sh[r]), 0.f) : vv[r];
+        acc = fmaf(u, ww[r], acc);
+      }
+    }
+#pragma unroll
+    for (int off = LPP / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (l == 0) o[pix] = acc + bias;
+  }
 }
 
 // ---------------- head conv, banded (bf16 input) ---------------------------------------
@@ -815,7 +880,12 @@ extern "C" int catseg_conv3x3_head_gn(const void* x, int64_t B, int T, int H, in
   if (dtype == CATSEG_BF16)
     hipLaunchKernelGGL(head_kernel<bf16>, grid, dim3(256), sh, (hipStream_t)stream, (const bf16*)x, B, T, H, W,
                        C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
-  else
+  else if (C == 32 && ((uintptr_t)x % 16) == 0) {
+    // fp32, 32 channels (the decoder's last width): 8 lanes per pixel, 32 pixels per block pass
+    const unsigned gx = (unsigned)std::min<int64_t>(((int64_t)H * W + 31) / 32, 64);
+    hipLaunchKernelGGL(head_vec_kernel<8>, dim3(gx, (unsigned)(B * T)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)x, T, H, W, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
+  } else
     hipLaunchKernelGGL(head_kernel<float>, grid, dim3(256), sh, (hipStream_t)stream, (const float*)x, B, T, H,
                        W, C, weight, bias, mean, rstd, gamma, beta, cpg, classes, T_out, out);
   return catseg_launch_status("conv3x3_head");
