@@ -549,6 +549,18 @@ def rows_gemm(x, w, out, *, ln=None, eps=1e-5, bias=None, add=None, addmap=None,
     """out = epi(LN?(x) . w^T) over 128-wide rows (catseg_rows_gemm)."""
     M = M if M is not None else x.shape[0]
     N = w.shape[0]
+    if x.dtype == torch.float32 and out.dtype == torch.float32:
+        # fp32 (config 2): catseg_layernorm + catseg_gemm (same epilogue order: bias, add, act, res, res2)
+        # run at ~76 TF/s on these K = 128 GEMMs against the fused row kernel's ~55 (64-row workgroups,
+        # 4 MFMAs per k-step per wave)
+        a = x
+        if ln is not None:
+            a = torch.empty(M, w.shape[1], device=x.device, dtype=torch.float32)
+            layernorm(x, ln[0], ln[1], a, rows=M, eps=eps)
+        ncols = add_ncols if add_ncols is not None else (add.shape[-1] if add is not None else None)
+        gemm(a, w, out, M=M, bias=bias, add=add, addmap=addmap, add_ncols=ncols, act=act, res=res, res2=res2,
+             store=store)
+        return out
     e = _rows_epi(out, bias, add, addmap, add_ncols, act, res, res2, store)
     g, b = (ln if ln is not None else (None, None))
     with _rec("rows_gemm", 2 * M * N * w.shape[1], x.element_size() * M * (w.shape[1] + N)):
@@ -573,6 +585,16 @@ def rows_mlp(y, w1, b1, w2, out, *, ln, b2=None, act=L.ACT_GELU, res=None, res2=
     reference's row count when it computes padded rows (the class MLP, model.py:413)."""
     M = M if M is not None else y.shape[0]
     hidden = w1.shape[0]
+    if y.dtype == torch.float32 and out.dtype == torch.float32:
+        # fp32 (config 2): LayerNorm + two GEMM launches beat the fused row kernel, whose one workgroup
+        # per 64 rows re-stages the 2 x 256 KB of fp32 weights per hidden chunk at one wave per SIMD
+        # (1.67 ms per launch at 345,600 rows); the hidden tensor round-trips HBM instead (M x 512 fp32)
+        h = torch.empty(M, w1.shape[1], device=y.device, dtype=torch.float32)
+        layernorm(y, ln[0], ln[1], h, rows=M, eps=eps)
+        u = torch.empty(M, hidden, device=y.device, dtype=torch.float32)
+        gemm(h, w1, u, M=M, bias=b1, act=act)
+        gemm(u, w2, out, M=M, bias=b2, res=res, res2=res2)
+        return out
     e = _rows_epi(out, b2, None, None, None, L.ACT_NONE, res, res2, None)
     ref = 4 * ref_rows * hidden * w1.shape[1] if ref_rows else None
     with _rec("rows_mlp", 4 * M * hidden * w1.shape[1], y.element_size() * M * 2 * w1.shape[1], ref_flops=ref):
