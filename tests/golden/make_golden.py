@@ -330,7 +330,97 @@ def class_data():
     return toks
 
 
+def train_case(name, arch, T, seed=3, n_sub=256):
+    """The training step (cat_seg_model.py:57-75 requires_grad for CLIP_FINETUNE 'attention', :136-146 +
+    :178-203 forward and one-hot BCE loss, cat_seg_predictor.py:150-160,190-224 text embeddings with
+    grad) through the reference's own modules in float64, backward, and the gradient of every trainable
+    parameter.  A gradient is stored as an evenly strided sample of at most n_sub entries of the
+    flattened tensor (the build's parameters have the reference's shapes) plus max |g|, with the
+    relative error of the same reference graph run in float32 (the gate's scale); inputs are the GPU
+    test's (tests/test_gpu_train_head.py::test_catseg_train_step_matches_reference_gradients)."""
+    sd = synthesize_state_dict(arch, seed=0)
+    gen = torch.Generator().manual_seed(seed)
+    toks = torch.zeros(T, arch.context_length, dtype=torch.long)
+    toks[:, 0] = 1
+    toks[:, 1:4] = torch.randint(2, 400, (T, 3), generator=gen)
+    toks[:, 4] = 511                                   # EOT = the argmax id
+    ims = [torch.randint(0, 256, (3, 384, 384), generator=gen).float() for _ in range(2)]
+    sems = [torch.randint(0, T, (384, 384), generator=gen) for _ in range(2)]
+    sems[0][:20] = 255
+    targets = torch.stack(sems)
+    grads, losses = {}, {}
+    # model_vpt.py:156-162's LayerNorm casts its input to float32 (an fp16 guard): the identity for the
+    # float32 run; for the float64 run it is bypassed so the graph stays float64 end to end
+    ln_forward = model_vpt.LayerNorm.forward
+    for dt in (torch.float64, torch.float32):
+        model_vpt.LayerNorm.forward = nn.LayerNorm.forward if dt == torch.float64 else ln_forward
+        clip, agg, up1, up2 = build_reference(arch, sd, pad_len=arch.pad_len)
+        clip, agg, up1, up2 = clip.to(dt), agg.to(dt), up1.to(dt), up2.to(dt)
+        for n, p in clip.named_parameters():         # cat_seg_model.py:57-75, CLIP_FINETUNE "attention"
+            rg = False
+            if "transformer" in n:
+                rg = ("q_proj" in n or "v_proj" in n) if "attn" in n else ("position" in n)
+            p.requires_grad_(rg)
+        for m in (clip, agg, up1, up2):
+            m.train()
+        text = clip.encode_text(toks)
+        text = (text / text.norm(dim=-1, keepdim=True)).unsqueeze(1)
+        layers = []
+        hs = [clip.visual.transformer.resblocks[l].register_forward_hook(lambda m, i, o: layers.append(o))
+              for l in arch.hook_layers]
+        clip_images = glue_preprocess(arch, ims).to(dt)
+        feats = clip.encode_image(clip_images, dense=True)
+        for h in hs:
+            h.remove()
+        g = arch.grid
+        B = feats.shape[0]
+        res3 = feats[:, 1:, :].reshape(B, g, g, -1).permute(0, 3, 1, 2)
+        res4 = up1(layers[0][1:].permute(1, 2, 0).reshape(B, -1, g, g))
+        res5 = up2(layers[1][1:].permute(1, 2, 0).reshape(B, -1, g, g))
+        out = agg(res3, text.repeat(B, 1, 1, 1), [res3, res4, res5])
+        out = F.interpolate(out, size=targets.shape[-2:], mode="bilinear", align_corners=False)
+        mask = targets != 255
+        out = out.permute(0, 2, 3, 1)
+        tg = torch.zeros(out.shape, dtype=dt)
+        tg[mask] = F.one_hot(targets[mask], num_classes=out.shape[-1]).to(dt)
+        loss = F.binary_cross_entropy_with_logits(out, tg)
+        loss.backward()
+        losses[dt] = loss.item()
+        named = {CLIP_P + n: p for n, p in clip.named_parameters()}
+        named.update({AGG_P + n: p for n, p in agg.named_parameters()})
+        named.update({"upsample1." + n: p for n, p in up1.named_parameters()})
+        named.update({"upsample2." + n: p for n, p in up2.named_parameters()})
+        grads[dt] = {k: (None if p.grad is None else p.grad.detach().double().reshape(-1))
+                     for k, p in named.items() if p.requires_grad}
+    model_vpt.LayerNorm.forward = ln_forward
+    kw = dict(tokens=toks, targets=targets.to(torch.int16), loss64=losses[torch.float64],
+              loss32=losses[torch.float32], image0=ims[0].to(torch.uint8), image1=ims[1].to(torch.uint8))
+    names, none = [], []
+    for k, g64 in grads[torch.float64].items():
+        if g64 is None:
+            none.append(k)
+            continue
+        n = g64.numel()
+        step = max(1, n // n_sub)
+        idx = torch.arange(0, n, step)[:n_sub]
+        g32 = grads[torch.float32][k]
+        mx = g64.abs().max().item()
+        names.append(k)
+        kw["g_" + k] = g64[idx].numpy()
+        kw["i_" + k] = idx.numpy().astype(np.int64)
+        kw["m_" + k] = np.array([mx, (g32 - g64).abs().max().item() / (mx + 1e-300)])
+    kw["names"] = np.array(names)
+    kw["none"] = np.array(none)
+    save(name, **kw)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "train":
+        torch.set_num_threads(8)
+        # the training step at TINY geometry, the training config's POOLING [2,2], T=9 < pad_len (padding
+        # tokens train), CLIP q / v of both encoders
+        train_case("train_tiny_pool2", TINY.replace(pooling_size=(2, 2)), 9)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "classes":
         class_data()
         return

@@ -288,3 +288,49 @@ def test_catseg_train_step_backward_and_optimizer():
     sd_new = {k: v.detach().cpu() for k, v in model.named_parameters()}
     ref = O.catseg_forward(arch, sd_new, [{"image": ims[0]}], O.text_embeds(arch, sd_new, toks))[0]["sem_seg"]
     assert (out.cpu() - ref).abs().max().item() < 1e-3
+
+
+def test_catseg_train_step_matches_reference_gradients():
+    """The whole training step pinned to the REFERENCE's own modules, not the oracle: the loss and every
+    trainable parameter's gradient against tests/golden/train_tiny_pool2.npz, which
+    tests/golden/make_golden.py ("train") produced by running the reference's model_vpt.CLIP and
+    Aggregator (requires_grad per cat_seg_model.py:57-75, loss per :189-203, text per
+    cat_seg_predictor.py:190-224) in float64 on the same inputs.  Per parameter, an evenly strided
+    sample of the flattened gradient and its max magnitude are compared, gate max(1e-4, 8 x the same
+    reference graph's own float32 error); the Swin k biases (zero in exact arithmetic) against the k
+    weights' scale."""
+    import numpy as np
+    from conftest import ROOT
+    g = np.load(os.path.join(ROOT, "tests", "golden", "train_tiny_pool2.npz"))
+    cfg = tiny_cfg(**{"MODEL.SEM_SEG_HEAD.POOLING_SIZES": "[2,2]"})
+    model = build_model(cfg).cuda()
+    model.sem_seg_head.predictor.set_class_tokens(torch.from_numpy(g["tokens"]))
+    ims = [torch.from_numpy(g["image0"]).float(), torch.from_numpy(g["image1"]).float()]
+    tg = torch.from_numpy(g["targets"]).long()
+    model.train()
+    loss = model([{"image": ims[i], "sem_seg": tg[i]} for i in range(2)])["loss_sem_seg"]
+    loss.backward()
+    l64 = float(g["loss64"])
+    assert abs(loss.item() - l64) <= 1e-5 * abs(l64), (loss.item(), l64)
+    named = dict(model.named_parameters())
+    names = [str(k) for k in g["names"]]
+    assert {k for k, p in named.items() if p.requires_grad} == set(names) | {str(k) for k in g["none"]}
+    rows = []
+    try:
+        for k in names:
+            mx, e32 = (float(v) for v in g["m_" + k])
+            got = named[k].grad.detach().double().cpu().reshape(-1)
+            if ".swin_block." in k and k.endswith("attn.k.bias"):
+                scale = float(g["m_" + k[:-len("bias")] + "weight"][0])
+                assert got.abs().max().item() <= 1e-5 * scale, k
+                continue
+            if mx == 0.0:                 # the dense block's dead q / k projections
+                assert got.abs().max().item() == 0.0, k
+                continue
+            idx = torch.from_numpy(g["i_" + k])
+            err = max((got[idx] - torch.from_numpy(g["g_" + k])).abs().max().item() / mx,
+                      abs(got.abs().max().item() - mx) / mx)
+            rows.append((err, e32, k))
+            assert err <= max(TOL, 8 * e32), f"{k}: {err:.3e} (reference fp32 {e32:.3e})"
+    finally:
+        _write_report("reference_modules_train_step", sorted(rows, reverse=True))
