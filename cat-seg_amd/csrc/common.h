@@ -31,6 +31,14 @@ DEV unsigned f2bf2(float lo, float hi) {
   return __builtin_bit_cast(unsigned, h);
 }
 
+// ReLU of a packed bf16 pair: a signed 16-bit max with 0 (v_pk_max_i16) maps every negative value
+// and -0 to +0 and keeps the rest, the same bits as rounding the ReLU'd floats
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+DEV unsigned relu_bf16x2(unsigned v) {
+  const s16x2_t r = __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, v), (s16x2_t){0, 0});
+  return __builtin_bit_cast(unsigned, r);
+}
+
 template <typename T> DEV float to_f(T v);
 template <> DEV float to_f<float>(float v) { return v; }
 template <> DEV float to_f<bf16>(bf16 v) { return bf2f(v); }

@@ -3,11 +3,11 @@
 // DoubleConv inside Up, :540-555).
 //
 // A workgroup walks a band of consecutive 128-pixel chunks of one NHWC slice.  The
-// input rows live in a 6-row LDS ring (row y in slot (y + 1) % 6, one zero halo column
-// each side, rows outside the image zero) and each row is loaded from HBM ONCE per band:
-// while the MFMAs of chunk c run, the rows chunk c+1 adds are already in flight in
-// registers (global -> VGPR), and are written into the slots chunk c+1 no longer needs
-// after the chunk's barrier.  Channels [0, c1) come from the per-slice tensor
+// input rows live in an NR-row LDS ring (row y in slot (y + 1) % NR, one zero halo column
+// each side, rows outside the image zero) and each pixel is loaded from HBM ONCE per band:
+// while the MFMAs of chunk c run, the CH pixels chunk c+1 adds (the linear pixel stream
+// one row + one pixel ahead of it) are already in flight in registers (global -> VGPR), and
+// are written into the slots chunk c+1 no longer needs after the chunk's MFMAs.  Channels [0, c1) come from the per-slice tensor
 // (GroupNorm+ReLU'd on the way in when the conv consumes relu(GN(x))), [c1, C) from the
 // per-image guidance tensor (the concat + repeat of Up.forward, model.py:551-554, never
 // materialised).  An optional fp32 per-image addend (the guidance half of the conv,
@@ -83,7 +83,6 @@ template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, 
 __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   constexpr int CPX = C / 8;
   constexpr int PS = RingGeom<C>::PS;
-  constexpr int MAXPF = (NPOS * CPX + NT - 1) / NT;     // prefetch chunks per thread
   constexpr int PXW = CH / WPX, FM = PXW / 16;          // pixels per wave, their 16-px tiles
   constexpr int COW = COUT / WCO, FN = COW / 16;        // output channels per wave
   constexpr int KC = C / 32;                            // full MFMA k-steps per tap
@@ -148,6 +147,41 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[i][r] = p.bias ? p.bias[ch0 + 16 * i + 4 * q + r] : 0.f;
 
+  // ---- the halo columns (ring columns 0 and W + 1) of every slot are zeroed once: the pixel
+  // loads below never write them ----
+  for (int i = tid; i < NR * 2 * CPX; i += NT) {
+    const int slot = i / (2 * CPX), side = (i / CPX) & 1;
+    st16(&ring[slot * RPE + (side ? W + 1 : 0) * PS + (i % CPX) * 8], make_uint4(0, 0, 0, 0));
+  }
+  // Ring loads are PIXEL-granular: the image is one linear pixel stream P = y * W + x (row -1 and
+  // rows >= H read as zeros), and the ring holds pixels [.., lp) of it.  Chunk c needs pixels up to
+  // the bottom-right neighbour of its last pixel, p0 + CH + W (exclusive end p0 + CH + W + 1), so
+  // each chunk adds exactly CH pixels = CH * CPX 16-byte items, MAXPF per thread, with no idle
+  // passes for partial rows and no halo writes.  (When a chunk ends at a row end the last of
+  // those pixels is column 0 of the row after the bottom halo row; its slot cannot alias a row in
+  // use -- that case spans one row less than the worst case the NR of each variant is sized
+  // for, ring_plan_ok() checks every launch.)
+  constexpr int MAXPF = CH * CPX / NT;
+  static_assert(MAXPF * NT == CH * CPX, "a chunk's pixels fill whole passes of the workgroup");
+  // ring-write item order: with 4 chunks per pixel (C = 32, 96-byte pixel stride) the 8 lanes of a
+  // ds_write_b128 group would write pixels p, p+1 and hit 8 banks twice; swapping bits 2 and 3 of
+  // the item index gives them pixels p, p+2 (distinct 16-byte bank slots), a bijection on every
+  // aligned block of 16 items
+  auto perm = [](int i) { return CPX == 4 ? (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1) : i; };
+  // per-thread prefetch items, decoded once: (pixel offset << 8) | 16-byte channel chunk
+  int pf_code[MAXPF];
+#pragma unroll
+  for (int k = 0; k < MAXPF; ++k) {
+    const int i = perm(tid + k * NT);
+    pf_code[k] = ((i / CPX) << 8) | (i % CPX);
+  }
+  // ring element offset of pixel P (P >= -W), channel chunk ch
+  auto ring_at = [&](int P, int ch) {
+    const unsigned y1 = (unsigned)(P + W) / (unsigned)W;           // y + 1 >= 0
+    const int x = P + W - (int)y1 * W;
+    return (int)(y1 % NR) * RPE + (x + 1) * PS + ch * 8;
+  };
+
   for (int64_t unit = blockIdx.x / nsplit; unit < nunits; unit += ustride) {
   const int64_t s = unit / p.bands;
   const int band = (int)(unit % p.bands);
@@ -165,58 +199,68 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
   }
   const bf16* s1base = p.s1 + s * p.s1_ss;
   const bf16* s2base = p.s2 ? p.s2 + (s / p.s2_div) * p.s2_ss : nullptr;
+  const bool gn = p.gmean != nullptr;
 
-  // load 16-byte chunk (row y, ring column xc, chunk ch) from HBM (zero outside the image)
-  auto gload = [&](int y, int xc, int ch) -> uint4 {
-    const int x = xc - 1, ci = ch * 8;
-    if (y < 0 || y >= H || x < 0 || x >= W) return make_uint4(0, 0, 0, 0);
-    const int pix = y * W + x;
-    return ci < p.c1 ? ld16(s1base + (int64_t)pix * p.c1 + ci) : ld16(s2base + (int64_t)pix * p.c2 + (ci - p.c1));
-  };
-  auto lput = [&](int y, int xc, int ch, uint4 u) {
+  // 16-byte item (pixel P, channel chunk ch) from HBM: the address of pixel P when it is in the
+  // image, else of pixel 0 (the caller zero-selects)
+  auto gsrc = [&](int P, int ch) -> const bf16* {
     const int ci = ch * 8;
-    if (p.gmean && ci < p.c1 && y >= 0 && y < H && xc >= 1 && xc <= W) {
-      bf16* e = reinterpret_cast<bf16*>(&u);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) e[k] = f2bf(fmaxf(fmaf(bf2f(e[k]), gsc[ci + k], gsh[ci + k]), 0.f));
-    }
-    st16(&ring[((y + 1) % NR) * RPE + xc * PS + ch * 8], u);
+    return ci < p.c1 ? s1base + (int64_t)__umul24(P, p.c1) + ci : s2base + (int64_t)__umul24(P, p.c2) + (ci - p.c1);
   };
-  const int row_items = WP * CPX;
-  // ring-write item order: with 4 chunks per pixel (C = 32, 96-byte pixel stride) the 8 lanes of a
-  // ds_write_b128 group would write pixels p, p+1 and hit 8 banks twice; swapping bits 2 and 3 of
-  // the item index gives them pixels p, p+2 (distinct 16-byte bank slots), a bijection on every
-  // aligned block of 16 items (validity is tested on the permuted index)
-  auto perm = [](int i) { return CPX == 4 ? (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1) : i; };
+  // write an item into the ring, GroupNorm+ReLU'd when it is an in-image s1 channel chunk
+  // (ReLU on the rounded bf16 pair as a signed 16-bit max with 0: the same bits as rounding the
+  // ReLU'd float)
+  auto lput = [&](int P, int ch, bool in_image, uint4 u) {
+    const int ci = ch * 8;
+    if (gn && in_image && ci < p.c1) {
+      const float4 a0 = *reinterpret_cast<const float4*>(gsc + ci), a1 = *reinterpret_cast<const float4*>(gsc + ci + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(gsh + ci), b1 = *reinterpret_cast<const float4*>(gsh + ci + 4);
+      const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float sh[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = __uint_as_float(w[e] << 16), hi = __uint_as_float(w[e] & 0xffff0000u);
+        const unsigned r = f2bf2(fmaf(lo, sc[2 * e], sh[2 * e]), fmaf(hi, sc[2 * e + 1], sh[2 * e + 1]));
+        w[e] = relu_bf16x2(r);
+      }
+      u = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    st16(&ring[ring_at(P, ch)], in_image ? u : make_uint4(0, 0, 0, 0));
+  };
 
-  // ---- prime: rows needed by the first chunk ----
-  __syncthreads();   // gsc/gsh
-  int loaded_to;     // rows [.., loaded_to] are in the ring
+  // ---- prime: from the top halo row of the first chunk to its bottom-right neighbour ----
+  __syncthreads();   // gsc/gsh (and, first unit, the halo columns)
+  int lp;            // pixels [.., lp) are in the ring
   {
     const int p0 = c_begin * CH;
-    const int ya = p0 / W - 1, yb = (p0 + CH - 1) / W + 1;
-    const int total = (yb - ya + 1) * row_items;
+    const int pa = (p0 / W - 1) * W, pe = p0 + CH + W + 1;
+    const int total = (pe - pa) * CPX;
     for (int i0 = 0; i0 < total; i0 += NT * 8) {
       uint4 u[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = perm(i0 + j * NT + tid);
-        u[j] = i < total ? gload(ya + i / row_items, (i % row_items) / CPX, i % CPX) : make_uint4(0, 0, 0, 0);
+        const int P = pa + i / CPX;
+        u[j] = i < total && P >= 0 && P < HW ? ld16(gsrc(P, i % CPX)) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = perm(i0 + j * NT + tid);
-        if (i < total) lput(ya + i / row_items, (i % row_items) / CPX, i % CPX, u[j]);
+        const int P = pa + i / CPX;
+        if (i < total) lput(P, i % CPX, P >= 0 && P < HW, u[j]);
       }
     }
-    loaded_to = yb;
+    lp = pe;
   }
-  // per-thread prefetch items, decoded once: (row offset << 16) | (ring column << 4) | chunk
-  int pf_code[MAXPF];
+  // the ring row / column of each of this wave's pixel tiles (pixel p0 + wpx * PXW + 16 j + r16),
+  // advanced by CH pixels per chunk: slot of the row above (y - 1 + 1) % NR and column x
+  int srow[FM], pcol[FM];
 #pragma unroll
-  for (int k = 0; k < MAXPF; ++k) {
-    const int i = perm(tid + k * NT);
-    pf_code[k] = ((i / row_items) << 16) | (((i % row_items) / CPX) << 4) | (i % CPX);
+  for (int j = 0; j < FM; ++j) {
+    const int pp = c_begin * CH + wpx * PXW + 16 * j + r16;
+    srow[j] = (pp / W) % NR;
+    pcol[j] = pp % W;
   }
   __syncthreads();
 
@@ -236,35 +280,23 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         for (int j = 0; j < FM; ++j)
           ad[i][j] = *reinterpret_cast<const float4*>(addb + (16 * j + r16) * COUT * nsplit + 16 * i + 4 * q);
     }
-    // ---- prefetch the rows the next chunk adds: unconditional loads from clamped addresses
-    // (zero-selected at the ring write), so the code is straight-line and every wait is an
-    // exact vmcnt count ----
+    if constexpr (ADD) __builtin_amdgcn_sched_barrier(0);     // (the addend loads issue before the prefetch loads)
+    // ---- prefetch the CH pixels the next chunk adds, [lp, lp + CH): unconditional loads from
+    // clamped addresses (zero-selected at the ring write), so the code is straight-line and every
+    // wait is an exact vmcnt count ----
     uint4 pf[MAXPF];
-    int nnew = 0;
-    if (c + 1 < c_end) {
-      const int yb_next = min((p0 + 2 * CH - 1) / W + 1, H);
-      nnew = yb_next - loaded_to;
-    }
-    unsigned pf_ok = 0;
 #pragma unroll
     for (int k = 0; k < MAXPF; ++k) {
-      const int dy = pf_code[k] >> 16, xc = (pf_code[k] >> 4) & 0xfff, ch = pf_code[k] & 15;
-      const int y = loaded_to + 1 + dy, x = xc - 1, ci = ch * 8;
-      const bool ok = dy < nnew && y < H && x >= 0 && x < W;
-      const int pix = ok ? y * W + x : 0;
-      const bf16* src = ci < p.c1 ? s1base + pix * p.c1 + ci : s2base + pix * p.c2 + (ci - p.c1);
-      pf[k] = ld16(src);
-      pf_ok |= (ok ? 1u : 0u) << k;
+      const int P = lp + (pf_code[k] >> 8);
+      pf[k] = ld16(gsrc(P < HW ? P : 0, pf_code[k] & 255));
     }
+    // with an addend, its loads and the prefetch loads stay ahead of the MFMAs (left to itself the
+    // scheduler sinks them below the tap loop, and the epilogue then waits out their full latency;
+    // without one, sinking the prefetch measured faster: 48-wide 64-channel conv 312 -> 272 us)
+    if constexpr (ADD) __builtin_amdgcn_sched_barrier(0);
 
     // ---- MFMAs: 9 taps x (KC + tail) k-steps over the ring ----
-    int prow[FM], pcol[FM];
-#pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int pp = p0 + wpx * PXW + 16 * j + r16;
-      prow[j] = pp / W;
-      pcol[j] = pp - prow[j] * W;            // ring column of the left tap (x - 1 + 1)
-    }
+    auto wrap = [](int r) { return r >= NR ? r - NR : r; };
     f32x4 acc[FN][FM];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
       for (int sy = 0; sy < 2; ++sy)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) rbu[sy][j] = ((prow[j] + pa + sy) % NR) * RPE + (pcol[j] + pb) * PS;
+        for (int j = 0; j < FM; ++j) rbu[sy][j] = wrap(srow[j] + pa + sy) * RPE + (pcol[j] + pb) * PS;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
@@ -296,7 +328,7 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) rb[dy][j] = ((prow[j] + dy) % NR) * RPE + pcol[j] * PS;
+      for (int j = 0; j < FM; ++j) rb[dy][j] = wrap(srow[j] + dy) * RPE + pcol[j] * PS;
 #pragma unroll
     for (int dy = 0; dy < (UP ? 0 : 3); ++dy) {
 #pragma unroll
@@ -343,7 +375,9 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
           adv[0] = av.x; adv[1] = av.y; adv[2] = av.z; adv[3] = av.w;
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += adv[r] + bv[i][r];
+        // (acc + addend) + bias: no addend-only subexpression the scheduler could hoist above the
+        // tap loop (it would wait there for the addend loads)
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = (ADD ? acc[i][j][r] + adv[r] : acc[i][j][r]) + bv[i][r];
         if (p.act != ACT_NONE)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] = apply_act(acc[i][j][r], p.act);
@@ -397,25 +431,54 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         }
     }
 
-    // ---- rotate the ring: prefetched rows into the slots the next chunk no longer needs ----
+    // ---- the prefetched pixels into the ring (slots the next chunk's rows own), and the pixel
+    // tiles one chunk on ----
     if constexpr (!OB) __syncthreads();
+    if (c + 1 < c_end) {
 #pragma unroll
-    for (int k = 0; k < MAXPF; ++k)
-      if ((pf_code[k] >> 16) < nnew)
-        lput(loaded_to + 1 + (pf_code[k] >> 16), (pf_code[k] >> 4) & 0xfff, pf_code[k] & 15,
-             (pf_ok >> k) & 1 ? pf[k] : make_uint4(0, 0, 0, 0));
-    loaded_to += nnew > 0 ? nnew : 0;
+      for (int k = 0; k < MAXPF; ++k) {
+        const int P = lp + (pf_code[k] >> 8);
+        lput(P, pf_code[k] & 255, P < HW, pf[k]);
+      }
+    }
+    lp += CH;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      pcol[j] += CH % W;
+      srow[j] += CH / W;
+      if (pcol[j] >= W) { pcol[j] -= W; srow[j] += 1; }
+      srow[j] = wrap(srow[j]);
+    }
     __syncthreads();
   }
   }   // units
 }
 
+// The pixel-granular ring plan on an H x W map with CH-pixel chunks and NR slots: for every chunk
+// (any chunk may start a band), the band prime's rows fit the ring, and the rows chunk c's prefetch
+// writes never share a slot with a row a chunk still reads (OB: chunk c's own rows, which other
+// waves may still be reading; two-barrier: chunk c+1's).
+static bool ring_plan_ok(int H, int W, int CH, int NR, bool OB) {
+  const int nchunks = H * W / CH;
+  for (int c = 0; c < nchunks; ++c) {
+    const int p0 = c * CH;
+    const int first = p0 / W - 1;                         // top halo row of chunk c
+    const int prime_last = (p0 + CH + W) / W;             // row of the prime's last pixel
+    if (prime_last - first + 1 > NR) return false;
+    if (c + 1 == nchunks) break;
+    const int wr_last = (p0 + 2 * CH + W) / W;            // row of the prefetch's last pixel
+    const int oldest = OB ? first : (p0 + CH) / W - 1;    // oldest row still read
+    if (wr_last - oldest + 1 > NR) return false;
+  }
+  return true;
+}
+
 template <int C>
 size_t ring_lds(int W, int NR) { return (size_t)NR * RingGeom<C>::pitch(W) * 2 + 2 * C * 4; }
 
-// NPOS bounds the ring positions one chunk adds (W + 2 columns per new row): CH = 128 adds
-// <= 3 rows (156) for 48 <= W <= 50 and <= 2 rows (198) for W <= 96; CH = 64 at W = 48
-// adds <= 2 rows (104).
+// NPOS: the ring positions one chunk added under round 4's row-granular loads (W + 2 columns per
+// new row: 156 / 198 for CH = 128 at W = 48 / 96, 104 for CH = 64 at W = 48); with pixel-granular
+// loads it no longer sizes anything and only names the width class of a variant (launch_ring).
 template <int C, int COUT, int WPX, int WCO, int NPOS, int CH, int OCC, int NR, bool ADD, bool UP = false, int WFIX = 0,
           bool OB = false>
 int launch_ring_t(const RingP& p0, hipStream_t st) {
@@ -447,6 +510,10 @@ int launch_ring_t(const RingP& p0, hipStream_t st) {
   }
   if (nsplit < 1 || nsplit > 4 || (COUT / WCO) % 16 != 0 || ((int64_t)p.H * p.W) % CH != 0 || (WFIX > 0 && p.W != WFIX)) {
     catseg_set_error("conv ring: bad channel split %d or H*W %% %d != 0", nsplit, CH);
+    return -1;
+  }
+  if (!ring_plan_ok(p.H, p.W, CH, NR, OB)) {
+    catseg_set_error("conv ring: %d ring slots do not cover %d-pixel chunks on a %d-wide map", NR, CH, p.W);
     return -1;
   }
   int64_t grid = p.S * bands * nsplit;

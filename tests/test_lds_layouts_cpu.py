@@ -23,9 +23,9 @@ def test_ring_conv_layouts_conflict_free():
         reads = M.extra(M.ring_fragment_reads(C, W, H, CH, NR, up, psb, M.ring_pad(psb)), "read")
         assert reads == 0.0, (C, W, reads)
         if C in (32, 64, 128):                               # the hot-path ring widths
-            writes = M.extra(M.ring_writes(C, W, NR, psb, M.ring_pad(psb), M.ring_perm(C)), "write")
+            writes = M.extra(M.ring_pixel_writes(C, W, H, CH, NR, psb, M.ring_pad(psb), M.ring_perm(C)), "write")
             assert writes < 0.02, (C, W, writes)
-    # what the pad and the write order fix (round 3)
+    # what the pad and the write order fix (round 3's row-granular writes)
     assert M.extra(M.ring_fragment_reads(128, 24, 24, 64, 6, True, 288, 0), "read") > 0.3
     assert M.extra(M.ring_writes(32, 96, 5, 96, 0, lambda i: i), "write") > 0.8
 

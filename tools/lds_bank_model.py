@@ -95,6 +95,24 @@ def ring_writes(C: int, W: int, NR: int, psb: int, rpad: int, perm: Callable[[in
             yield out
 
 
+def ring_pixel_writes(C: int, W: int, H: int, CH: int, NR: int, psb: int, rpad: int, perm: Callable[[int], int]):
+    """The pixel-granular ring writes (round 5): each chunk adds the CH pixels [lp, lp + CH) of the
+    linear pixel stream, item i -> (pixel lp + i // cpx, chunk i % cpx) after the item permutation,
+    the halo columns never written."""
+    cpx = C // 8
+    pitch = (W + 2) * psb + rpad
+    for c in range(H * W // CH - 1):
+        lp = c * CH + CH + W + 1
+        for i0 in range(0, CH * cpx, 64):
+            out = []
+            for lane in range(64):
+                i = perm(i0 + lane)
+                P = lp + i // cpx
+                y, x = P // W, P % W
+                out.append(((y + 1) % NR) * pitch + (x + 1) * psb + (i % cpx) * 16)
+            yield out
+
+
 def ring_perm(C: int) -> Callable[[int], int]:
     """conv_ring.hip's write-item order: bits 2 and 3 swapped at 4 chunks per pixel."""
     if C // 8 == 4:
@@ -153,7 +171,8 @@ def main():
         psb = ring_psb(C)
         for label, rpad, perm in (("round 3", 0, lambda i: i), ("shipped", ring_pad(psb), ring_perm(C))):
             r = extra(ring_fragment_reads(C, W, H, CH, NR, up, psb, rpad), "read")
-            w = extra(ring_writes(C, W, NR, psb, rpad, perm), "write")
+            w = extra(ring_writes(C, W, NR, psb, rpad, perm) if label == "round 3" else
+                      ring_pixel_writes(C, W, H, CH, NR, psb, rpad, perm), "write")
             print(f"ring C={C:3d} W={W:2d} {label}: fragment reads +{r:.3f}, ring writes +{w:.3f}")
     for label, ldh, sw in (("round 3 (+16 pad)", 528, False), ("shipped (+16 pad, swizzle)", 528, True)):
         print(f"MLP hidden tile {label}: GEMM1 stores +{extra(mlp_hidden_writes(ldh, sw), 'write'):.3f}, "
