@@ -705,10 +705,18 @@ __global__ __launch_bounds__(256) void head_tap_kernel(const bf16* __restrict__ 
         const int tile = wave * HT_TPS + j, i = 2 * k + tile / HT_TPR, yy = y0 - 1 + i;
         const int x0 = (tile % HT_TPR) * 16;
         const bool in = i < nin && yy >= 0 && yy < H;       // wave-uniform
-        const bf16* e = reinterpret_cast<const bf16*>(&cur[j]);
+        // GroupNorm affine on bf16 pairs, rounded to f16 pairs (v_cvt_pk_f16_f32), ReLU in f16
+        // (v_pk_max_f16: the same values as rounding the ReLU'd floats)
+        const unsigned wv[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
         h8 a;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] = (_Float16)(in ? fmaxf(fmaf(bf2f(e[q]), sc[q], sh[q]), 0.f) : 0.f);
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 y = {fmaf(__uint_as_float(wv[q] << 16), sc[2 * q], sh[2 * q]),
+                           fmaf(__uint_as_float(wv[q] & 0xffff0000u), sc[2 * q + 1], sh[2 * q + 1])};
+          const h2 hh = __builtin_elementwise_max(__builtin_convertvector(y, h2), (h2){(_Float16)0.f, (_Float16)0.f});
+          a[2 * q] = in ? hh[0] : (_Float16)0.f;
+          a[2 * q + 1] = in ? hh[1] : (_Float16)0.f;
+        }
         const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, wb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         // D[pixel x0 + 4g + r][tap r16]
         if (r16 < 9) *reinterpret_cast<f32x4*>(&ring[(i % HT_NR)][r16][4 + x0 + 4 * g]) = d;
