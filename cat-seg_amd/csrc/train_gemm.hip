@@ -21,6 +21,13 @@
 namespace {
 
 constexpr int TBM = 128, TBN = 128, TBK = 16, TNT = 256;
+// catseg_gemm_ex's product form (gemm_ex_kernel TERMS): -1 = automatic (6 for the tall reductions,
+// K >= 8192 -- the weight gradients, K = the row count -- else 0), 0 = exact-f32 MFMA, 6 / 3 = split-bf16
+// MFMA.  tools/micro_gemm_ex.py at the training shapes (4 x 171 x 576 rows of 128 / 512 channels):
+// dW 484 -> 395 us (128 -> 512), 454 -> 402 (512 -> 128), 134 -> 123 (128 -> 128), 350 -> 310 (128 -> 384)
+// at the f32 form's error (rel 7-10e-7 vs 6-8e-7); dX (K = 128 / 512) 446-509 vs 487-496 us, so it keeps
+// the f32 form; TERMS 3 runs dW in 290-294 us at ~5e-6 (not used).
+int g_gemm_ex_terms = -1;
 
 // d act / d u in the GEMM epilogue.  GELU' = Phi(u) + u phi(u) with erf by Abramowitz & Stegun 7.1.26
 // (|error| <= 1.5e-7) sharing its exp(-u^2 / 2) with phi: one exp + one rcp per value, where
@@ -50,17 +57,50 @@ DEV float act_grad(float v, int act) {
 constexpr int LP = TBM + 16;  // LDS row (one k) of a tile: 144 floats, the 4 k rows of a fragment read on
                                // disjoint 16-bank groups
 
+// fp32 x -> the bf16 pieces x = p0 + p1 (+ p2) + (error <= 2^-24 |x| with three pieces): each piece is
+// the round-to-nearest-even bf16 of what the previous ones left (v_cvt_pk_bf16_f32 per pair), and
+// every residual x - p is exact in fp32.  Products of pieces are exact in the MFMA's fp32 accumulator.
+template <int NP>
+DEV void split_bf16(const float (&x)[8], s16x8 (&piece)[NP]) {
+  float r[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = x[e];
+#pragma unroll
+  for (int pi = 0; pi < NP; ++pi) {
+    unsigned w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      w[e] = f2bf2(r[2 * e], r[2 * e + 1]);
+      if (pi + 1 < NP) {
+        r[2 * e] -= __uint_as_float(w[e] << 16);
+        r[2 * e + 1] -= __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+    uint4 u = make_uint4(w[0], w[1], w[2], w[3]);
+    piece[pi] = *reinterpret_cast<s16x8*>(&u);
+  }
+}
+
 // AM: A is m-contiguous (a_sm == 1) else k-contiguous (a_sk == 1).
 // BN: B is n-contiguous (b_sn == 1) else k-contiguous (b_sk == 1).
-template <bool AM, bool BNC>
+// KS: k depth of one LDS slab (16, or 32 for the bf16 MFMA).
+// TERMS: 0 = exact-f32 MFMA (v_mfma_f32_16x16x4_f32); 6 = the fp32 products from bf16 pieces
+//   (3 per operand, split at fragment load): a b = sum over the 6 piece pairs (i, j) with i + j <= 2
+//   of a_i b_j, smallest first, each one v_mfma_f32_16x16x32_bf16 (16 issue cycles for 32 k vs 8 x 32
+//   for the f32 form); the dropped pairs are below 2^-24 |a b|, so the result is an fp32 GEMM's up
+//   to accumulation order; 3 = pieces 0-1 only (a0 b0 + a0 b1 + a1 b0, ~2^-17 relative).
+template <bool AM, bool BNC, int KS = TBK, int TERMS = 0>
 __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ A, int64_t a_sm, int64_t a_sk,
                                                       const float* __restrict__ B, int64_t b_sk, int64_t b_sn,
                                                       int64_t M, int64_t N, int64_t K, int64_t k_chunk,
                                                       float* __restrict__ C, int64_t ldc, float alpha, int beta,
                                                       float* __restrict__ part, int tiles_n,
                                                       const float* __restrict__ act_u, int64_t ld_u, int act) {
-  __shared__ __attribute__((aligned(16))) float As[2][TBK * LP];
-  __shared__ __attribute__((aligned(16))) float Bs[2][TBK * LP];
+  static_assert(TERMS == 0 ? KS % 4 == 0 : KS % 32 == 0, "k slab");
+  constexpr int CH = TBM * KS / 4 / TNT;        // 16-byte chunks per operand per thread per slab
+  constexpr int CPK = KS / 4;                    // chunks per k-contiguous row of a slab
+  __shared__ __attribute__((aligned(16))) float As[2][KS * LP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][KS * LP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntiles = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, ntiles);
@@ -69,18 +109,18 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
   const int64_t ke = kb + k_chunk < K ? kb + k_chunk : K;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
 
-  // staging: 2 x 16-byte chunks per operand per thread per k-slab
-  float4 ra[2], rb[2];
+  // staging: CH x 16-byte chunks per operand per thread per k-slab
+  float4 ra[CH], rb[CH];
   auto gload = [&](int64_t k0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int c = tid + i * TNT;
       if constexpr (AM) {                      // chunk = 4 consecutive m at one k
         const int k = c >> 5, m4 = (c & 31) * 4;
         const int64_t gm = m0 + m4, gk = k0 + k;
         ra[i] = (gm < M && gk < ke) ? *reinterpret_cast<const float4*>(A + gm + gk * a_sk) : make_float4(0, 0, 0, 0);
       } else {                                 // chunk = 4 consecutive k at one m
-        const int m = c >> 2, k4 = (c & 3) * 4;
+        const int m = c / CPK, k4 = (c % CPK) * 4;
         const int64_t gm = m0 + m, gk = k0 + k4;
         ra[i] = (gm < M && gk < ke) ? *reinterpret_cast<const float4*>(A + gm * a_sm + gk) : make_float4(0, 0, 0, 0);
       }
@@ -89,7 +129,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
         const int64_t gn = n0 + n4, gk = k0 + k;
         rb[i] = (gn < N && gk < ke) ? *reinterpret_cast<const float4*>(B + gn + gk * b_sk) : make_float4(0, 0, 0, 0);
       } else {
-        const int n = c >> 2, k4 = (c & 3) * 4;
+        const int n = c / CPK, k4 = (c % CPK) * 4;
         const int64_t gn = n0 + n, gk = k0 + k4;
         rb[i] = (gn < N && gk < ke) ? *reinterpret_cast<const float4*>(B + gn * b_sn + gk) : make_float4(0, 0, 0, 0);
       }
@@ -102,13 +142,13 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
   auto swz = [](int k) { return ((k >> 2) & 3) << 3; };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int c = tid + i * TNT;
       if constexpr (AM) {
         const int k = c >> 5;
         *reinterpret_cast<float4*>(&As[buf][k * LP + (((c & 31) * 4) ^ swz(k))]) = ra[i];
       } else {
-        const int m = c >> 2, k4 = (c & 3) * 4, mm = m ^ swz(k4);
+        const int m = c / CPK, k4 = (c % CPK) * 4, mm = m ^ swz(k4);
         As[buf][(k4 + 0) * LP + mm] = ra[i].x; As[buf][(k4 + 1) * LP + mm] = ra[i].y;
         As[buf][(k4 + 2) * LP + mm] = ra[i].z; As[buf][(k4 + 3) * LP + mm] = ra[i].w;
       }
@@ -116,7 +156,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
         const int k = c >> 5;
         *reinterpret_cast<float4*>(&Bs[buf][k * LP + (((c & 31) * 4) ^ swz(k))]) = rb[i];
       } else {
-        const int n = c >> 2, k4 = (c & 3) * 4, nn = n ^ swz(k4);
+        const int n = c / CPK, k4 = (c % CPK) * 4, nn = n ^ swz(k4);
         Bs[buf][(k4 + 0) * LP + nn] = rb[i].x; Bs[buf][(k4 + 1) * LP + nn] = rb[i].y;
         Bs[buf][(k4 + 2) * LP + nn] = rb[i].z; Bs[buf][(k4 + 3) * LP + nn] = rb[i].w;
       }
@@ -131,7 +171,7 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)((ke - kb + TBK - 1) / TBK);
+  const int nk = (int)((ke - kb + KS - 1) / KS);
   const int r = lane & 15, g = lane >> 4;
   if (nk > 0) {
     gload(kb);
@@ -140,20 +180,63 @@ __global__ __launch_bounds__(TNT) void gemm_ex_kernel(const float* __restrict__ 
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kb + (int64_t)(kt + 1) * TBK);
+    if (kt + 1 < nk) gload(kb + (int64_t)(kt + 1) * KS);
     const float* as = As[buf];
     const float* bs = Bs[buf];
+    if constexpr (TERMS == 0) {
 #pragma unroll
-    for (int kk = 0; kk < TBK; kk += 4) {
-      float av[4], bv[4];
+      for (int kk = 0; kk < KS; kk += 4) {
+        float av[4], bv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) av[j] = as[(kk + g) * LP + ((wm + 16 * j + r) ^ swz(kk))];
+        for (int j = 0; j < 4; ++j) av[j] = as[(kk + g) * LP + ((wm + 16 * j + r) ^ swz(kk))];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = bs[(kk + g) * LP + ((wn + 16 * i + r) ^ swz(kk))];
+        for (int i = 0; i < 4; ++i) bv[i] = bs[(kk + g) * LP + ((wn + 16 * i + r) ^ swz(kk))];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(bv[i], av[j], acc[i][j]);
+      }
+    } else {
+      constexpr int NP = TERMS == 6 ? 3 : 2;
+#pragma unroll
+      for (int kk = 0; kk < KS; kk += 32) {
+        // lane (r, g) holds k = kk + 8g .. +7 of its row (the 16x16x32 bf16 operand layout); the
+        // swizzle of k is ((2g + e / 4) & 3) << 3 for element e
+        const int k0 = kk + 8 * g;
+        const int s0 = swz(k0), s1 = swz(k0 + 4);
+        // the A pieces of all four m-fragments stay live; each n-fragment's pieces are made just
+        // before its 4 x TERMS MFMAs (register pressure: two waves per SIMD)
+        s16x8 ap[4][NP];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = wm + 16 * j + r;
+          float x[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = as[(k0 + e) * LP + (m ^ (e < 4 ? s0 : s1))];
+          split_bf16<NP>(x, ap[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = wn + 16 * i + r;
+          float x[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = bs[(k0 + e) * LP + (n ^ (e < 4 ? s0 : s1))];
+          s16x8 bp[NP];
+          split_bf16<NP>(x, bp);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f32x4 c = acc[i][j];
+            if constexpr (NP == 3) {
+              c = mfma_bf16(bp[2], ap[j][0], c);
+              c = mfma_bf16(bp[1], ap[j][1], c);
+              c = mfma_bf16(bp[0], ap[j][2], c);
+            }
+            c = mfma_bf16(bp[1], ap[j][0], c);
+            c = mfma_bf16(bp[0], ap[j][1], c);
+            acc[i][j] = mfma_bf16(bp[0], ap[j][0], c);
+          }
+        }
+      }
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
@@ -335,6 +418,7 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 }  // namespace
 
 CATSEG_KNOB(g_gemm_ex_splits, "gemm_ex_splits");
+CATSEG_KNOB(g_gemm_ex_terms, "gemm_ex_terms");
 
 extern "C" int64_t catseg_gemm_ex_workspace(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
@@ -370,17 +454,25 @@ extern "C" int catseg_gemm_ex(const CatsegGemmExArgs* g, void* stream) {
   const int64_t ws_need = splits > 1 ? (int64_t)splits * g->M * g->N * (int64_t)sizeof(float) : 0;
   if (splits > 1) CATSEG_CHECK(g->workspace && g->workspace_bytes >= ws_need, "gemm_ex: workspace too small");
   int64_t kc = (g->K + splits - 1) / splits;
-  kc = (kc + TBK - 1) / TBK * TBK;
+  const int terms = g_gemm_ex_terms >= 0 ? g_gemm_ex_terms : (g->K >= 8192 ? 6 : 0);
+  const int ks = terms ? 32 : TBK;
+  kc = (kc + ks - 1) / ks * ks;
   hipStream_t st = (hipStream_t)stream;
   float* part = splits > 1 ? (float*)g->workspace : nullptr;
   dim3 grid((unsigned)(tm * tn), (unsigned)splits);
-#define GEX(a_, b_) hipLaunchKernelGGL((gemm_ex_kernel<a_, b_>), grid, dim3(TNT), 0, st, (const float*)g->A, g->a_sm, \
-                                       g->a_sk, (const float*)g->B, g->b_sk, g->b_sn, g->M, g->N, g->K, kc, (float*)g->C, \
-                                       g->ldc, g->alpha, g->beta, part, (int)tn, (const float*)g->act_u, g->ld_u, act)
-  if (AM && BNC) GEX(true, true);
-  else if (AM) GEX(true, false);
-  else if (BNC) GEX(false, true);
-  else GEX(false, false);
+#define GEX(a_, b_, ks_, t_) hipLaunchKernelGGL((gemm_ex_kernel<a_, b_, ks_, t_>), grid, dim3(TNT), 0, st, (const float*)g->A, \
+                                       g->a_sm, g->a_sk, (const float*)g->B, g->b_sk, g->b_sn, g->M, g->N, g->K, kc, \
+                                       (float*)g->C, g->ldc, g->alpha, g->beta, part, (int)tn, (const float*)g->act_u, \
+                                       g->ld_u, act)
+#define GEX4(ks_, t_)                      \
+  if (AM && BNC) GEX(true, true, ks_, t_); \
+  else if (AM) GEX(true, false, ks_, t_);  \
+  else if (BNC) GEX(false, true, ks_, t_); \
+  else GEX(false, false, ks_, t_);
+  if (terms == 6) { GEX4(32, 6) }
+  else if (terms == 3) { GEX4(32, 3) }
+  else { GEX4(TBK, 0) }
+#undef GEX4
 #undef GEX
   if (splits > 1) {
     const int64_t n = g->M * (g->N / 4);

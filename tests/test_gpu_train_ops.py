@@ -56,6 +56,31 @@ def test_gemm_ex_layouts(M, N, K):
             close(out, 0.5 * ref + 3.0)
 
 
+@pytest.mark.parametrize("terms,tol", [(0, 2e-6), (6, 2e-6), (3, 3e-5)])
+@pytest.mark.parametrize("M,N,K", [(300, 132, 68), (128, 384, 20000), (7, 12, 100)])
+def test_gemm_ex_split_bf16_forms(terms, tol, M, N, K):
+    """The product forms of catseg_gemm_ex (tuning knob gemm_ex_terms): exact-f32 MFMA, the six-pair
+    split-bf16 form (automatic for K >= 8192: fp32-class error) and the three-pair form (~2^-17),
+    in every operand layout, against fp64 at fp32-scale gates."""
+    A = g(M, K, seed=11)
+    B = g(K, N, seed=12)
+    ref = A @ B
+    L.tune("gemm_ex_terms", terms)
+    try:
+        for a_t in (False, True):
+            for b_t in (False, True):
+                if (a_t and M % 4) or (not a_t and K % 4) or (b_t and K % 4) or (not b_t and N % 4):
+                    continue
+                a_sm, a_sk = (1, M) if a_t else (K, 1)
+                b_sk, b_sn = (1, K) if b_t else (N, 1)
+                out = torch.empty(M, N, device=DEV)
+                TO.gemm_ex(dev(A.t() if a_t else A), a_sm, a_sk, dev(B.t() if b_t else B), b_sk, b_sn, out,
+                           M=M, N=N, K=K)
+                close(out, ref, tol)
+    finally:
+        L.tune("gemm_ex_terms", -1)
+
+
 @pytest.mark.parametrize("act,fn", [(L.ACT_GELU, F.gelu), (L.ACT_RELU, F.relu),
                                     (L.ACT_QUICKGELU, lambda t: t * torch.sigmoid(1.702 * t))])
 def test_gemm_ex_activation_backward_epilogue(act, fn):

@@ -1,7 +1,8 @@
 """Time the training GEMMs (catseg_gemm_ex, fp32 MFMA) and the forward fp32 GEMM on the shapes of the
 training step (B/16@384: R = 4 x 171 x 576 rows of 128 channels) and check them against torch.
 
-usage: python tools/micro_gemm_ex.py
+usage: python tools/micro_gemm_ex.py [terms, default "0"]   (tuning knob gemm_ex_terms: 0 = exact-f32
+MFMA, 6 / 3 = split-bf16 MFMA; each gemm_ex line is repeated per value)
 """
 import os
 import sys
@@ -12,10 +13,12 @@ import torch  # noqa: E402
 
 from cat_seg import ops  # noqa: E402
 from cat_seg import train_ops as TO  # noqa: E402
+from cat_seg import _lib as L  # noqa: E402
 
 dev = "cuda"
 torch.manual_seed(0)
 R = int(os.environ.get("MGX_R", 4 * 171 * 576))
+TERMS = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0").split(",")]
 
 
 def timeit(fn, reps=10):
@@ -50,13 +53,16 @@ for Kin, Nout in ((128, 512), (512, 128), (128, 128), (128, 384)):
     Y = torch.empty(R, Nout, device=dev)
     t = timeit(lambda: ops.gemm(X, W, Y))
     report(f"fwd  X.W^T   ({Kin}->{Nout})", R, Nout, Kin, t, rel(Y, X.double() @ W.double().t()))
-    # dX = dY . W (gemm_ex: A k-contiguous, B n-contiguous)
     dX = torch.empty(R, Kin, device=dev)
-    t = timeit(lambda: TO.mm(dY, W, out=dX))
-    report(f"dX   dY.W    ({Kin}->{Nout})", R, Kin, Nout, t, rel(dX, dY.double() @ W.double()))
-    # dW = dY^T . X (A m-contiguous, K = R: split-K)
     dW = torch.empty(Nout, Kin, device=dev)
-    t = timeit(lambda: TO.mm(dY.t(), X, out=dW))
-    report(f"dW   dY^T.X  ({Kin}->{Nout})", Nout, Kin, R, t, rel(dW, dY.double().t() @ X.double()))
+    for tv in TERMS:
+        L.tune("gemm_ex_terms", tv)
+        # dX = dY . W (gemm_ex: A k-contiguous, B n-contiguous)
+        t = timeit(lambda: TO.mm(dY, W, out=dX))
+        report(f"dX   dY.W    ({Kin}->{Nout}) t{tv}", R, Kin, Nout, t, rel(dX, dY.double() @ W.double()))
+        # dW = dY^T . X (A m-contiguous, K = R: split-K)
+        t = timeit(lambda: TO.mm(dY.t(), X, out=dW))
+        report(f"dW   dY^T.X  ({Kin}->{Nout}) t{tv}", Nout, Kin, R, t, rel(dW, dY.double().t() @ X.double()))
+    L.tune("gemm_ex_terms", 0)
     del X, W, dY, Y, dX, dW
     torch.cuda.empty_cache()
