@@ -643,6 +643,115 @@ __global__ __launch_bounds__(256) void conv_partial_vec_kernel(const bf16* __res
   }
 }
 
+// The same per-image partial conv on the MFMA (g_partial_mfma, default): an im2col GEMM over
+// k = tap * CIN + ci, D^T = W . X^T per 16-pixel tile (a lane ends with 4 consecutive output channels
+// of one pixel: float4 stores).  The guidance is bf16 (exact as an MFMA operand); the fp32 weights
+// enter as two bf16 pieces w = w_hi + w_lo (w_lo = bf16(w - w_hi)), two MFMAs per k-step, so the
+// weights keep ~16 mantissa bits (relative 2^-17) instead of bf16's 8.  CIN = 32: one tap per 32-deep
+// k-step (9 steps); CIN = 16: taps 2s (lanes q < 2) and 2s + 1 (q >= 2) share step s (5 steps, tap 9
+// zero).  Each wave walks 16-pixel tiles with its 9 / 5 guidance fragment loads issued before the
+// MFMAs; the weight pieces are staged once per workgroup in LDS ([co][k] rows padded by 16 bytes).
+template <int CIN, bool PAR = false>
+__global__ __launch_bounds__(256) void conv_partial_mfma_kernel(const bf16* __restrict__ g, int64_t B, int H, int W,
+                                                               const float* __restrict__ w, int cout, float* out,
+                                                               const float* __restrict__ tap_bias, int64_t ntiles) {
+  static_assert(CIN == 16 || CIN == 32, "CIN");
+  constexpr int KS = CIN == 32 ? 9 : 5;            // 32-deep k-steps
+  constexpr int LDR = KS * 32 + 8;                 // LDS row (one output channel), elements
+  extern __shared__ __attribute__((aligned(16))) char smem_p[];
+  bf16* whi = reinterpret_cast<bf16*>(smem_p);     // [cout][LDR]
+  bf16* wlo = whi + cout * LDR;
+  float* stb = reinterpret_cast<float*>(wlo + cout * LDR);   // PAR: [9][cout]
+  // k = tap * CIN + ci is also the order of a weight row w[co][tap][ci]: 16-byte loads, k >= 9 CIN zero
+  for (int i = threadIdx.x; i < cout * KS * 8; i += blockDim.x) {
+    const int co = i / (KS * 8), k4 = (i % (KS * 8)) * 4;
+    const float4 v = k4 < 9 * CIN ? *reinterpret_cast<const float4*>(w + (int64_t)co * 9 * CIN + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const unsigned h0 = f2bf2(v.x, v.y), h1 = f2bf2(v.z, v.w);
+    const unsigned l0 = f2bf2(v.x - __uint_as_float(h0 << 16), v.y - __uint_as_float(h0 & 0xffff0000u));
+    const unsigned l1 = f2bf2(v.z - __uint_as_float(h1 << 16), v.w - __uint_as_float(h1 & 0xffff0000u));
+    *reinterpret_cast<uint2*>(whi + co * LDR + k4) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(wlo + co * LDR + k4) = make_uint2(l0, l1);
+  }
+  if constexpr (PAR)
+    for (int i = threadIdx.x; i < 9 * cout; i += blockDim.x) stb[i] = tap_bias ? tap_bias[i] : 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int HW = H * W;
+  const int nt = cout / 16;
+  // guidance fragments of a tile: lane (pixel r16, q) holds k = 32 s + 8 q .. +7; the next tile's are
+  // requested before this tile's MFMAs
+  auto gather = [&](int64_t tile, s16x8 (&xf)[KS]) {
+    const int64_t pixg = tile * 16 + r16;
+    const int64_t b = pixg / HW;
+    const int pix = (int)(pixg - b * HW), y = pix / W, x = pix - y * W;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int tap = CIN == 32 ? st : 2 * st + (q >> 1), ci = CIN == 32 ? 8 * q : 8 * (q & 1);
+      const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+      const bool ok = tile < ntiles && tap < 9 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const uint4 u = ok ? ld16(g + ((b * H + yy) * W + xx) * CIN + ci) : make_uint4(0, 0, 0, 0);
+      xf[st] = __builtin_bit_cast(s16x8, u);
+    }
+  };
+  const int64_t tstride = (int64_t)gridDim.x * 4;
+  s16x8 xn[KS];
+  gather((int64_t)blockIdx.x * 4 + wave, xn);
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += tstride) {
+    const int64_t pixg = tile * 16 + r16;          // this lane's pixel (the second operand's column)
+    const int64_t b = pixg / HW;
+    const int pix = (int)(pixg - b * HW), y = pix / W, x = pix - y * W;
+    s16x8 xf[KS];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) xf[st] = xn[st];
+    gather(tile + tstride, xn);
+    for (int n = 0; n < nt; ++n) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bf16* rh = whi + (n * 16 + r16) * LDR + 8 * q;
+      const bf16* rl = wlo + (n * 16 + r16) * LDR + 8 * q;
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        acc = mfma_bf16(*reinterpret_cast<const s16x8*>(rl + st * 32), xf[st], acc);
+        acc = mfma_bf16(*reinterpret_cast<const s16x8*>(rh + st * 32), xf[st], acc);
+      }
+      // lane: output channels 16 n + 4 q .. +3 of pixel r16
+      const int co = n * 16 + 4 * q;
+      if constexpr (PAR) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+          if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+          acc += *reinterpret_cast<const f32x4*>(stb + tap * cout + co);
+        }
+        const int64_t o = ((b * (H / 2) + y / 2) * (W / 2) + x / 2) * 4 * cout + ((y & 1) * 2 + (x & 1)) * cout + co;
+        *reinterpret_cast<f32x4*>(out + o) = acc;
+      } else {
+        *reinterpret_cast<f32x4*>(out + pixg * cout + co) = acc;
+      }
+    }
+  }
+}
+
+int g_partial_mfma = 1;   // 1 = conv_partial_mfma_kernel, 0 = the VALU kernel (conv_partial_vec_kernel)
+
+template <int CIN, bool PAR>
+void launch_partial_mfma(const bf16* g, int64_t B, int H, int W, const float* w, int cout, float* out,
+                         const float* tap_bias, hipStream_t st) {
+  constexpr int KS = CIN == 32 ? 9 : 5, LDR = KS * 32 + 8;
+  const size_t sh = (size_t)2 * cout * LDR * 2 + (PAR ? (size_t)9 * cout * 4 : 0);
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_partial_mfma_kernel<CIN, PAR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    configured = true;
+  }
+  const int64_t ntiles = B * H * W / 16;
+  // two workgroups per CU (the weight pieces are staged once per workgroup, 16-byte loads)
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, 2LL * catseg_device_cus()));
+  hipLaunchKernelGGL((conv_partial_mfma_kernel<CIN, PAR>), dim3(grid), dim3(256), sh, st, g, B, H, W, w, cout, out,
+                     tap_bias, ntiles);
+}
+
 }  // namespace
 
 // Variant table of the ring kernel: 0 = not applicable, else an id; *tile = pixels per
@@ -741,7 +850,10 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
     }
     const size_t shv = (size_t)9 * cin * (cout + 4) * 4;   // padded LDS rows (conv_partial_vec_kernel)
     CATSEG_CHECK(shv <= 128 * 1024, "conv3x3_partial: weights <= 128 KB");
-    if (cin == 16)
+    if (g_partial_mfma && cout % 16 == 0 && (H * W) % 16 == 0 && cout <= 128) {
+      if (cin == 16) launch_partial_mfma<16, false>((const bf16*)g, B, H, W, weight, cout, out, nullptr, (hipStream_t)stream);
+      else launch_partial_mfma<32, false>((const bf16*)g, B, H, W, weight, cout, out, nullptr, (hipStream_t)stream);
+    } else if (cin == 16)
       hipLaunchKernelGGL(conv_partial_vec_kernel<16>, dim3(vgrid), dim3(256), shv, (hipStream_t)stream, (const bf16*)g,
                          B, H, W, weight, cout, out);
     else
@@ -757,6 +869,7 @@ extern "C" int catseg_conv3x3_partial(const void* g, int64_t B, int H, int W, in
 }
 
 CATSEG_KNOB(g_ring_persist, "ring_persist");
+CATSEG_KNOB(g_partial_mfma, "partial_mfma");
 CATSEG_KNOB(g_ring_onebar, "ring_onebar");
 
 // ---- ConvTranspose2d(k=2, s=2) folded into the following conv3x3 (Up, model.py:546-555) ----
@@ -785,7 +898,10 @@ extern "C" int catseg_upconv_addend(const void* g, int64_t B, int H2, int W2, in
   }
   const int64_t total = B * H2 * W2 * (cout / 4);
   const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 512);
-  if (cin == 16)
+  if (g_partial_mfma && cout % 16 == 0 && (H2 * W2) % 16 == 0 && cout <= 128) {
+    if (cin == 16) launch_partial_mfma<16, true>((const bf16*)g, B, H2, W2, weight, cout, out, tap_bias, (hipStream_t)stream);
+    else launch_partial_mfma<32, true>((const bf16*)g, B, H2, W2, weight, cout, out, tap_bias, (hipStream_t)stream);
+  } else if (cin == 16)
     hipLaunchKernelGGL((conv_partial_vec_kernel<16, true>), dim3(grid), dim3(256), sh, (hipStream_t)stream,
                        (const bf16*)g, B, H2, W2, weight, cout, out, tap_bias);
   else
