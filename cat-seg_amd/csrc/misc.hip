@@ -253,6 +253,10 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
   __shared__ float sin[1024];          // (H + 6) x (W + 6) zero-padded slice (host-checked)
   __shared__ float sbias[HID];
   __shared__ float sw[HID * 49];       // stage_w: the [128][49] weights, one coalesced sweep
+  // each wave's 16-pixel x 128-channel bf16 output tile, transposed through LDS so the stores are
+  // whole 256-byte pixel rows (16 lanes x 16 B) instead of 8-byte pieces 16 rows apart
+  constexpr int OLD = HID + 8;
+  __shared__ __attribute__((aligned(16))) bf16 sout[4][16 * OLD];
   const int PW = W + 6, PH = H + 6;
   const int HW = H * W;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -339,15 +343,19 @@ __global__ __launch_bounds__(256) void corr_embed_mfma_kernel(const float* corr,
           acc[i] = mfma_bf16(wlo[i][ks], bhi[ks], acc[i]);
         }
       }
-      if (valid) {
-        bf16* o = out + (s * HW + pix) * HID;
+      bf16* so = sout[wave];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int c = 16 * i + 4 * q;
-          const float4 bb = *reinterpret_cast<const float4*>(sbias + c);
-          *reinterpret_cast<uint2*>(o + c) = make_uint2(f2bf2(acc[i][0] + bb.x, acc[i][1] + bb.y),
-                                                        f2bf2(acc[i][2] + bb.z, acc[i][3] + bb.w));
-        }
+      for (int i = 0; i < 8; ++i) {
+        const int c = 16 * i + 4 * q;
+        const float4 bb = *reinterpret_cast<const float4*>(sbias + c);
+        *reinterpret_cast<uint2*>(so + r16 * OLD + c) = make_uint2(f2bf2(acc[i][0] + bb.x, acc[i][1] + bb.y),
+                                                                  f2bf2(acc[i][2] + bb.z, acc[i][3] + bb.w));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = 4 * k + (lane >> 4), c8 = (lane & 15) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(so + row * OLD + c8);
+        if (tile * 16 + row < HW) st16(out + (s * HW + tile * 16 + row) * HID + c8, v);
       }
     }
   }
