@@ -8,7 +8,8 @@
 #   bash tools/gpu.sh TAG train [ARGS...]          tools/bench_train.py --profile
 #   bash tools/gpu.sh TAG trace                    rocprofv3 --kernel-trace --stats of the bench command
 #   bash tools/gpu.sh TAG pmc [HEAD]               FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic.json
-#   bash tools/gpu.sh TAG sq [SCRIPT]              SQ stall / mix / LDS / MFMA-busy passes -> summary.txt, mfma_util.txt
+#   bash tools/gpu.sh TAG sq [SCRIPT [ARGS...]]    SQ stall / mix / LDS / MFMA-busy passes -> summary.txt, mfma_util.txt
+#                                                  (CATSEG_HIP_LIB=... in the environment: another library, for A/B)
 #   bash tools/gpu.sh TAG final [HEAD]             tests + smoke + headline (with CPU leg) + configs + trace + pmc + sq
 #   bash tools/gpu.sh TAG final1                    the first half of final: tests + smoke + headline + configs
 #   bash tools/gpu.sh TAG final2 [HEAD]             the second half: trace + pmc + sq + the training step
@@ -54,12 +55,13 @@ pmc() {
 }
 sq() {
   local PY=${1:-tools/pmc_step.py}
+  shift || true                       # the rest: the script's arguments (e.g. micro_decoder.py's knob values)
   (cd /tmp &&
    timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
-     SQ_INSTS_MFMA SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace -f csv -d "$O/sqa" -o run -- python3 "$R/$PY" \
+     SQ_INSTS_MFMA SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace -f csv -d "$O/sqa" -o run -- python3 "$R/$PY" "$@" \
      > "$O/sqa.log" 2>&1 &&
    timeout -s KILL 150 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
-     SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -f csv -d "$O/sqb" -o run -- python3 "$R/$PY" \
+     SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -f csv -d "$O/sqb" -o run -- python3 "$R/$PY" "$@" \
      > "$O/sqb.log" 2>&1) &&
   python3 tools/pmc_summary.py "$O/sqa" "$O/sqb" --top 30 > "$O/summary.txt" 2>&1 &&
   python3 tools/mfma_util.py "$O/sqb" --top 40 > "$O/mfma_util.txt" 2>&1
