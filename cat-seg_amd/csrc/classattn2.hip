@@ -267,13 +267,23 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
     if (stamp && it < 8) stamps[it * 4 + 2] = __builtin_amdgcn_s_memtime();
     // ---------------- B: queries, output, residual ----------------
     // the next tile's q-guidance and residual rows are fetched one tile ahead (rows past T clamp)
+    // the residual rows as 16-byte loads: lane pair (q, q ^ 1) of a row reads the head's channels
+    // 8 (q & 2) + 16 (q & 1) .. +7 (the 4 + 4 that the even lane's jb = 0 and the odd lane's jb = 1
+    // need, plus their partner's) and swaps halves; 64-byte segments per row instead of 32
+    const int xcol = (q & 1) ? 12 + 4 * q : 4 * q;       // q = 0, 1, 2, 3 -> channels 0, 16, 8, 24
     auto fetch = [&](int tt, uint2* g, uint2* xr) {
       const int t = (a.dbg & 2) ? 0 : min(16 * tt + r16, T - 1);
 #pragma unroll
-      for (int ib = 0; ib < 2; ++ib) {
+      for (int ib = 0; ib < 2; ++ib)
         g[ib] = *reinterpret_cast<const uint2*>(tgb + t * ldg + h * D + ib * 16 + 4 * q);
-        xr[ib] = *reinterpret_cast<const uint2*>(xrow0 + t * xs + h * D + ib * 16 + 4 * q);
-      }
+      const uint4 w = *reinterpret_cast<const uint4*>(xrow0 + t * xs + h * D + xcol);
+      // even q holds channels 4q .. 4q+7 (its jb = 0 half, then the odd partner's); odd q holds
+      // 16 + 4(q-1) .. +7 (the even partner's jb = 1 half, then its own)
+      const uint2 mine = (q & 1) ? make_uint2(w.z, w.w) : make_uint2(w.x, w.y);
+      const uint2 give = (q & 1) ? make_uint2(w.x, w.y) : make_uint2(w.z, w.w);
+      const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
+      xr[0] = (q & 1) ? got : mine;
+      xr[1] = (q & 1) ? mine : got;
     };
     auto tile = [&](int tt, const uint2 (&gq)[2], const uint2 (&xr)[2]) {
       const int t = 16 * tt + r16;            // this lane's class row
@@ -308,16 +318,22 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
         o[jb] = mfma_bf16(khi[jb], bq8, f32x4{0.f, 0.f, 0.f, 0.f});
         o[jb] = mfma_bf16(klo[jb], bq8, o[jb]);
       }
-      if (t < T) {
+      uint2 yv[2];
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          // o[jb][r] = O[t][j = jb*16 + 4q + r]
-          const float xv[4] = {__uint_as_float(xr[jb].x << 16), __uint_as_float(xr[jb].x & 0xffff0000u),
-                               __uint_as_float(xr[jb].y << 16), __uint_as_float(xr[jb].y & 0xffff0000u)};
-          *reinterpret_cast<uint2*>(yrow0 + ((a.dbg & 2) ? 0 : t) * ys + h * D + jb * 16 + 4 * q) =
-              make_uint2(f2bf2(xv[0] + o[jb][0] * sc, xv[1] + o[jb][1] * sc),
-                         f2bf2(xv[2] + o[jb][2] * sc, xv[3] + o[jb][3] * sc));
-        }
+      for (int jb = 0; jb < 2; ++jb) {
+        // o[jb][r] = O[t][j = jb*16 + 4q + r]
+        const float xv[4] = {__uint_as_float(xr[jb].x << 16), __uint_as_float(xr[jb].x & 0xffff0000u),
+                             __uint_as_float(xr[jb].y << 16), __uint_as_float(xr[jb].y & 0xffff0000u)};
+        yv[jb] = make_uint2(f2bf2(xv[0] + o[jb][0] * sc, xv[1] + o[jb][1] * sc),
+                            f2bf2(xv[2] + o[jb][2] * sc, xv[3] + o[jb][3] * sc));
+      }
+      // one 16-byte store per lane: the pair (q, q ^ 1) swaps halves so that it holds 8 consecutive
+      // channels (the same layout as the residual load above); the swap runs on every lane
+      const uint2 give = (q & 1) ? yv[0] : yv[1];
+      const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
+      if (t < T) {
+        const uint4 w = (q & 1) ? make_uint4(got.x, got.y, yv[1].x, yv[1].y) : make_uint4(yv[0].x, yv[0].y, got.x, got.y);
+        *reinterpret_cast<uint4*>(yrow0 + ((a.dbg & 2) ? 0 : t) * ys + h * D + xcol) = w;
       }
     };
     uint2 gqA[2], xrA[2], gqB[2], xrB[2];

@@ -44,7 +44,8 @@ def main():
         d = (ys[variants[0]].float() - ys[variants[-1]].float()).abs()
         med = {v: sorted(t)[len(t) // 2] for v, t in times.items()}
         print(f"T={T}: max|diff| first/last variant {d.max().item():.3e} mean {d.mean().item():.3e}"
-              + "".join(f"  v{v} {med[v]:.1f} us" for v in variants), flush=True)
+              + "".join(f"  v{v} {med[v]:.1f} us" for v in variants)
+              + f"  checksum {ys[variants[0]].view(torch.int16).double().abs().sum().item():.0f}", flush=True)
 
 
 if __name__ == "__main__":

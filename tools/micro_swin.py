@@ -32,7 +32,7 @@ for shift in (0, 6):
         run(); torch.cuda.synchronize()
         o = out.float().clone()
         ref = o if ref is None else ref
-        res[v] = {"diff": (o - ref).abs().max().item(), "t": []}
+        res[v] = {"diff": (o - ref).abs().max().item(), "t": [], "ck": out.view(torch.int16).double().abs().sum().item()}
     for r in range(5):
         for v in variants:
             L.tune("swin_variant", v)
@@ -43,6 +43,7 @@ for shift in (0, 6):
             e1.record(); torch.cuda.synchronize()
             res[v]["t"].append(e0.elapsed_time(e1) / 5)
     for v in variants:
-        print(f"shift {shift} variant {v}: {sorted(res[v]['t'])[2] * 1e3:7.1f} us  max diff vs first {res[v]['diff']:.3e}",
+        print(f"shift {shift} variant {v}: {sorted(res[v]['t'])[2] * 1e3:7.1f} us  max diff vs first {res[v]['diff']:.3e}"
+              f"  checksum {res[v]['ck']:.0f}",
               flush=True)
 L.tune("swin_variant", 0)
