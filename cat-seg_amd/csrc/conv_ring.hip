@@ -408,27 +408,37 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         }
       }
     }
-    if constexpr (UP) {
-      // parity (pa, pb) of source pixel (y, x) -> pixel (2y + pa, 2x + pb) of the 2H x 2W map, COW channels
-#pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int pp = p0 + 16 * j + r16, yy = pp / W, xx = pp - yy * W;
-        bf16* ob = p.out + ((int64_t)s * 4 * HW + (2 * yy + pa) * (2 * W) + 2 * xx + pb) * CO + half * COW;
+    // bf16 stores of a pixel's 16 n-tile channels: with two n-tiles (32 channels of the pixel per
+    // wave) the lane pair (q, q ^ 1) swaps halves so that each lane holds 8 consecutive channels
+    // (even q: 4q .. 4q+7, odd q: 16 + 4(q-1) .. +7) and writes them as one 16-byte store -- the
+    // pixel's 64 bytes in one instruction instead of two 32-byte pieces
+    auto store_px = [&](bf16* ob, int j) {
+      if constexpr (FN == 2) {
+        const uint2 y0 = make_uint2(f2bf2(acc[0][j][0], acc[0][j][1]), f2bf2(acc[0][j][2], acc[0][j][3]));
+        const uint2 y1 = make_uint2(f2bf2(acc[1][j][0], acc[1][j][1]), f2bf2(acc[1][j][2], acc[1][j][3]));
+        const uint2 give = (q & 1) ? y0 : y1;
+        const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
+        st16(ob + ((q & 1) ? 12 + 4 * q : 4 * q),
+             (q & 1) ? make_uint4(got.x, got.y, y1.x, y1.y) : make_uint4(y0.x, y0.y, got.x, got.y));
+      } else {
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
           const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           store4<bf16>(ob + 16 * i + 4 * q, v);
         }
       }
+    };
+    if constexpr (UP) {
+      // parity (pa, pb) of source pixel (y, x) -> pixel (2y + pa, 2x + pb) of the 2H x 2W map, COW channels
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int pp = p0 + 16 * j + r16, yy = pp / W, xx = pp - yy * W;
+        store_px(p.out + ((int64_t)s * 4 * HW + (2 * yy + pa) * (2 * W) + 2 * xx + pb) * CO + half * COW, j);
+      }
     } else {
       bf16* ob = p.out + ((int64_t)s * HW + p0 + wpx * PXW) * COUT + wco * COW;
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          store4<bf16>(ob + (int64_t)(16 * j + r16) * COUT + 16 * i + 4 * q, v);
-        }
+      for (int j = 0; j < FM; ++j) store_px(ob + (int64_t)(16 * j + r16) * COUT, j);
     }
 
     // ---- the prefetched pixels into the ring (slots the next chunk's rows own), and the pixel

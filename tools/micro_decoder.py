@@ -61,4 +61,6 @@ for name in cases:
     for v in values:
         t = sorted(res[(name, v)])[2]
         same = torch.equal(outs[(name, v)], outs[(name, values[0])])
-        print(f"{name:10s} {knob}={v}: {t * 1e3:8.1f} us   bit-identical to {values[0]}: {same}", flush=True)
+        ck = outs[(name, v)].view(torch.int16).double().abs().sum().item()
+        print(f"{name:10s} {knob}={v}: {t * 1e3:8.1f} us   bit-identical to {values[0]}: {same}  checksum {ck:.0f}",
+              flush=True)
