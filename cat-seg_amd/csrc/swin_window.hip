@@ -342,6 +342,11 @@ DEV int local_region5(int wloc, int i, int shift) {   // region3 renumbered with
   return lh * 2 + lw;
 }
 
+// swin_win5's window image Xn: row-major 256-byte rows, 16-byte chunk c of row r at slot c ^ (r & 15):
+// the LDS-DMA fills whole rows (16 lanes per row), a fragment read (16 rows x one chunk) and a
+// LayerNorm row read (one row x 16 chunks) touch 16 distinct 16-byte bank slots
+DEV int xs5(int c, int r) { return (r * 16 + (c ^ (r & 15))) * 8; }
+
 template <bool SWM, bool GLIN>
 __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
@@ -376,7 +381,10 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
   auto fetch = [&](int win) {
     const int slice = win / NWIN;
     for (int k = h; k < NDMA; k += NW5) {
-      const int sl = k * 64 + lane, c = sl / L, i = (sl % L) ^ (c & 15);
+      // row-major image, chunk XOR-swizzled by the row (xs5): the 16 lanes of a row fetch its 16 chunks,
+      // so a wave-instruction reads 4 whole 256-byte rows (the chunk-major image it replaces read one
+      // 16-byte chunk of 64 rows)
+      const int sl = k * 64 + lane, i = sl >> 4, c = (sl & 15) ^ (i & 15);
       const bf16* src = p.x + (int64_t)win_row3(slice, wloc, i, p.shift) * p.ld_x + c * 8;
       dma16_opaque(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xn + k * 64 * 8)));
     }
@@ -426,7 +434,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
 #pragma unroll
       for (int st_ = 0; st_ < LNS5; ++st_) {
         const int i = min(st_ * 16 + lrow0, L - 1);
-        const uint4 raw = *reinterpret_cast<const uint4*>(&Xn[cs<L>(lc, i)]);
+        const uint4 raw = *reinterpret_cast<const uint4*>(&Xn[xs5(lc, i)]);
         const bf16* e = reinterpret_cast<const bf16*>(&raw);
         float v[8], sum = 0.f;
 #pragma unroll
@@ -441,7 +449,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = v[j] * rstd * lg[j] + lb[j];
         if (st_ * 16 + 4 * NW5 <= L || st_ * 16 + lrow0 < L)
-          st16(&Xn[cs<L>(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
+          st16(&Xn[xs5(lc, i)], make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7])));
       }
     }
     __syncthreads();
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       const int rb = 16 * t;
       s16x8 xb[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(((ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
+      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[xs5(ks * 4 + g, rb + r16)]);
       f32x4 dk[2], dv[2];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
@@ -492,7 +500,7 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
       const int rb = 16 * t;
       s16x8 xb[4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[(((ks * 4 + g) * L) + rb + (r16 ^ ((ks * 4 + g) & 15))) * 8]);
+      for (int ks = 0; ks < 4; ++ks) xb[ks] = *reinterpret_cast<const s16x8*>(&Xn[xs5(ks * 4 + g, rb + r16)]);
       f32x4 dq[2];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
