@@ -533,16 +533,24 @@ __global__ __launch_bounds__(NW * 64, (2 * NW + 3) / 4) void vit_attn3_kernel(At
       }
     }
   }
+  // 16-byte stores: per pair of 16-channel tiles (dt, dt + 1) the lane pair (g, g ^ 1) of a query
+  // swaps halves so that each lane holds 8 consecutive channels (even g: 4g .. 4g+7 of tile dt, odd g:
+  // 4(g-1) .. +7 of tile dt + 1); the swaps run on every lane, the stores only for queries < L
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     const int qi = q0 + 16 * t + col;
-    if (qi >= L) continue;
     const float inv = 1.f / osum[t][0];
-    bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + qi) * p.ldo + h * D;
+    bf16* O = reinterpret_cast<bf16*>(p.out) + (row0 + (qi < L ? qi : 0)) * p.ldo + h * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      float v[4] = {o[t][dt][0] * inv, o[t][dt][1] * inv, o[t][dt][2] * inv, o[t][dt][3] * inv};
-      store4<bf16>(O + dt * 16 + 4 * g, v);
+    for (int dp = 0; dp < 2; ++dp) {
+      const f32x4 a0 = o[t][2 * dp] * inv, a1 = o[t][2 * dp + 1] * inv;
+      const uint2 y0 = make_uint2(f2bf2(a0[0], a0[1]), f2bf2(a0[2], a0[3]));
+      const uint2 y1 = make_uint2(f2bf2(a1[0], a1[1]), f2bf2(a1[2], a1[3]));
+      const uint2 give = (g & 1) ? y0 : y1;
+      const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
+      if (qi < L)
+        st16(O + 32 * dp + ((g & 1) ? 12 + 4 * g : 4 * g),
+             (g & 1) ? make_uint4(got.x, got.y, y1.x, y1.y) : make_uint4(y0.x, y0.y, got.x, got.y));
     }
   }
 }

@@ -43,5 +43,7 @@ for v in variants:
     setv(v); run(); torch.cuda.synchronize()
     err = (out.float() - ref.float()).abs().max().item()
     t = sorted(res[v])[2]
-    print(f"variant {v}: {t * 1e3:7.1f} us  {flops / t / 1e9:6.1f} TF/s  max diff vs v0 {err:.2e}", flush=True)
+    ck = out.view(torch.int16).double().abs().sum().item()
+    print(f"variant {v}: {t * 1e3:7.1f} us  {flops / t / 1e9:6.1f} TF/s  max diff vs v0 {err:.2e}  checksum {ck:.0f}",
+          flush=True)
 setv(0)
