@@ -181,16 +181,18 @@ def layernorm(x, gamma, beta, out, *, rows=None, inmap=None, eps=1e-5, cols=None
 def l2normalize(x, out, *, rows=None, cols=None, inmap=None, eps=1e-12):
     cols = cols if cols is not None else out.shape[-1]
     rows = rows if rows is not None else out.shape[0]
-    call("catseg_l2normalize", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
-         rows, cols, eps, _stream())
+    with _rec("l2normalize", 0, rows * cols * (x.element_size() + out.element_size())):
+        call("catseg_l2normalize", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out),
+             _dt(out), rows, cols, eps, _stream())
     return out
 
 
 def convert(x, out, *, rows=None, cols=None, inmap=None):
     cols = cols if cols is not None else out.shape[-1]
     rows = rows if rows is not None else out.shape[0]
-    call("catseg_convert", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
-         rows, cols, _stream())
+    with _rec("convert", 0, rows * cols * (x.element_size() + out.element_size())):
+        call("catseg_convert", x.data_ptr(), _ld(x), inmap or IDENTITY, _dt(x), out.data_ptr(), _ld(out), _dt(out),
+             rows, cols, _stream())
     return out
 
 
@@ -204,7 +206,10 @@ def attention(q, k, v, out, *, n_seq, seq_len, n_heads, head_dim, scale, causal=
     a.scale, a.causal = scale, int(causal)
     a.mode, a.img_h, a.img_w, a.window, a.shift = mode, img_hw[0], img_hw[1], window, shift
     a.dtype = _dt(q)
-    with _rec("attention_window" if mode == 1 else "attention", 4 * n_seq * n_heads * seq_len * seq_len * head_dim):
+    # algorithmic bytes: q, k, v read once, the output written once
+    nbytes = n_seq * seq_len * n_heads * head_dim * (3 * q.element_size() + out.element_size())
+    with _rec("attention_window" if mode == 1 else "attention", 4 * n_seq * n_heads * seq_len * seq_len * head_dim,
+              nbytes):
         call("catseg_attention", a, _stream())
     return out
 
@@ -297,6 +302,21 @@ def _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, s1_offset, src2,
     return a
 
 
+def _conv_bytes(src1, weight, out, S, HW, c1, src2, c2, src2_div, addend, addend_div, out_px=None, out_ch=None):
+    """Algorithmic bytes of a 3x3 conv launch: each input pixel read once (the per-image src2 and
+    addend once per image), each output pixel written once, the weights read once."""
+    out_px = HW if out_px is None else out_px
+    out_ch = weight.shape[0] if out_ch is None else out_ch
+    n = S * HW * c1 * src1.element_size() + weight.numel() * weight.element_size()
+    if src2 is not None:
+        n += (S // max(src2_div, 1)) * HW * c2 * src2.element_size()
+    if out is not None:
+        n += S * out_px * out_ch * out.element_size()
+    if addend is not None:
+        n += (S // max(addend_div, 1)) * out_px * out_ch * 4
+    return n
+
+
 def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0,
             src2=None, c2=0, s2_slice_stride=0, s2_offset=0, src2_div=1,
             bias=None, act=L.ACT_NONE, gn=None, stats=None, stats_cpg=16, addend=None, addend_div=1):
@@ -309,7 +329,8 @@ def conv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, s1_offset=0
     if ws_bytes > 0:   # split-K scratch of small-grid convs (caching allocator; graph-capturable)
         ws = torch.empty(ws_bytes // 4, device=out.device, dtype=torch.float32)
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws_bytes
-    with _rec("conv3x3", 2 * S * H * W * weight.shape[0] * weight.shape[1]):
+    with _rec("conv3x3", 2 * S * H * W * weight.shape[0] * weight.shape[1],
+              _conv_bytes(src1, weight, out, S, H * W, c1, src2, c2, src2_div, addend, addend_div)):
         call("catseg_conv3x3", a, _stream())
     return out
 
@@ -330,7 +351,8 @@ def conv3x3_partial(g, weight, out, *, B, H, W):
     cout, k = weight.shape
     cin = k // 9
     assert g.shape[-1] == cin and out.dtype == torch.float32 and weight.dtype == torch.float32
-    with _rec("conv3x3_partial", 2 * B * H * W * cout * k):
+    with _rec("conv3x3_partial", 2 * B * H * W * cout * k,
+              B * H * W * (cin * g.element_size() + 4 * cout) + 4 * cout * k):
         call("catseg_conv3x3_partial", g.data_ptr(), B, H, W, cin, weight.data_ptr(), cout, out.data_ptr(), _dt(g),
              _stream())
     return out
@@ -348,7 +370,9 @@ def upconv3x3(src1, weight, out, *, S, H, W, c1, s1_slice_stride=None, gn=None, 
     # reference: ConvTranspose2d(c1 -> m, k=2, s=2) then conv3x3 over [up (m) | guidance (ref_guid)]
     m = ref_convt_out or 0
     ref = (2 * S * H * W * 4 * m * c1 + 2 * S * 4 * H * W * cout * 9 * (m + ref_guid)) if m else None
-    with _rec("upconv3x3", 2 * S * H * W * weight.shape[0] * 4 * c1, ref_flops=ref):
+    nbytes = _conv_bytes(src1, weight, out, S, H * W, c1, None, 0, 1, addend, addend_div, out_px=4 * H * W,
+                         out_ch=cout)
+    with _rec("upconv3x3", 2 * S * H * W * weight.shape[0] * 4 * c1, nbytes, ref_flops=ref):
         call("catseg_upconv3x3", a, _stream())
     return out
 
@@ -364,7 +388,8 @@ def upconv_addend(g, weight, tap_bias, out, *, B, H2, W2):
     cout, k = weight.shape
     cin = k // 9
     assert g.shape[-1] == cin and out.dtype == torch.float32 and weight.dtype == torch.float32
-    with _rec("conv3x3_partial", 2 * B * H2 * W2 * cout * k, ref_flops=0):   # in upconv3x3's reference count
+    with _rec("conv3x3_partial", 2 * B * H2 * W2 * cout * k,
+              B * H2 * W2 * (cin * g.element_size() + 4 * cout) + 4 * cout * k, ref_flops=0):   # in upconv3x3's reference count
         call("catseg_upconv_addend", g.data_ptr(), B, H2, W2, cin, weight.data_ptr(), _p(tap_bias), cout,
              out.data_ptr(), _dt(g), _stream())
     return out
@@ -375,8 +400,9 @@ def conv_tile_rows() -> int:
 
 
 def groupnorm_stats(partials, S, tiles, groups, tile_count, mean, rstd, eps=1e-5):
-    call("catseg_groupnorm_stats", partials.data_ptr(), S, tiles, groups, tile_count, eps, mean.data_ptr(),
-         rstd.data_ptr(), _stream())
+    with _rec("groupnorm_stats", 0, 4 * (S * tiles * groups * 2 + 2 * S * groups)):
+        call("catseg_groupnorm_stats", partials.data_ptr(), S, tiles, groups, tile_count, eps, mean.data_ptr(),
+             rstd.data_ptr(), _stream())
 
 
 def groupnorm_relu(x, y, *, S, HW, C, cpg, mean, rstd, gamma, beta):
@@ -391,15 +417,20 @@ def conv3x3_head(x, *, B, T, H, W, C, weight, bias, out, T_out, classes=None, gn
              out.data_ptr(), _dt(x), _stream())
     else:
         mean, rstd, gamma, beta, cpg = gn
-        call("catseg_conv3x3_head_gn", x.data_ptr(), B, T, H, W, C, weight.data_ptr(), bias, mean.data_ptr(),
-             rstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), cpg, _p(classes), T_out, out.data_ptr(), _dt(x),
-             _stream())
+        # one output channel: 9 taps x C MACs per pixel; x read once, the fp32 logit plane written once
+        with _rec("conv3x3_head_gn", 2 * B * T * H * W * C * 9, B * T * H * W * (C * x.element_size() + 4)):
+            call("catseg_conv3x3_head_gn", x.data_ptr(), B, T, H, W, C, weight.data_ptr(), bias, mean.data_ptr(),
+                 rstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), cpg, _p(classes), T_out, out.data_ptr(),
+                 _dt(x), _stream())
     return out
 
 
 def corr_embed(corr, *, t_stride, b_stride, B, T, H, W, weight, bias, out, classes=None):
-    call("catseg_corr_embed", corr.data_ptr(), t_stride, b_stride, _p(classes), B, T, H, W, weight.data_ptr(),
-         bias.data_ptr(), weight.shape[0], out.data_ptr(), _dt(out), _stream())
+    hidden = weight.shape[0]
+    # Conv2d(1, hidden, 7, pad 3): 49 MACs per output channel; each fp32 cost slice read once, X written once
+    with _rec("corr_embed", 2 * B * T * H * W * hidden * 49, B * T * H * W * (4 + hidden * out.element_size())):
+        call("catseg_corr_embed", corr.data_ptr(), t_stride, b_stride, _p(classes), B, T, H, W, weight.data_ptr(),
+             bias.data_ptr(), hidden, out.data_ptr(), _dt(out), _stream())
     return out
 
 
@@ -441,14 +472,19 @@ def fill(out, value):
 
 def preprocess_im2col(raw, sizes, *, mean, std, res, patch, out):
     B, _, Hp, Wp = raw.shape
-    call("catseg_preprocess_im2col", raw.data_ptr(), sizes.data_ptr(), B, Hp, Wp, mean.data_ptr(), std.data_ptr(),
-         res, patch, out.data_ptr(), _ld(out), _dt(out), _stream())
+    # the padded fp32 canvas read once, the patch matrix (with its zero K padding) written once
+    G = res // patch
+    with _rec("preprocess_im2col", 0, raw.numel() * 4 + B * G * G * _ld(out) * out.element_size()):
+        call("catseg_preprocess_im2col", raw.data_ptr(), sizes.data_ptr(), B, Hp, Wp, mean.data_ptr(),
+             std.data_ptr(), res, patch, out.data_ptr(), _ld(out), _dt(out), _stream())
     return out
 
 
 def vit_embed(patches, cls, pos, gamma, beta, out, *, B, G2, width):
-    call("catseg_vit_embed", patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-         B, G2, width, out.data_ptr(), _stream())
+    # fp32 patch rows read, the fp32 residual stream written (pos / cls / LN params are L2-resident)
+    with _rec("vit_embed", 0, 4 * width * (B * G2 + B * (G2 + 1))):
+        call("catseg_vit_embed", patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), gamma.data_ptr(),
+             beta.data_ptr(), B, G2, width, out.data_ptr(), _stream())
     return out
 
 
@@ -461,7 +497,8 @@ def postprocess(logits, out, *, crop=None):
     B, T, h, w = logits.shape
     H, W = out.shape[-2:]
     ch, cw = crop if crop is not None else (h, w)
-    call("catseg_postprocess", logits.data_ptr(), B, T, h, w, ch, cw, out.data_ptr(), H, W, _stream())
+    with _rec("postprocess", 0, 4 * B * T * (ch * cw + H * W)):
+        call("catseg_postprocess", logits.data_ptr(), B, T, h, w, ch, cw, out.data_ptr(), H, W, _stream())
     return out
 
 

@@ -431,33 +431,38 @@ DEV void lin_idx(int dst, int in_size, float scale, int& i0, int& i1, float& l1)
   l1 = src - (float)i0;
 }
 
-template <typename TO>
-__global__ void pre_im2col_kernel(const float* raw, const int32_t* sizes, int64_t B, int Hp, int Wp, const float* mean,
-                                  const float* stdv, int res, int patch, TO* out, int64_t ld_out) {
+constexpr int PRE_NT = 256;
+
+template <typename TO, int PATCH>
+__global__ __launch_bounds__(PRE_NT) void pre_im2col_kernel(const float* raw, const int32_t* sizes, int64_t B, int Hp, int Wp, const float* mean,
+                                  const float* stdv, int res, int patch_rt, TO* out, int64_t ld_out) {
+  const int patch = PATCH ? PATCH : patch_rt;   // 14 (L/14) and 16 (B/16) compiled: divisions by constants
+  // one workgroup per patch row m = (b, gy, gx): the row's image / patch coordinates are found once
+  // and the K columns are walked with 32-bit index math (per-element 64-bit div / mod before: 22 us)
   const int G = res / patch;
-  const int Kc = 3 * patch * patch;
-  const int64_t total = B * (int64_t)G * G * ld_out;
+  const int P2 = patch * patch;
+  const int Kc = 3 * P2;
+  const int64_t m = blockIdx.x;
+  const int64_t b = m / (G * G);
+  const int gp = (int)(m - b * (G * G)), gy = gp / G, gx = gp - gy * G;
   const float sy = (float)Hp / (float)res, sx = (float)Wp / (float)res;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int kcol = (int)(i % ld_out);
-    const int64_t m = i / ld_out;
+  const int h = sizes[2 * b], w = sizes[2 * b + 1];
+  TO* orow = out + m * ld_out;
+  for (int kcol = threadIdx.x; kcol < ld_out; kcol += blockDim.x) {
     float v = 0.f;
     if (kcol < Kc) {
-      const int64_t b = m / (G * G);
-      const int gp = (int)(m % (G * G)), gy = gp / G, gx = gp % G;
-      const int c = kcol / (patch * patch), kk = kcol % (patch * patch), ky = kk / patch, kx = kk % patch;
+      const int c = kcol / P2, kk = kcol - c * P2, ky = kk / patch, kx = kk - ky * patch;
       const int oy = gy * patch + ky, ox = gx * patch + kx;
       int y0, y1, x0, x1;
       float ly, lx;
       lin_idx(oy, Hp, sy, y0, y1, ly);
       lin_idx(ox, Wp, sx, x0, x1, lx);
-      const int h = sizes[2 * b], w = sizes[2 * b + 1];
       const float* img = raw + (b * 3 + c) * (int64_t)Hp * Wp;
       const float mu = mean[c], inv = 1.f / stdv[c];
-      auto px = [&](int y, int x) -> float { return (y < h && x < w) ? (img[(int64_t)y * Wp + x] - mu) * inv : 0.f; };
+      auto px = [&](int y, int x) -> float { return (y < h && x < w) ? (img[y * Wp + x] - mu) * inv : 0.f; };
       v = (1.f - ly) * ((1.f - lx) * px(y0, x0) + lx * px(y0, x1)) + ly * ((1.f - lx) * px(y1, x0) + lx * px(y1, x1));
     }
-    out[i] = from_f<TO>(v);
+    orow[kcol] = from_f<TO>(v);
   }
 }
 
@@ -814,14 +819,22 @@ extern "C" int catseg_preprocess_im2col(const float* raw, const int32_t* sizes, 
                                         int64_t ld_out, int dtype, void* stream) {
   CATSEG_CHECK(raw && sizes && mean && stdv && out && B > 0 && Hp > 0 && Wp > 0, "preprocess: bad args");
   CATSEG_CHECK(patch > 0 && res % patch == 0 && ld_out >= 3 * patch * patch, "preprocess: bad geometry");
+  CATSEG_CHECK((int64_t)Hp * Wp < (1ll << 31), "preprocess: canvas too large");
   const int G = res / patch;
-  const int64_t total = B * (int64_t)G * G * ld_out;
-  if (dtype == CATSEG_BF16)
-    hipLaunchKernelGGL(pre_im2col_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, raw, sizes, B,
-                       Hp, Wp, mean, stdv, res, patch, (bf16*)out, ld_out);
-  else
-    hipLaunchKernelGGL(pre_im2col_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, raw, sizes,
-                       B, Hp, Wp, mean, stdv, res, patch, (float*)out, ld_out);
+  const dim3 grid((unsigned)(B * G * G));
+  auto go = [&](auto kern, auto* o) {
+    hipLaunchKernelGGL(kern, grid, dim3(PRE_NT), 0, (hipStream_t)stream, raw, sizes, B, Hp, Wp, mean, stdv, res, patch, o,
+                       ld_out);
+  };
+  if (dtype == CATSEG_BF16) {
+    if (patch == 14) go(pre_im2col_kernel<bf16, 14>, (bf16*)out);
+    else if (patch == 16) go(pre_im2col_kernel<bf16, 16>, (bf16*)out);
+    else go(pre_im2col_kernel<bf16, 0>, (bf16*)out);
+  } else {
+    if (patch == 14) go(pre_im2col_kernel<float, 14>, (float*)out);
+    else if (patch == 16) go(pre_im2col_kernel<float, 16>, (float*)out);
+    else go(pre_im2col_kernel<float, 0>, (float*)out);
+  }
   return catseg_launch_status("preprocess_im2col");
 }
 

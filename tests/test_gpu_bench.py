@@ -62,4 +62,5 @@ def test_bench_one_gpu_line_contract():
     # every kernel family carries its floor (max of MFMA time and byte time) and the fraction reached
     for k, e in line["kernels"].items():
         assert e["floor_ms"] >= 0 and e["floor_bound"] in ("mfma", "hbm"), k
+        assert e["gflop"] > 0 or e["algorithmic_mb"] > 0, ("family without an algorithmic count", k, e)
         assert e["floor_frac"] is None or 0 <= e["floor_frac"] <= 1.5, (k, e)
