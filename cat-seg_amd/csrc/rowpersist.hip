@@ -236,6 +236,67 @@ DEV int hoff(int r, int e) { return r * LDH + ((((e >> 3) ^ ((r >> 2) & 1))) << 
 // holding units 8q .. 8q+7 of the pair: one 16-byte ds_write_b128 per row instead of two
 // 8-byte stores 16 units apart (whose 16 lanes sat 4-way on one bank pair at the 264-dword
 // row stride).  Every hidden unit is still one MFMA chain over the same k order: bit-identical.
+// GELU of the persistent MLPs as a segment table (tools/gelu_table_fit.py): Phi on [-5, 5] as 32 cubics
+// in the in-segment position, GELU(x) = x * P_seg(f).  Per value: fma + med3 (segment coordinate),
+// cvt + fract, one 16-byte LDS read of the segment's coefficients (512-byte table: at most two
+// segments per bank group), 3 fma + mul: 9 single-rate VALU against 2 med3 + 12 packed ops per value
+// pair for the degree-8 polynomial (gelu1, 3.0e-5), at a max GELU error of 4.3e-6.  Same box
+// (tools/micro_mlp.py): Swin proj + MLP 390 -> 379 us (the file built without SLP, Makefile).
+// GELU_SEG=0 builds the polynomial form (A/B).
+#ifndef GELU_SEG
+#define GELU_SEG 1
+#endif
+constexpr int GSEG = 32;
+__device__ const float kGeluSeg[GSEG][4] = {
+    {2.857138099e-07f, 4.937455742e-07f, 2.254223403e-07f, 3.768647900e-07f},
+    {1.379555215e-06f, 2.212427944e-06f, 1.064327307e-06f, 1.411648441e-06f},
+    {6.061552995e-06f, 9.013059753e-06f, 4.444804745e-06f, 4.744361377e-06f},
+    {2.424740342e-05f, 3.337237649e-05f, 1.648918806e-05f, 1.427804364e-05f},
+    {8.835084009e-05f, 1.122780523e-04f, 5.447883814e-05f, 3.837561962e-05f},
+    {2.934156510e-04f, 3.431500809e-04f, 1.605219877e-04f, 9.178832261e-05f},
+    {8.887727745e-04f, 9.524713387e-04f, 4.219991388e-04f, 1.943924581e-04f},
+    {2.457518829e-03f, 2.400514437e-03f, 9.894206887e-04f, 3.618174233e-04f},
+    {6.209207233e-03f, 5.492324010e-03f, 2.066157293e-03f, 5.848744768e-04f},
+    {1.435265690e-02f, 1.140593924e-02f, 3.833262948e-03f, 8.041608962e-04f},
+    {3.039636090e-02f, 2.149616554e-02f, 6.291609723e-03f, 9.010374779e-04f},
+    {5.908574536e-02f, 3.676088154e-02f, 9.071586654e-03f, 7.322515594e-04f},
+    {1.056510732e-01f, 5.703652650e-02f, 1.135013346e-02f, 2.143343008e-04f},
+    {1.742523909e-01f, 8.028168976e-02f, 1.203648932e-02f, -5.833524046e-04f},
+    {2.659869790e-01f, 1.025029495e-01f, 1.025549136e-02f, -1.413749764e-03f},
+    {3.773308992e-01f, 1.187075824e-01f, 5.908886902e-03f, -1.946855802e-03f},
+    {4.999994934e-01f, 1.246847883e-01f, -6.831953942e-05f, -1.946855802e-03f},
+    {6.226683259e-01f, 1.187726855e-01f, -6.014242303e-03f, -1.413749764e-03f},
+    {7.340127826e-01f, 1.026046127e-01f, -1.028643269e-02f, -5.833524046e-04f},
+    {8.257479072e-01f, 8.037979901e-02f, -1.199313626e-02f, 2.143343008e-04f},
+    {8.943495154e-01f, 5.710081011e-02f, -1.126834191e-02f, 7.322515594e-04f},
+    {9.409148097e-01f, 3.678249940e-02f, -8.994722739e-03f, 9.010374779e-04f},
+    {9.696039557e-01f, 2.148494869e-02f, -6.245745812e-03f, 8.041608962e-04f},
+    {9.856474400e-01f, 1.137926243e-02f, -3.820780898e-03f, 5.848744768e-04f},
+    {9.937907457e-01f, 5.464808084e-03f, -2.074873075e-03f, 3.618174233e-04f},
+    {9.975423813e-01f, 2.379646990e-03f, -1.005176571e-03f, 1.943924581e-04f},
+    {9.991111159e-01f, 9.395590168e-04f, -4.358869628e-04f, 9.178832261e-05f},
+    {9.997065067e-01f, 3.363625729e-04f, -1.696057006e-04f, 3.837561962e-05f},
+    {9.999116063e-01f, 1.091848826e-04f, -5.932331987e-05f, 1.427804364e-05f},
+    {9.999757409e-01f, 3.213575474e-05f, -1.867788887e-05f, 4.744361377e-06f},
+    {9.999939203e-01f, 8.576027540e-06f, -5.299272743e-06f, 1.411648441e-06f},
+    {9.999986291e-01f, 2.075184739e-06f, -1.356016696e-06f, 3.768647900e-07f},
+};
+// (fit: R = 5, 32 cubic segments; max |GELU error| 4.3e-6 on [-12, 12], 1.7e-6 on [-4, 4])
+DEV void stage_gelu_table(float4* sG) {
+  if (threadIdx.x < GSEG) sG[threadIdx.x] = *reinterpret_cast<const float4*>(kGeluSeg[threadIdx.x]);
+}
+DEV float gelu_seg(float x, const float4* sG) {
+  const float u = __builtin_amdgcn_fmed3f(__builtin_fmaf(x, GSEG / 10.f, GSEG / 2.f), 0.f, GSEG - 0x1p-18f);
+  const float4 c = sG[(int)u];
+  const float f = __builtin_amdgcn_fractf(u);
+  return x * __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, f, c.z), f, c.y), f, c.x);
+}
+template <int ACT>
+DEV float mlp_act(float v, const float4* sG) {
+  if constexpr (ACT == ACT_GELU) return GELU_SEG ? gelu_seg(v, sG) : gelu1(v);
+  else return act_t<ACT>(v);
+}
+
 template <int ACT, bool RES2, bool PROJ = false, bool PAIR = true>
 __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y, int64_t ldy, int64_t M,
                                                      const float* ln_g, const float* ln_b, float eps,
@@ -252,9 +313,11 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   __shared__ __attribute__((aligned(16))) float st[BM * SLD];
   // gamma / beta / b1 / b2 (/ bp) in LDS (see pgemm_kernel: no global loads behind the prefetch)
   __shared__ __attribute__((aligned(16))) float sPar[NPAR];
+  __shared__ __attribute__((aligned(16))) float4 sG[GSEG];
   for (int i = threadIdx.x; i < NPAR; i += NT)
     sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
             : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
+  stage_gelu_table(sG);
   __syncthreads();
   const float* sb1 = sPar + 2 * KD;
   const float* sb2 = sPar + 2 * KD + HID;
@@ -365,8 +428,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
-              else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
+              v[4 * i + r] = mlp_act<ACT>(acc1[i][j][r], sG);
             }
           st16(&sH[(16 * j + r16) * LDH + hh + hsw], pack8(v));
         }
@@ -377,13 +439,8 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
           float v[4];
-          if constexpr (ACT == ACT_GELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gelu1(acc1[i][j][r]);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc1[i][j][r]);
-          }
+          for (int r = 0; r < 4; ++r) v[r] = mlp_act<ACT>(acc1[i][j][r], sG);
           store4<bf16>(&sH[hoff(16 * j + r16, hh)], v);
         }
       }
@@ -447,9 +504,11 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
   __shared__ __attribute__((aligned(16))) bf16 r2res[RES2 ? 2 : 1][RES2 ? BM * KD : 8];
   __shared__ __attribute__((aligned(16))) bf16 xres[PROJ ? BM * KD : 8];       // PROJ: the x rows
   __shared__ __attribute__((aligned(16))) float sPar[NPAR];
+  __shared__ __attribute__((aligned(16))) float4 sG[GSEG];
   for (int i = threadIdx.x; i < NPAR; i += NT)
     sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
             : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
+  stage_gelu_table(sG);
   const float* sb1 = sPar + 2 * KD;
   const float* sb2 = sPar + 2 * KD + HID;
   const float* sbp = sPar + 3 * KD + HID;
@@ -521,8 +580,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if constexpr (ACT == ACT_GELU) v[4 * i + r] = gelu1(acc1[i][j][r]);
-            else v[4 * i + r] = act_t<ACT>(acc1[i][j][r]);
+            v[4 * i + r] = mlp_act<ACT>(acc1[i][j][r], sG);
           }
         st16(&sH[(16 * j + r16) * LDH + hh + hsw], pack8(v));
       }

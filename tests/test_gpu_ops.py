@@ -742,23 +742,26 @@ def test_topk_classes_exact(B, T, HW, k):
         assert cls[b].cpu().tolist() == order
 
 
-def test_preprocess_im2col():
+@pytest.mark.parametrize("p,res", [(16, 384), (14, 336), (12, 384)])
+def test_preprocess_im2col(p, res):
+    """Normalise + bilinear resize of ragged padded images + patch im2col vs the oracle's preprocess,
+    for the two compiled patch sizes (B/16, L/14) and the runtime-patch kernel."""
     arch_mean = torch.tensor([122.7709383, 116.7460125, 104.09373615])
     arch_std = torch.tensor([68.5005327, 66.6321579, 70.3231630])
     imgs = [torch.randint(0, 256, (3, 300, 352), generator=torch.Generator().manual_seed(1)).float(),
             torch.randint(0, 256, (3, 320, 256), generator=torch.Generator().manual_seed(2)).float()]
 
     class A:
-        clip_pixel_mean, clip_pixel_std, size_divisibility, clip_resolution = arch_mean.tolist(), arch_std.tolist(), 32, 384
+        clip_pixel_mean, clip_pixel_std, size_divisibility, clip_resolution = arch_mean.tolist(), arch_std.tolist(), 32, res
     ref, sizes = O.preprocess(A, imgs)
     Hp, Wp = 320, 352
     raw = torch.zeros(2, 3, Hp, Wp)
     for i, im in enumerate(imgs):
         raw[i, :, :im.shape[1], :im.shape[2]] = im
-    p = 16
-    out = torch.empty(2 * 24 * 24, 3 * p * p + 32, device=dev)
+    G = res // p
+    out = torch.empty(2 * G * G, 3 * p * p + 32, device=dev)
     ops.preprocess_im2col(raw.to(dev), torch.tensor(sizes, dtype=torch.int32).to(dev), mean=arch_mean.to(dev),
-                          std=arch_std.to(dev), res=384, patch=p, out=out)
+                          std=arch_std.to(dev), res=res, patch=p, out=out)
     cols = F.unfold(ref, p, stride=p).transpose(1, 2).reshape(-1, 3 * p * p)
     close(out[:, :3 * p * p], cols, atol=2e-5, what="preprocess")
     assert out[:, 3 * p * p:].abs().max().item() == 0
