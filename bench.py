@@ -41,7 +41,7 @@ sys.path.insert(0, ROOT)
 
 from cat_seg import ops  # noqa: E402
 from cat_seg import _lib as L  # noqa: E402
-from cat_seg.distributed import gather_logits, gather_logits_async  # noqa: E402
+from cat_seg.distributed import gather_logits, gather_logits_async, init_distributed  # noqa: E402
 from cat_seg.arch import VIT_B16, VIT_L14_336  # noqa: E402
 from cat_seg.engine import CatSegEngine  # noqa: E402
 from cat_seg.weights import synthesize_state_dict  # noqa: E402
@@ -79,9 +79,13 @@ def parse():
     ap.add_argument("--cpu-images", type=int, default=-1,
                     help="oracle sample size for cpu_baseline (-1 = the benched batch, 0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-boundary", action="store_true",
+                    help="skip the drop-in boundary leg (CATSeg.forward(list[dict]) on host uint8 images)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend for N > 1: nccl (= RCCL) when every rank has its own GPU, "
                          "gloo (logits staged through the host) to rehearse N ranks on fewer GPUs")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds before a rendezvous or collective that has not completed fails the run (N > 1)")
     ap.add_argument("--vit-fp8", action="store_true",
                     help="e4m3 CLIP image-encoder GEMMs (config 5's setting) on another config")
     return ap.parse_args()
@@ -140,10 +144,8 @@ def main():
     if world > 1:
         if backend == "auto":
             backend = "nccl" if n_dev >= world else "gloo"
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # bounded: a missing rank or a stuck collective exits non-zero after --dist-timeout seconds
+        init_distributed(backend, timeout_s=args.dist_timeout, device=dev)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}")
     cfg = CONFIGS[args.config]
@@ -261,6 +263,9 @@ def main():
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    boundary = None
+    if rank == 0 and world == 1 and not cfg5 and not args.no_boundary and args.config == 3:
+        boundary = boundary_pass(cfg, B, S, T, args.steps, args.warmup, value)
     roofline, kernels = None, None
     if rank == 0 and not args.no_roofline:
         roofline, kernels = roofline_pass(step, stream, dtype, vit_fp8, args.config)
@@ -293,6 +298,7 @@ def main():
                        "hipgraph": bool(graphs),
                        "gather_overlap": overlap if world > 1 else None},
             "roofline": roofline,
+            "boundary": boundary,
             # the whole path's fraction of the dtype's dense peak; None with fp8 ViT GEMMs (a mix of
             # fp8 and bf16 work has no single roof)
             "path_roofline": None if vit_fp8 else {
@@ -305,6 +311,41 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def boundary_pass(cfg, B, S, T, steps, warmup, engine_value):
+    """The reference's call shape (cat_seg_model.py:147-229, detectron2's inference loop): build_model(cfg)
+    -> CATSeg.forward(list[{"image": uint8 (3, S, S) HOST tensor}]) -> list[{"sem_seg": (T, S, S)}], timed
+    over the same steps as the engine leg.  Each call stages the host images through the model's reused
+    pinned canvas (one H2D copy of the uint8 bytes, the fp32 conversion on the device), replays the
+    forward's hipGraph and returns every image's probabilities as fresh device tensors."""
+    from cat_seg import build_model, get_cfg
+    c = get_cfg()
+    c.merge_from_file(os.path.join(ROOT, "cat-seg_amd", "configs", "vitl_336.yaml"))
+    c.merge_from_list(["MODEL.SEM_SEG_HEAD.POOLING_SIZES", "[1,1]", "MODEL.CATSEG_HIP.DTYPE", "bf16"])
+    model = build_model(c).cuda().eval()
+    model.sem_seg_head.predictor.set_class_tokens(class_tokens(cfg["tokens"], T))
+    gen = torch.Generator().manual_seed(4321)
+    batch = [{"image": (torch.rand(3, S, S, generator=gen) * 255).to(torch.uint8)} for _ in range(B)]
+    with torch.no_grad():
+        for _ in range(max(warmup, 1)):
+            out = model(batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = model(batch)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    assert len(out) == B and tuple(out[0]["sem_seg"].shape) == (T, S, S)
+    v = B * steps / el
+    res = {"value": round(v, 3), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "vs_engine": round(v / engine_value, 4),
+           "call": "build_model(cfg) -> CATSeg.forward(list[{'image': uint8 (3,336,336) host tensor}]) -> "
+                   f"{B} x {{'sem_seg': fp32 ({T},336,336) device tensor}}",
+           "staging": "reused pinned uint8 canvas, one H2D copy, fp32 conversion on the device, hipGraph replay"}
+    del model
+    torch.cuda.empty_cache()
+    return res
 
 
 def lib_sha16() -> str:

@@ -190,4 +190,5 @@ def add_cat_seg_config(cfg):
     cfg.MODEL.CATSEG_HIP.BPE_VOCAB = ""          # path to CLIP's bpe_simple_vocab_16e6.txt.gz
     cfg.MODEL.CATSEG_HIP.SYNTHETIC_SEED = 0      # weights when MODEL.WEIGHTS is empty
     cfg.MODEL.CATSEG_HIP.VIT_FP8 = False         # config 5: e4m3 CLIP image-encoder GEMMs (bf16 engine)
+    cfg.MODEL.CATSEG_HIP.GRAPH = True            # eval forward replayed from a hipGraph per input geometry
     return cfg

@@ -35,6 +35,23 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return begin, begin + sizes[rank]
 
 
+DEFAULT_TIMEOUT_S = 300.0
+
+
+def init_distributed(backend: str, timeout_s: float = DEFAULT_TIMEOUT_S, device=None) -> None:
+    """torch.distributed.init_process_group from the launcher's environment (RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT) with a BOUNDED timeout, so that a missing rank or a stuck first
+    collective ends the process with an error instead of hanging for the default 10 minutes (30 for
+    gloo): the rendezvous raises after `timeout_s`, and on RCCL the watchdog aborts a collective
+    that has not completed within it (TORCH_NCCL_ASYNC_ERROR_HANDLING, on unless the caller
+    disabled it)."""
+    import datetime
+    kw = {"timeout": datetime.timedelta(seconds=float(timeout_s))}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+
+
 def _world(group) -> Tuple[int, int]:
     if not (dist.is_available() and dist.is_initialized()):
         return 0, 1
@@ -103,14 +120,29 @@ def allreduce_gradients(params, group=None, bucket_mb: float = 64.0) -> int:
     train_net.py's `Trainer`, train_net.py:309-311 / detectron2 create_ddp_model): the `.grad` of every
     parameter that has one, flattened into fp32 buckets of <= bucket_mb, one all_reduce(SUM) per bucket
     (RCCL over xGMI on the GPU box; gloo stages device buckets through the host), divided by the world
-    size and copied back.  Buckets are filled in parameter order, so every rank reduces the same
-    buckets.  Returns the number of collectives issued (0 at world size 1)."""
+    size and copied back.  Every rank must reduce the SAME buckets even when ranks produced gradients
+    for different parameters (an unused branch on one rank): one small all_reduce(MAX) of the per-
+    parameter "has a gradient" flags comes first; a parameter with a gradient on ANY rank is reduced
+    everywhere (zeros where this rank has none, as DDP's unused-parameter path), one with a gradient on
+    no rank keeps `.grad = None`.  Buckets are filled in parameter order.  Returns the number of
+    collectives issued (0 at world size 1)."""
     rank, world = _world(group)
     if world == 1:
         return 0
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
+    ps = [p for p in params if p.requires_grad]
+    if not ps:
         return 0
+    dev = ps[0].device
+    staged = dev.type == "cuda" and dist.get_backend(group) == "gloo"
+    has = torch.tensor([p.grad is not None for p in ps], dtype=torch.int32, device="cpu" if staged else dev)
+    dist.all_reduce(has, op=dist.ReduceOp.MAX, group=group)
+    used = has.tolist()
+    for p, u in zip(ps, used):
+        if u and p.grad is None:
+            p.grad = torch.zeros_like(p)
+    grads = [p.grad for p, u in zip(ps, used) if u]
+    if not grads:
+        return 1
     limit = max(1, int(bucket_mb * (1 << 20)) // 4)
     buckets, cur, n = [], [], 0
     for g in grads:
@@ -133,7 +165,7 @@ def allreduce_gradients(params, group=None, bucket_mb: float = 64.0) -> int:
         for g in b:
             g.copy_(flat[o:o + g.numel()].view_as(g))
             o += g.numel()
-    return len(buckets)
+    return 1 + len(buckets)
 
 
 def create_ddp_model(model: torch.nn.Module, **kwargs) -> torch.nn.Module:

@@ -103,7 +103,26 @@ class AdamW(torch.optim.Optimizer):
              self.max_grad_norm, self._norm.data_ptr() if clip else None, self._ws.data_ptr() if clip else None,
              self._ws.numel() * 4 if clip else 0, _stream())
         self._keep = raw          # the descriptor array must outlive the queued kernels
+        # the kernel wrote the parameters through raw pointers, which autograd's version counters do
+        # not see: bump them as an in-place torch op would, so that everything keyed on `_version`
+        # (CATSeg.engine's converted inference weights, saved-tensor checks) sees the update
+        torch.autograd.graph.increment_version([p for p, *_ in entries])
         return loss
+
+
+class FullModelClipSGD(torch.optim.SGD):
+    """torch.optim.SGD inside the reference's FullModelGradientClippingOptimizer (train_net.py:228-243):
+    clip_grad_norm_ over every parameter of every group, then the SGD step."""
+
+    def __init__(self, params, lr, momentum=0.0, max_grad_norm: float = 0.0):
+        super().__init__(params, lr, momentum=momentum)
+        self.max_grad_norm = float(max_grad_norm)
+
+    def step(self, closure=None):
+        if self.max_grad_norm > 0:
+            all_params = [p for g in self.param_groups for p in g["params"]]
+            torch.nn.utils.clip_grad_norm_(all_params, self.max_grad_norm)
+        return super().step(closure=closure)
 
 
 _NORM_TYPES = (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d, torch.nn.BatchNorm3d, torch.nn.SyncBatchNorm,
@@ -114,14 +133,15 @@ _NORM_TYPES = (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d, torch.nn.BatchNorm3d,
 def build_optimizer(cfg, model: torch.nn.Module) -> torch.optim.Optimizer:
     """Trainer.build_optimizer (train_net.py:174-258): one group per trainable parameter with the
     reference's rules (BACKBONE_MULTIPLIER on "backbone", CLIP_MULTIPLIER on "clip_model",
-    WEIGHT_DECAY_NORM on norm modules, WEIGHT_DECAY_EMBED on nn.Embedding), SOLVER.OPTIMIZER ADAMW on
-    the device with full-model clipping when SOLVER.CLIP_GRADIENTS asks for it; SGD stays torch's."""
+    WEIGHT_DECAY_NORM on norm modules, WEIGHT_DECAY_EMBED on nn.Embedding, weight decay 0 for
+    relative_position_bias_table / absolute_pos_embed), SOLVER.OPTIMIZER ADAMW on the device, SGD as
+    torch's; either with full-model clipping when SOLVER.CLIP_GRADIENTS asks for it."""
     S = cfg.SOLVER
     defaults = {"lr": S.BASE_LR, "weight_decay": S.WEIGHT_DECAY}
     params: List[Dict[str, Any]] = []
     memo: Set[torch.nn.Parameter] = set()
     for module_name, module in model.named_modules():
-        for _, value in module.named_parameters(recurse=False):
+        for param_name, value in module.named_parameters(recurse=False):
             if not value.requires_grad or value in memo:
                 continue
             memo.add(value)
@@ -130,6 +150,8 @@ def build_optimizer(cfg, model: torch.nn.Module) -> torch.optim.Optimizer:
                 hyper["lr"] = hyper["lr"] * S.BACKBONE_MULTIPLIER
             if "clip_model" in module_name:
                 hyper["lr"] = hyper["lr"] * S.CLIP_MULTIPLIER
+            if "relative_position_bias_table" in param_name or "absolute_pos_embed" in param_name:
+                hyper["weight_decay"] = 0.0            # train_net.py:216-221 (Swin-backbone parameters)
             if isinstance(module, _NORM_TYPES):
                 hyper["weight_decay"] = S.WEIGHT_DECAY_NORM
             if isinstance(module, torch.nn.Embedding):
@@ -143,5 +165,5 @@ def build_optimizer(cfg, model: torch.nn.Module) -> torch.optim.Optimizer:
     if S.OPTIMIZER == "ADAMW":
         return AdamW(params, S.BASE_LR, max_grad_norm=cg.CLIP_VALUE if full_clip else 0.0)
     if S.OPTIMIZER == "SGD":
-        return torch.optim.SGD(params, S.BASE_LR, momentum=S.MOMENTUM)
+        return FullModelClipSGD(params, S.BASE_LR, momentum=S.MOMENTUM, max_grad_norm=cg.CLIP_VALUE if full_clip else 0.0)
     raise NotImplementedError(f"no optimizer type {S.OPTIMIZER}")

@@ -693,6 +693,409 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Wide tiles for the ViT GEMMs: BM = 320 (or 256) rows x BN = 256 / 192 columns, one 8-wave
+// workgroup per CU.  At M = 4616 the 320-row tiles make ONE round on 240 CUs for fc1 (15 x 16 at
+// BN 256) and QKV (15 x 16 at BN 192), with half of gemm3's L2 -> LDS bytes per FLOP (142 FLOP
+// per byte at 320 x 256 vs 71 at 160 x 128).
+//   * ring: S stages of BK = 32 (64 bytes per row), filled by LDS-DMA (16 B per lane, lane-linear
+//     1 KB per wave-instruction = 16 rows); wave w issues instructions w, w + 8, ... of a stage
+//     (5 or 4 of the 36 of a 320 + 256 stage), counted per wave in vmcnt;
+//   * swizzle: the 16-byte chunk c of row r sits at slot c ^ g[(r >> 2) & 3], g = {0, 2, 3, 1}:
+//     the four lane groups of a ds_read_b128 fragment read (rows 0-15, chunk = lane >> 4) hit 16
+//     distinct bank slots each (tools/lds_bank_model.py), and the DMA writes are linear;
+//   * 8 waves as 2 (m) x 4 (n), a (BM / 2) x (BN / 4) wave tile: 160 x 64 = 14 fragment reads per
+//     40 MFMAs, 160 accumulator VGPRs;
+//   * epilogue through LDS in rounds of 64 rows (coalesced 16-byte stores of whole rows).
+// gemm4 is the plain K-loop (one barrier per K-step, all waves in step); gemm5 the ping-pong form.
+// Arithmetic per output = gemm3's (the same MFMA over the same k order, the same epilogue
+// expression), so the tile choice never changes a bit (batch invariance).
+// ------------------------------------------------------------------------------------
+// 16-byte LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds): base and size are wave-
+// uniform, the lane's part is a 32-bit byte offset, `soff` a uniform byte offset (SGPR)
+DEV void dma_buf16(const void* base, int bytes, void* lds, int voff, int soff) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, soff, 0, 0);
+}
+
+DEV int swz4(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }   // g = {0, 2, 3, 1} as 2-bit fields
+
+// Tile origin for the wide kernels: after the XCD remap, groups of `group_m` m-tiles sweep the
+// n-tiles, so an XCD's contiguous range of workgroups covers a compact block of A and W panels.
+DEV void wide_tile(int wg, int64_t M, int BM, int tiles_n, int group_m, int& tm_i, int& tn_i) {
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int per = group_m * tiles_n, g = wg / per, r = wg - g * per;
+  const int gs = min(group_m, tiles_m - g * group_m);
+  tm_i = g * group_m + r % gs;
+  tn_i = r / gs;
+}
+
+// LDS-staged epilogue shared by gemm4 / gemm5: rounds of 64 tile rows (2 m-fragments per wave
+// row) staged as fp32, each thread then stores 8 consecutive columns of whole rows; the bias of a
+// thread's items is loaded once, a round's residual rows are all requested before the round's
+// first barrier.
+template <typename TO, int BM, int BN, int EPI, int FM, int FN>
+DEV void wide_epilogue(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, int64_t M, int64_t m0, int64_t n0) {
+  constexpr int NT4 = 512, WGM = 2, WM = BM / WGM, WN = BN / 4;
+  constexpr int JR = 2, ROWS = WGM * JR * 16, SLD = BN + 4;
+  static_assert(FM % JR == 0, "epilogue rounds");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wmi = wave / 4, wn = (wave % 4) * WN;
+  float* stg = reinterpret_cast<float*>(smem);
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  constexpr int CG = BN / 8, ITEMS = ROWS * CG, IPT = (ITEMS + NT4 - 1) / NT4;
+  static_assert(ITEMS % 64 == 0, "whole waves per epilogue item slot");
+  // when 512 is a multiple of the column groups every item of a thread has the same 8 columns
+  constexpr bool SAMEC = NT4 % CG == 0;
+  constexpr int NB = SAMEC ? 1 : IPT;
+  int lr[IPT], c8[IPT];
+  float bias[NB][8];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int idx = min(tid + k * NT4, ITEMS - 1);
+    lr[k] = idx / CG;
+    c8[k] = (idx % CG) * 8;
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bias[k][r] = 0.f;
+    if (e.bias) load8f(e.bias + n0 + c8[k], bias[k]);
+  }
+  const bool res = EPI == 1 && e.res;
+#pragma unroll
+  for (int h = 0; h < FM / JR; ++h) {
+    int64_t mk[IPT];
+    float rv[IPT][8];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int lrow = lr[k], wi = lrow / (JR * 16), jj = (lrow / 16) % JR, rr = lrow % 16;
+      mk[k] = m0 + wi * WM + (h * JR + jj) * 16 + rr;
+      if (res) load8f(reinterpret_cast<const TO*>(e.res) + min<int64_t>(mk[k], M - 1) * e.ld_res + n0 + c8[k], rv[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < JR; ++jj)
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        *reinterpret_cast<f32x4*>(&stg[((wmi * JR + jj) * 16 + col) * SLD + wn + 16 * i + rq]) = acc[i][h * JR + jj];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      if (tid + k * NT4 < ITEMS && mk[k] < M) {
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(&stg[lr[k] * SLD + c8[k]]);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(&stg[lr[k] * SLD + c8[k] + 4]);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += bias[SAMEC ? 0 : k][r];
+        if constexpr (EPI == 2) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = apply_act(v[r], ACT_QUICKGELU);
+        }
+        if (res) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] += rv[k][r];
+        }
+        store8f(reinterpret_cast<TO*>(e.out) + mk[k] * e.ldo + n0 + c8[k], v);
+      }
+    }
+  }
+}
+
+// DMA plan of a wide stage: instruction i = wave + 8 j covers stage rows 16 i .. 16 i + 15 (A rows
+// first, then W rows); lane -> row 16 i + lane / 4, physical slot lane % 4, which holds logical
+// chunk (lane % 4) ^ g(row).  Rows past M read row M - 1 (masked in the epilogue).
+template <int BM, int BN>
+struct WideDma {
+  static constexpr int BK = 32, STAGE = (BM + BN) * BK, NI = (BM + BN) / 16, JMAX = (NI + 7) / 8;
+  static_assert(BM % 16 == 0 && BN % 16 == 0, "rows per DMA instruction");
+  const bf16* src[JMAX];
+  bool full;                                   // this wave issues JMAX instructions per stage (else JMAX - 1)
+  DEV WideDma(const bf16* A, int64_t lda, const bf16* W, int64_t ldw, int64_t M, int64_t m0, int64_t n0, int wave,
+              int lane) {
+    full = (wave + 8 * (JMAX - 1)) < NI;
+    const int dch = (lane & 3) ^ swz4(lane >> 2);
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+      const int i = min(wave + 8 * j, NI - 1);
+      const int row = 16 * i + (lane >> 2);
+      if (row < BM) {
+        const int64_t m = min<int64_t>(m0 + row, M - 1);
+        src[j] = A + m * lda + dch * 8;
+      } else {
+        src[j] = W + (n0 + row - BM) * ldw + dch * 8;
+      }
+    }
+  }
+  DEV void issue(bf16* stage, int64_t k0, int wave) const {
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j)
+      if (j < JMAX - 1 || full)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[j] + k0), (lds_void_t*)(stage + (wave + 8 * j) * 512), 16, 0, 0);
+  }
+  // wait until at most `tiles` younger stages of this wave's DMA are outstanding
+  template <int TILES>
+  DEV void wait() const {
+    if (full) wait_vmcnt<TILES * JMAX>();
+    else wait_vmcnt<TILES * (JMAX - 1)>();
+  }
+};
+
+template <typename TO, int BM, int BN, int S, int EPI>
+__global__ __launch_bounds__(512) void gemm4_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
+                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
+                                                    int group_m) {
+  constexpr int BK = 32, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
+  using D = WideDma<BM, BN>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[S * D::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tm_i, tn_i;
+  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int wm = (wave / 4) * WM, wn = (wave % 4) * WN;
+  const D dma(A, lda, W, ldw, M, m0, n0, wave, lane);
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15;
+  const int foff = r16 * BK + (((lane >> 4) ^ swz4(r16)) * 8);
+  const int ktiles = (int)(K / BK);
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < ktiles) dma.issue(smem + t * D::STAGE, (int64_t)t * BK, wave);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    if (kt + S - 2 < ktiles) dma.template wait<S - 2>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();                 // stage kt visible; stage (kt - 1) % S free
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + S - 1 < ktiles) dma.issue(smem + ((kt + S - 1) % S) * D::STAGE, (int64_t)(kt + S - 1) * BK, wave);
+    const bf16* As = smem + (kt % S) * D::STAGE;
+    const bf16* Ws = As + BM * BK;
+    s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + foff]);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + foff]);
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
+  }
+  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
+}
+
+// gemm5: the same tile as a PING-PONG loop (cdna_hip_programming.md §5, the staggered 8-wave
+// template).  Waves w and w + 4 share a SIMD; the waves of the second m-half (group 1 = waves 4-7)
+// run one barrier behind group 0, so between any two barriers one group issues its K-step's
+// fragment reads, LDS-DMA and counted waits (the LOAD segment) while the other issues its MFMAs
+// (the COMPUTE segment): each SIMD's matrix pipe is fed by one wave while its partner loads.
+// Per K-step t a wave: LOAD(t) = read all fragments of stage t, issue the DMA of stage t + S - 1
+// (into the slot of stage t - 1, whose reads every wave retired before the previous barrier),
+// lgkmcnt(0), wait its own DMA of stage t + 1, barrier; COMPUTE(t) = FM x FN MFMAs, barrier.
+// Barrier #k (B0 = the prologue's): group 0's LOAD(t) ends at #2t+1, COMPUTE(t) at #2t+2; group 1's
+// at #2t+2 / #2t+3.  RAW: stage t + 1 is read after #2t+2 (group 0) / #2t+3 (group 1), and every
+// wave waited its DMA of t + 1 before #2t+2.  WAR: stage t - 1's slot is refilled in LOAD(t), after
+// #2t (group 0) / #2t+1 (group 1); the last reads of t - 1 (group 1's LOAD(t - 1)) retired before #2t.
+template <typename TO, int BM, int BN, int S, int EPI, int ABL = 0>
+__global__ __launch_bounds__(512) void gemm5_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
+                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
+                                                    int group_m) {
+  constexpr int BK = 32, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
+  static_assert(S >= 3, "the ping-pong ring needs a stage beyond the two being read");
+  using D = WideDma<BM, BN>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[S * D::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave-uniform group (scalar branch for the stagger barrier)
+  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;
+  int tm_i, tn_i;
+  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int wm = grp * WM, wn = (wave % 4) * WN;
+  const D dma(A, lda, W, ldw, M, m0, n0, wave, lane);
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15;
+  const int foff = r16 * BK + (((lane >> 4) ^ swz4(r16)) * 8);
+  const int ktiles = (int)(K / BK);
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < ktiles) dma.issue(smem + t * D::STAGE, (int64_t)t * BK, wave);
+  if (S - 1 <= ktiles) dma.template wait<S - 2>();     // own stage 0 landed
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();                        // B0: stage 0 visible
+  if (grp == 1) __builtin_amdgcn_s_barrier();          // the stagger
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    // ---- LOAD(kt) ----
+    const bf16* As = smem + (kt % S) * D::STAGE;
+    const bf16* Ws = As + BM * BK;
+    s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + foff]);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + foff]);
+    if (ABL != 1 && kt + S - 1 < ktiles) dma.issue(smem + ((kt + S - 1) % S) * D::STAGE, (int64_t)(kt + S - 1) * BK, wave);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (ABL == 1) {
+    } else if (kt + S - 1 < ktiles) {
+      dma.template wait<S - 2>();   // own stage kt + 1 landed (kt + 2 .. kt + S - 1 in flight)
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- COMPUTE(kt) ----
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (ABL == 2) {
+      // ablation: no MFMAs (keep the fragments live)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) asm volatile("" :: "v"(bfrag[j]));
+#pragma unroll
+      for (int i = 0; i < FN; ++i) asm volatile("" :: "v"(afrag[i]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
+  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
+}
+
+// gemm6: gemm5's ping-pong with FULL-LINE staging.  The ablations of gemm5 at 8192^3 (256 x 256)
+// show the fill, not the MFMA loop, is its bound: without the LDS-DMA the loop runs at 0.71 of the
+// dense peak, without the MFMAs the loads alone take 724 of the 893 us.  gemm5's DMA moves 16 rows x
+// 64 B per wave-instruction (BK = 32: half a 128-B line per row), the fragment-shaped pattern the
+// guide prices at twice the TA work of whole lines.  gemm6 stages BK = 64 (8 rows x 128 B per
+// instruction) into S = 2 slots (2 x (BM + BN) x 128 B of LDS) and runs each K64 tile as two k32
+// phases, so the per-wave fragment registers stay those of one k32 step.
+// Schedule (interval = the span between two barriers; group 1 one interval behind group 0):
+//   group 0: L(t,0) @4t, C(t,0) @4t+1, L(t,1) @4t+2, C(t,1) @4t+3;  group 1: each one later.
+//   L(t,0) issues the wave's share of tile t + 1's DMA (slot (t + 1) % 2 = (t - 1) % 2, whose last
+//   reads -- group 1's L(t - 1, 1) @4t-1 -- retired before the barrier that opened @4t);
+//   tile t + 1 is read from @4t+4 (group 0) / @4t+5 (group 1), so every wave waits its own DMA of
+//   t + 1 before the barrier closing @4t+3: group 0 at the end of C(t,1), group 1 at the end of L(t,1).
+// Swizzle: the 16-byte chunk c of row r sits at slot c ^ ((r / 2) % 8) (Swz<64>, as gemm3).
+template <typename TO, int BM, int BN, int EPI, int ABL = 0>
+__global__ __launch_bounds__(512) void gemm6_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
+                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
+                                                    int group_m) {
+  constexpr int BK = 64, BKC = 8, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
+  constexpr int STAGE = (BM + BN) * BK, NI = (BM + BN) / 8, JMAX = (NI + 7) / 8;
+  static_assert(BM % 16 == 0 && BN % 16 == 0, "rows per fragment");
+  using SW = Swz<64>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;
+  int tm_i, tn_i;
+  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int wm = grp * WM, wn = (wave % 4) * WN;
+
+  // DMA plan: instruction i = wave + 8 j covers stage rows 8 i .. 8 i + 7 (A rows, then W rows);
+  // lane -> row 8 i + lane / 8, physical slot lane % 8 = logical chunk SW::slot(row, lane % 8).
+  // Buffer loads (buffer_load_dwordx4 ... lds): whether instruction j reads A or W is wave-uniform,
+  // the lane's part is one 32-bit byte offset, the K offset goes in soffset (no per-issue VALU).
+  const int64_t abytes = M * lda * 2, wbytes = (int64_t)tiles_n * BN * ldw * 2;
+  const int anr = abytes < 0x7fffffff ? (int)abytes : 0x7fffffff, wnr = wbytes < 0x7fffffff ? (int)wbytes : 0x7fffffff;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const bool full = (wave + 8 * (JMAX - 1)) < NI;
+  int voff[JMAX];
+#pragma unroll
+  for (int j = 0; j < JMAX; ++j) {
+    const int i = min(wave + 8 * j, NI - 1);
+    const int row = 8 * i + (lane >> 3), ch = SW::slot(row, lane & 7);
+    if (row < BM) {
+      const int64_t m = min<int64_t>(m0 + row, M - 1);
+      voff[j] = (int)((m * lda + ch * 8) * 2);
+    } else {
+      voff[j] = (int)(((n0 + row - BM) * ldw + ch * 8) * 2);
+    }
+  }
+  auto issue = [&](int kt) {
+    bf16* st = smem + (kt & 1) * STAGE;
+    const int kb = kt * BK * 2;
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+      if (j < JMAX - 1 || full) {
+        if ((wv + 8 * j) * 8 < BM) dma_buf16(A, anr, st + (wv + 8 * j) * 512, voff[j], kb);   // wave-uniform choice
+        else dma_buf16(W, wnr, st + (wv + 8 * j) * 512, voff[j], kb);
+      }
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, q = lane >> 4;
+  // fragment address of row base rb (a multiple of 16), k32 half h: rows rb + r16, chunk 4 h + q,
+  // whose slot (4 h + q) ^ ((r16 / 2) % 8) depends on the lane only
+  const int fo0 = r16 * BK + ((q ^ ((r16 >> 1) & 7)) * 8), fo1 = r16 * BK + (((4 + q) ^ ((r16 >> 1) & 7)) * 8);
+  auto fptr = [&](const bf16* base, int rb, int h) {
+    return reinterpret_cast<const s16x8*>(&base[rb * BK + (h ? fo1 : fo0)]);
+  };
+  const int ktiles = (int)(K / BK);
+  issue(0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();                        // tile 0 visible
+  if (grp == 1) __builtin_amdgcn_s_barrier();          // the stagger
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const bf16* As = smem + (kt & 1) * STAGE;
+    const bf16* Ws = As + BM * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // ---- LOAD(kt, h) ----
+      s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) afrag[i] = *fptr(Ws, wn + 16 * i, h);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfrag[j] = *fptr(As, wm + 16 * j, h);
+      if (ABL != 1 && h == 0 && kt + 1 < ktiles) issue(kt + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ABL != 1 && h == 1 && grp == 1) wait_vmcnt<0>();     // group 1: own DMA of kt + 1 landed
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- COMPUTE(kt, h) ----
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (ABL == 2) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j) asm volatile("" :: "v"(bfrag[j]));
+#pragma unroll
+        for (int i = 0; i < FN; ++i) asm volatile("" :: "v"(afrag[i]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (ABL != 1 && h == 1 && grp == 0) wait_vmcnt<0>();     // group 0: own DMA of kt + 1 landed
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
+  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
+}
+
 int g_gemm_group = 4;   // gemm3 tile order: 0 = row-major, G > 0 = G m-tiles per group (catseg_set_gemm_group); 4 measured best (fc2 48.6 -> 47.4 us)
 
 EpiArgs make_epi(const CatsegGemmArgs* g) {
@@ -708,6 +1111,29 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   e.sa = nullptr; e.sw = nullptr;
   e.pf = g_epi_prefetch;
   return e;
+}
+
+int g_gemm4_group = 5;   // gemm4 tile order: G m-tiles per group (catseg_set_gemm4_group)
+
+// KIND 4 = gemm4 (plain K-loop), 5 = gemm5 (ping-pong)
+template <typename TO, int BM, int BN, int S, int EPI, int KIND = 5, int ABL = 0>
+bool launch4(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->N % BN != 0 || g->K % (KIND == 6 ? 64 : 32) != 0) return false;
+  const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
+  if (!ident) return false;
+  const EpiArgs e = make_epi(g);
+  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
+  if constexpr (KIND == 6) {
+    auto kern = gemm6_kernel<TO, BM, BN, EPI, ABL>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A, g->lda, (const bf16*)g->W,
+                       g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
+  } else if constexpr (KIND == 4)
+    hipLaunchKernelGGL((gemm4_kernel<TO, BM, BN, S, EPI>), dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A,
+                       g->lda, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
+  else
+    hipLaunchKernelGGL((gemm5_kernel<TO, BM, BN, S, EPI, ABL>), dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A,
+                       g->lda, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
+  return true;
 }
 
 template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool SC = false, int EPI = 0>
@@ -799,6 +1225,29 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 1 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 1>(g, st);
   if (epi == 2 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 2>(g, st);
   if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
+  // wide tiles (lean epilogues only): 30-33 gemm4, 40-45 gemm5 (ping-pong)
+  if (v >= 30 && v < 60 && (epi == 1 || epi == 2)) {
+    const bool e1 = epi == 1;
+    switch (v) {
+      case 30: return e1 ? launch4<TO, 320, 256, 4, 1, 4>(g, st) : launch4<TO, 320, 256, 4, 2, 4>(g, st);
+      case 31: return e1 ? launch4<TO, 320, 192, 4, 1, 4>(g, st) : launch4<TO, 320, 192, 4, 2, 4>(g, st);
+      case 40: return e1 ? launch4<TO, 320, 256, 4, 1>(g, st) : launch4<TO, 320, 256, 4, 2>(g, st);
+      case 41: return e1 ? launch4<TO, 320, 192, 4, 1>(g, st) : launch4<TO, 320, 192, 4, 2>(g, st);
+      case 42: return e1 ? launch4<TO, 256, 256, 4, 1>(g, st) : launch4<TO, 256, 256, 4, 2>(g, st);
+      case 43: return e1 ? launch4<TO, 320, 256, 3, 1>(g, st) : launch4<TO, 320, 256, 3, 2>(g, st);
+      case 44: return e1 ? launch4<TO, 256, 192, 4, 1>(g, st) : launch4<TO, 256, 192, 4, 2>(g, st);
+      case 45: return e1 ? launch4<TO, 256, 128, 4, 1>(g, st) : launch4<TO, 256, 128, 4, 2>(g, st);
+      case 46: return launch4<TO, 256, 256, 4, 1, 5, 1>(g, st);   // ablation: no LDS-DMA (wrong output)
+      case 47: return launch4<TO, 256, 256, 4, 1, 5, 2>(g, st);   // ablation: no MFMA (wrong output)
+      // gemm6 (ping-pong, full-line BK = 64 staging)
+      case 50: return e1 ? launch4<TO, 320, 256, 2, 1, 6>(g, st) : launch4<TO, 320, 256, 2, 2, 6>(g, st);
+      case 51: return e1 ? launch4<TO, 320, 192, 2, 1, 6>(g, st) : launch4<TO, 320, 192, 2, 2, 6>(g, st);
+      case 52: return e1 ? launch4<TO, 256, 256, 2, 1, 6>(g, st) : launch4<TO, 256, 256, 2, 2, 6>(g, st);
+      case 56: return launch4<TO, 256, 256, 2, 1, 6, 1>(g, st);   // ablation: no LDS-DMA (wrong output)
+      case 57: return launch4<TO, 256, 256, 2, 1, 6, 2>(g, st);   // ablation: no MFMA (wrong output)
+      default: return false;
+    }
+  }
   // forced tiles (gemm_variant, tests / tools/micro_gemm.py): the automatic candidates only
   switch (v) {
     case 1: return launch3<TO, 256, 256, 2, 4, 2, 64>(g, st);
@@ -905,6 +1354,7 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
 
 CATSEG_KNOB(g_gemm_variant, "gemm_variant");
 CATSEG_KNOB(g_gemm_group, "gemm_group");
+CATSEG_KNOB(g_gemm4_group, "gemm4_group");
 CATSEG_KNOB(g_epi_prefetch, "epi_prefetch");
 CATSEG_KNOB(g_gemm_f8_variant, "gemm_fp8_variant");
 

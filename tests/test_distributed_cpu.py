@@ -142,10 +142,12 @@ def _grad_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         gen = torch.Generator().manual_seed(100 + rank)
-        params = [torch.nn.Parameter(torch.zeros(s)) for s in ((300, 7), (11,), (5, 5, 5), (4096,))]
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in ((300, 7), (11,), (5, 5, 5), (4096,), (9,))]
         for p in params:
             p.grad = torch.randn(p.shape, generator=gen)
-        params[1].grad = None                        # a parameter without a gradient stays untouched
+        params[1].grad = None                        # no gradient on any rank: stays untouched
+        if rank == 1:
+            params[4].grad = None                    # an unused branch on rank 1 only
         n = D.allreduce_gradients(params, bucket_mb=0.01)
         torch.save({"n": n, "grads": [None if p.grad is None else p.grad for p in params]},
                    os.path.join(out_dir, f"g{rank}.pt"))
@@ -156,7 +158,8 @@ def _grad_worker(rank, world, port, out_dir):
 def test_allreduce_gradients_world2_gloo():
     """Data-parallel gradient averaging (the DDP all-reduce of train_net.py:309-311): every rank ends
     with the mean of the ranks' gradients, bucketed (three buckets at 10 KB), parameters without a
-    gradient untouched."""
+    gradient on any rank untouched, one with a gradient on one rank only reduced on both (the same
+    buckets on every rank)."""
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_grad_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         r = [torch.load(os.path.join(d, f"g{k}.pt"), weights_only=True) for k in range(2)]
@@ -165,9 +168,32 @@ def test_allreduce_gradients_world2_gloo():
         expect = []
         for rank in range(2):
             gen = torch.Generator().manual_seed(100 + rank)
-            expect.append([torch.randn(s, generator=gen) for s in ((300, 7), (11,), (5, 5, 5), (4096,))])
+            expect.append([torch.randn(s, generator=gen) for s in ((300, 7), (11,), (5, 5, 5), (4096,), (9,))])
         for i in (0, 2, 3):
             mean = (expect[0][i] + expect[1][i]) / 2
             assert torch.allclose(r[k]["grads"][i], mean, atol=1e-6)
         assert r[k]["grads"][1] is None
+        # used on rank 0 only: both ranks reduce it (zeros on rank 1) and hold the same mean
+        assert torch.allclose(r[k]["grads"][4], expect[0][4] / 2, atol=1e-6)
     assert all(torch.equal(a, b) for a, b in zip(r[0]["grads"][:1], r[1]["grads"][:1]))
+
+
+def test_missing_rank_fails_fast_not_hang():
+    """with a bounded timeout (init_distributed, what bench.py calls at N > 1) a run
+    whose second rank never arrives exits non-zero within the timeout instead of hanging."""
+    import subprocess
+    import sys
+    import time
+    port = _free_port()
+    code = ("import sys; sys.path[:0] = sys.argv[1:3]\n"
+            "from cat_seg.distributed import init_distributed\n"
+            "init_distributed('gloo', timeout_s=5)\n"
+            "print('joined')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="2")
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-c", code, os.path.join(root, "cat-seg_amd"), root], env=env,
+                       capture_output=True, text=True, timeout=120)
+    took = time.time() - t0
+    assert p.returncode != 0 and "joined" not in p.stdout
+    assert took < 60, took

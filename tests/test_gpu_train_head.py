@@ -334,3 +334,41 @@ def test_catseg_train_step_matches_reference_gradients():
             assert err <= max(TOL, 8 * e32), f"{k}: {err:.3e} (reference fp32 {e32:.3e})"
     finally:
         _write_report("reference_modules_train_step", sorted(rows, reverse=True))
+
+
+def test_hip_adamw_step_refreshes_the_eval_engine():
+    """the HIP AdamW (cat_seg.optim, as build_optimizer returns it) writes the parameters
+    through raw pointers; the eval forward after its step must run on the UPDATED weights (the engine is
+    keyed on the parameters' version counters), checked against the oracle on the new state dict."""
+    from cat_seg.optim import AdamW, build_optimizer
+    cfg = tiny_cfg(**{"SOLVER.CLIP_GRADIENTS.ENABLED": "True", "SOLVER.CLIP_GRADIENTS.CLIP_TYPE": "full_model",
+                      "SOLVER.CLIP_GRADIENTS.CLIP_VALUE": "0.01", "SOLVER.BASE_LR": "0.01"})
+    model = build_model(cfg).cuda()
+    T = 5
+    gen = torch.Generator().manual_seed(11)
+    toks = torch.zeros(T, 16, dtype=torch.long)
+    toks[:, 0] = 1
+    toks[:, 1:4] = torch.randint(2, 400, (T, 3), generator=gen)
+    toks[:, 4] = 511
+    model.sem_seg_head.predictor.set_class_tokens(toks)
+    ims = [torch.randint(0, 256, (3, 384, 384), generator=gen).float()]
+    sems = [torch.randint(0, T, (384, 384), generator=gen)]
+    model.eval()
+    with torch.no_grad():
+        out0 = model([{"image": ims[0]}])[0]["sem_seg"].clone()
+    opt = build_optimizer(cfg, model)
+    assert isinstance(opt, AdamW)
+    model.train()
+    model([{"image": i, "sem_seg": s} for i, s in zip(ims, sems)])["loss_sem_seg"].backward()
+    versions = [p._version for p in model.parameters()]
+    opt.step()
+    torch.cuda.synchronize()
+    assert any(p._version != v for p, v in zip(model.parameters(), versions))
+    model.eval()
+    with torch.no_grad():
+        out1 = model([{"image": ims[0]}])[0]["sem_seg"]
+    assert not torch.equal(out1, out0)
+    arch = model.arch
+    sd_new = {k: v.detach().cpu() for k, v in model.named_parameters()}
+    ref = O.catseg_forward(arch, sd_new, [{"image": ims[0]}], O.text_embeds(arch, sd_new, toks))[0]["sem_seg"]
+    assert (out1.cpu() - ref).abs().max().item() < 1e-3

@@ -67,6 +67,8 @@ def build_optimizer_groups(model, base_lr=2e-4, wd=1e-4, wd_norm=0.0, wd_embed=0
                 hp["lr"] *= 0.01
             if "clip_model" in module_name:
                 hp["lr"] *= clip_mult
+            if "relative_position_bias_table" in pname or "absolute_pos_embed" in pname:
+                hp["weight_decay"] = 0.0
             if isinstance(module, REF_NORM_TYPES):
                 hp["weight_decay"] = wd_norm
             if isinstance(module, torch.nn.Embedding):
@@ -153,6 +155,39 @@ def test_reference_build_optimizer_rules_apply():
     before = copy.deepcopy(dict(m.named_parameters())[agg + "head.bias"].detach())
     opt.step()
     assert not torch.equal(dict(m.named_parameters())[agg + "head.bias"].detach(), before)
+
+
+def test_sgd_full_model_clipping_and_position_table_decay():
+    """SOLVER.OPTIMIZER SGD gets the reference's FullModelGradientClippingOptimizer too
+    (train_net.py:228-256): its step equals clip_grad_norm_ over every parameter + torch SGD; and a
+    parameter named relative_position_bias_table / absolute_pos_embed gets weight decay 0
+    (train_net.py:216-221)."""
+    from cat_seg.optim import FullModelClipSGD, build_optimizer
+    cfg = tiny_cfg(**{"SOLVER.OPTIMIZER": "SGD", "SOLVER.CLIP_GRADIENTS.ENABLED": "True",
+                      "SOLVER.CLIP_GRADIENTS.CLIP_TYPE": "full_model", "SOLVER.CLIP_GRADIENTS.CLIP_VALUE": "0.01"})
+    m = build_model(cfg)
+    m.sem_seg_head.predictor.transformer.register_parameter("absolute_pos_embed", torch.nn.Parameter(torch.ones(4)))
+    opt = build_optimizer(cfg, m)
+    assert isinstance(opt, FullModelClipSGD) and opt.max_grad_norm == 0.01
+    pos = [g for g in opt.param_groups if g["params"][0].shape == (4,) and bool((g["params"][0] == 1).all())]
+    assert len(pos) == 1 and pos[0]["weight_decay"] == 0.0
+    m2 = copy.deepcopy(m)
+    params = [p for g in opt.param_groups for p in g["params"]]
+    torch.manual_seed(0)
+    for p in params:
+        p.grad = torch.randn_like(p)
+    name_of = {id(p): n for n, p in m.named_parameters()}
+    p2 = dict(m2.named_parameters())
+    ref_params = [p2[name_of[id(p)]] for p in params]
+    for p, q in zip(params, ref_params):
+        q.grad = p.grad.clone()
+    ref = torch.optim.SGD([{"params": [q], "lr": g["lr"], "weight_decay": g["weight_decay"]}
+                           for q, g in zip(ref_params, opt.param_groups)], cfg.SOLVER.BASE_LR, momentum=cfg.SOLVER.MOMENTUM)
+    torch.nn.utils.clip_grad_norm_(ref_params, 0.01)
+    ref.step()
+    opt.step()
+    for p, q in zip(params, ref_params):
+        assert torch.equal(p.detach(), q.detach())
 
 
 def test_custom_ops_are_registered_with_meta_kernels():

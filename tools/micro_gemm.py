@@ -17,7 +17,7 @@ variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").spli
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True),
-          "sq4k": (4096, 4096, L.ACT_NONE, False)}
+          "sq4k": (4096, 4096, L.ACT_NONE, False), "sq8k": (8192, 8192, L.ACT_NONE, False)}
 # MG_SHAPES=qkv,fc1,sq4k selects shapes (sq4k: M = N = K = 4096, the guide's reference size)
 sel = os.environ.get("MG_SHAPES", "qkv,proj,fc1,fc2").split(",")
 shapes = {k: v for k, v in shapes.items() if k in sel}
@@ -26,7 +26,7 @@ torch.manual_seed(0)
 lib = L.load()
 res = {}
 for name, (N, K, act, has_res) in shapes.items():
-    M = 4096 if name == "sq4k" else int(os.environ.get("MG_M", 8 * 577))   # MG_M=2308: config 4's 4 images
+    M = {"sq4k": 4096, "sq8k": 8192}.get(name, int(os.environ.get("MG_M", 8 * 577)))   # MG_M=2308: config 4's 4 images
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
     W = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
     bias = torch.rand(N, device=dev) - 0.5
@@ -82,6 +82,6 @@ for name, (N, K, act, has_res) in shapes.items():
     for v in variants:
         t = sorted(res[(name, v)]["t"])[3]
         print(f"{name:5s} N={N:5d} K={K:5d} variant {v:2d}: {t * 1e3:8.1f} us  {flops / t / 1e9:7.1f} TF/s  "
-              f"max_err {res[(name, v)]['err']:.3e}", flush=True)
+              f"({flops / t / 1e9 / 2500:.3f} of 2.5 PF)  max_err {res[(name, v)]['err']:.3e}", flush=True)
 L.tune("gemm_variant", 0)
 L.tune("gemm_group", 0)
