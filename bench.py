@@ -319,8 +319,9 @@ def boundary_pass(cfg, B, S, T, steps, warmup, engine_value):
     over the same steps as the engine leg.  Each call stages the host images through the model's reused
     pinned canvas (one H2D copy of the uint8 bytes, the fp32 conversion on the device), replays the
     forward's hipGraph and returns every image's probabilities as fresh device tensors."""
-    from cat_seg import build_model, get_cfg
+    from cat_seg import add_cat_seg_config, build_model, get_cfg
     c = get_cfg()
+    add_cat_seg_config(c)
     c.merge_from_file(os.path.join(ROOT, "cat-seg_amd", "configs", "vitl_336.yaml"))
     c.merge_from_list(["MODEL.SEM_SEG_HEAD.POOLING_SIZES", "[1,1]", "MODEL.CATSEG_HIP.DTYPE", "bf16"])
     model = build_model(c).cuda().eval()

@@ -257,9 +257,12 @@ class CATSeg(nn.Module):
     def _stage_canvas(self, eng: CatSegEngine, images: List[torch.Tensor], canvas: torch.Tensor) -> None:
         """Write the images into the zero-padded fp32 device canvas (ImageList.from_tensors geometry;
         the padding stays zero: every call of one geometry writes the same regions).  Host images go
-        through ONE pinned canvas of their own dtype (uint8 from detectron2's mappers: 4x fewer bytes
-        than fp32) and one async H2D copy, reused across calls (an event keeps the next call from
-        rewriting it while its copy is in flight); the dtype conversion runs on the device."""
+        through pinned staging canvases of their own dtype (uint8 from detectron2's mappers: 4x fewer
+        bytes than fp32), reused across calls in two slots: the H2D copy runs on a copy stream, so it
+        overlaps the previous call's forward still running on the compute stream, and events order
+        the slot's reuse (host slot rewritten after its copy finished; device slot refilled after the
+        previous conversion out of it ran); the dtype conversion runs on the device."""
+        cur = torch.cuda.current_stream(canvas.device)
         if all(i.is_cuda for i in images):
             for k, im in enumerate(images):
                 canvas[k, :, : im.shape[-2], : im.shape[-1]].copy_(im)
@@ -268,19 +271,29 @@ class CATSeg(nn.Module):
         key = (tuple(canvas.shape), dt, canvas.device)
         st = self._stage.get(key)
         if st is None:
-            st = {"host": torch.zeros(canvas.shape, dtype=dt, pin_memory=True),
-                  "dev": torch.zeros(canvas.shape, dtype=dt, device=canvas.device), "ev": None}
+            st = {"slots": [{"host": torch.zeros(canvas.shape, dtype=dt, pin_memory=True),
+                             "dev": torch.zeros(canvas.shape, dtype=dt, device=canvas.device),
+                             "copied": None, "used": None} for _ in range(2)],
+                  "next": 0, "stream": torch.cuda.Stream(device=canvas.device)}
             self._stage[key] = st
-        if st["ev"] is not None:
-            st["ev"].synchronize()             # the previous call's H2D has read the pinned canvas
-        host = st["host"]
+        slot = st["slots"][st["next"]]
+        st["next"] ^= 1
+        if slot["copied"] is not None:
+            slot["copied"].synchronize()       # this slot's previous H2D has read the pinned canvas
+        host = slot["host"]
         for k, im in enumerate(images):
             host[k, :, : im.shape[-2], : im.shape[-1]].copy_(im)
-        st["dev"].copy_(host, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        st["ev"] = ev
-        canvas.copy_(st["dev"])                # device-side dtype conversion
+        cs = st["stream"]
+        if slot["used"] is not None:
+            cs.wait_event(slot["used"])        # the previous conversion out of this device slot ran
+        with torch.cuda.stream(cs):
+            slot["dev"].copy_(host, non_blocking=True)
+            slot["copied"] = torch.cuda.Event()
+            slot["copied"].record(cs)
+        cur.wait_event(slot["copied"])
+        canvas.copy_(slot["dev"])              # device-side dtype conversion
+        slot["used"] = torch.cuda.Event()
+        slot["used"].record(cur)
 
     def _canvas_geometry(self, images: List[torch.Tensor]):
         d = max(self.size_divisibility, 1)
@@ -290,16 +303,15 @@ class CATSeg(nn.Module):
 
     def _forward_graph(self, eng: CatSegEngine, batched_inputs: List[dict]):
         """The eval forward as one hipGraph replay per input geometry (what bench.py times): the
-        first call of a geometry captures engine.head_logits + the postprocess into static buffers,
-        every call stages its images into the captured canvas and replays.  Outputs are returned as
-        fresh tensors (a device copy of the static ones), as the eager path returns them."""
+        first call of a geometry captures engine.head_logits, every call stages its images into the
+        captured canvas, replays, and resizes the captured logits into fresh output tensors."""
         images = [x["image"] for x in batched_inputs]
         H, W = self._canvas_geometry(images)
         sizes = tuple((int(i.shape[-2]), int(i.shape[-1])) for i in images)
         n = len(batched_inputs) if self.return_all_images else 1
         outs = tuple((int(batched_inputs[i].get("height", sizes[i][0])), int(batched_inputs[i].get("width", sizes[i][1])))
                      for i in range(n))
-        key = (id(eng), id(eng._text), len(images), H, W, sizes, outs)
+        key = (id(eng), id(eng._text), len(images), H, W, sizes)
         g = self._graphs.get(key)
         dev = eng.device
         if g is None:
@@ -308,30 +320,36 @@ class CATSeg(nn.Module):
             stream = torch.cuda.Stream(device=dev)
             stream.wait_stream(torch.cuda.current_stream(dev))
 
-            def body():
-                logits = eng.head_logits(raw, sizes_dev)
-                h_l, w_l = logits.shape[-2:]
-                res = []
-                for i in range(n):
-                    out = torch.empty(1, logits.shape[1], outs[i][0], outs[i][1], device=dev)
-                    ops.postprocess(logits[i:i + 1], out, crop=(min(h_l, sizes[i][0]), min(w_l, sizes[i][1])))
-                    res.append(out)
-                return res
             with torch.cuda.stream(stream):
-                body()                          # warm the allocator outside the capture
+                eng.head_logits(raw, sizes_dev)  # warm the allocator outside the capture
             torch.cuda.current_stream(dev).wait_stream(stream)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
-                static_out = body()
-            # the graph replays raw device pointers: hold the engine and its class-set buffers
-            # (ids in the key stay unique while referenced); keep the 4 newest geometries
-            g = {"graph": graph, "raw": raw, "out": static_out, "refs": (eng, eng._text)}
+                logits = eng.head_logits(raw, sizes_dev)
+            # the graph replays raw device pointers: hold every tensor it reads that was allocated
+            # outside the capture (the canvas, the sizes), the engine and its class-set buffers (ids in
+            # the key stay unique while referenced); keep the 4 newest geometries
+            g = {"graph": graph, "raw": raw, "sizes": sizes_dev, "logits": logits, "refs": (eng, eng._text)}
             while len(self._graphs) >= 4:
                 self._graphs.pop(next(iter(self._graphs)))
             self._graphs[key] = g
         self._stage_canvas(eng, images, g["raw"])
         g["graph"].replay()
-        return [{"sem_seg": o[0].clone()} for o in g["out"]]
+        # the resize to each image's output size runs after the replay into FRESH tensors (the caller
+        # may keep the results across calls), as the eager path does
+        logits = g["logits"]
+        h_l, w_l = logits.shape[-2:]
+        if n > 1 and len(set(outs)) == 1 and len(set(sizes[:n])) == 1:
+            # one launch for the whole batch (the engine leg's form); each result is a view of it
+            out = torch.empty(n, logits.shape[1], outs[0][0], outs[0][1], device=dev)
+            ops.postprocess(logits[:n], out, crop=(min(h_l, sizes[0][0]), min(w_l, sizes[0][1])))
+            return [{"sem_seg": out[i]} for i in range(n)]
+        results = []
+        for i in range(n):
+            out = torch.empty(1, logits.shape[1], outs[i][0], outs[i][1], device=dev)
+            ops.postprocess(logits[i:i + 1], out, crop=(min(h_l, sizes[i][0]), min(w_l, sizes[i][1])))
+            results.append({"sem_seg": out[0]})
+        return results
 
     def forward(self, batched_inputs: List[dict]):
         if self.training:

@@ -438,6 +438,7 @@ struct Swz {
 // bias loaded once (same box, M = 4616: out-proj 20.8 -> 19.9 us, fc1 55.1 -> 52.7, fc2 48.3 -> 47.1;
 // bit-identical); 0 = one residual round trip per epilogue round
 int g_epi_prefetch = 1;
+int g_wide_epi = 1;   // gemm6 bf16 outputs: 1 = register-side epilogue (wide_epilogue_bf16), 0 = fp32 LDS staging
 template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false,
           int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __restrict__ A, int64_t lda, RowMap amap,
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
   constexpr bool ONE = IPT >= 1 && IPT <= 2 && ROWS * (BN / 8) == IPT * NT3 && NT3 % (BN / 8) == 0 && EPI != 0 &&
                        !SC;
   if constexpr (ONE) {
-    if (e.pf) {
+    if (e.pf & 1) {
       const int c8 = (tid % (BN / 8)) * 8;
       const int64_t n = n0 + c8;
       float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -737,7 +738,7 @@ DEV void wide_tile(int wg, int64_t M, int BM, int tiles_n, int group_m, int& tm_
 template <typename TO, int BM, int BN, int EPI, int FM, int FN>
 DEV void wide_epilogue(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, int64_t M, int64_t m0, int64_t n0) {
   constexpr int NT4 = 512, WGM = 2, WM = BM / WGM, WN = BN / 4;
-  constexpr int JR = 2, ROWS = WGM * JR * 16, SLD = BN + 4;
+  constexpr int JR = FM % 2 == 0 ? 2 : 1, ROWS = WGM * JR * 16, SLD = BN + 4;
   static_assert(FM % JR == 0, "epilogue rounds");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wmi = wave / 4, wn = (wave % 4) * WN;
@@ -799,6 +800,70 @@ DEV void wide_epilogue(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, int64
         store8f(reinterpret_cast<TO*>(e.out) + mk[k] * e.ldo + n0 + c8[k], v);
       }
     }
+  }
+}
+
+// Register-side epilogue of the wide kernels for bf16 outputs without a residual (QKV: bias; fc1:
+// bias + QuickGELU).  The bias (4 columns per n-fragment, fixed per lane) and the activation are
+// applied on the accumulators in registers; the bf16 values go through LDS in TWO rounds of half the
+// tile's rows (both wave rows' m-fragments 0..FM/2-1, then the rest), 8-byte writes into rows of
+// BN + 8 elements (a row stride = 16 B mod 256: the 16 rows of a write group hit 16 distinct 16-B
+// slots), and leave as whole-row 16-byte stores.  Against wide_epilogue: 4 instead of 10 barriers and
+// half the LDS bytes (bf16 instead of fp32 staging); the arithmetic of an output is the same
+// expression (acc + bias, then the activation, then one rounding).
+template <int BM, int BN, int EPI, int FM, int FN>
+DEV void wide_epilogue_bf16(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, int64_t M, int64_t m0, int64_t n0) {
+  constexpr int NT4 = 512, WM = BM / 2, WN = BN / 4, SR = BN + 8;
+  constexpr int FH = FM / 2, ROWS = 2 * FH * 16;                 // rows staged per round
+  static_assert(FM % 2 == 0, "two rounds");
+  static_assert(ROWS * SR * 2 <= 160 * 1024, "staging exceeds LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wmi = wave / 4, wn = (wave % 4) * WN;
+  const int col = lane & 15, q = lane >> 4;
+  float bias[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    if (e.bias) {
+      const float4 b = *reinterpret_cast<const float4*>(e.bias + n0 + wn + 16 * i + 4 * q);
+      bias[i][0] = b.x; bias[i][1] = b.y; bias[i][2] = b.z; bias[i][3] = b.w;
+    } else {
+      bias[i][0] = bias[i][1] = bias[i][2] = bias[i][3] = 0.f;
+    }
+  }
+  constexpr int CG = BN / 8, ITEMS = ROWS * CG, IPT = (ITEMS + NT4 - 1) / NT4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < FH; ++jj)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const f32x4 a = acc[i][h * FH + jj];
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = a[r] + bias[i][r];
+          if constexpr (EPI == 2) v[r] = apply_act(v[r], ACT_QUICKGELU);
+        }
+        const int lrow = (wmi * FH + jj) * 16 + col;
+        *reinterpret_cast<uint2*>(&smem[lrow * SR + wn + 16 * i + 4 * q]) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+      }
+    __syncthreads();
+    uint4 val[IPT];
+    int64_t mr[IPT];
+    int cc[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int idx = min(tid + k * NT4, ITEMS - 1);
+      const int lrow = idx / CG, c8 = (idx % CG) * 8;
+      const int wi = lrow / (FH * 16), rr = lrow % (FH * 16);
+      mr[k] = m0 + wi * WM + h * FH * 16 + rr;
+      cc[k] = c8;
+      val[k] = *reinterpret_cast<const uint4*>(&smem[lrow * SR + c8]);
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k)
+      if (tid + k * NT4 < ITEMS && mr[k] < M) st16(reinterpret_cast<bf16*>(e.out) + mr[k] * e.ldo + n0 + cc[k], val[k]);
   }
 }
 
@@ -1093,6 +1158,140 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const bf16* __restrict__ A, 
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
+  if constexpr (ABL == 3) {   // ablation: no epilogue (the accumulators kept live)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
+  if constexpr (sizeof(TO) == 2) {
+    if ((e.pf & 2) && !(EPI == 1 && e.res)) {
+      wide_epilogue_bf16<BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
+      return;
+    }
+  }
+  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
+}
+
+// gemm7: REGISTER-prefetched staging for the narrow-N ViT GEMMs (out-proj, fc2: N = 1024, where a
+// one-round tile is at most ~160 x 128 and the per-CU fill -- (BM + BN) x K x 2 bytes, 2.36 MB per
+// CU for fc2 -- bounds the kernel).  The LDS-DMA ring holds at most one to three 36 KB stages in
+// flight in LDS; here each thread keeps the next D stages' chunks in VGPRs (D x 5 x 16 B: the 8-wave
+// 160 x 128 tile leaves ~150 VGPRs free), so D x 36 KB are in flight per CU beside a 2-slot LDS
+// double buffer, with full 128-B lines per row (8 lanes per row segment) and one cheap
+// global_load_dwordx4 per chunk instead of an LDS-DMA issue.  Per K-step k (BK = 64): wait for the
+// registers of stage k + 1 (counted vmcnt, D - 1 stages stay in flight), write them to LDS slot
+// (k + 1) % 2 (swizzled like gemm3: chunk c of row r at c ^ ((r / 2) % 8)), reload that register
+// slot with stage k + 1 + D, MFMA on slot k % 2, barrier.  Same MFMA and k order as gemm3.
+template <typename TO, int BM, int BN, int D, int EPI>
+__global__ __launch_bounds__(512) void gemm7_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
+                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
+                                                    int group_m) {
+  constexpr int NT = 512, BK = 64, BKC = 8, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
+  constexpr int STAGE = (BM + BN) * BK, CH = (BM + BN) * BKC, NL = (CH + NT - 1) / NT;
+  static_assert(NL == 5, "the wait statements name five destinations");
+  static_assert(D == 2 || D == 4, "register slots: the host checks K / 64 % D == 0");
+  using SW = Swz<64>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tm_i, tn_i;
+  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int wm = (wave / 4) * WM, wn = (wave % 4) * WN;
+
+  // Every thread issues NL loads per stage (uniform counts: one wait statement, no branches between
+  // a load and its wait); a chunk index past the stage re-loads chunk c - NT into the same LDS
+  // slot as its owner (identical bytes, a benign duplicate write).
+  const bf16* src[NL];
+  int ldo[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int c = tid + i * NT;
+    if (c >= CH) c -= NT;
+    const int row = c / BKC, ch = c % BKC;
+    if (row < BM) src[i] = A + min<int64_t>(m0 + row, M - 1) * lda + ch * 8;
+    else src[i] = W + (n0 + row - BM) * ldw + ch * 8;
+    ldo[i] = (row * BKC + SW::slot(row, ch)) * 8;
+  }
+  // The prefetch loads are inline asm: hipcc's waitcnt pass would drain every older load (vmcnt(0))
+  // before the first LDS write of a register slot, collapsing the D-stage prefetch to one.  Their
+  // completion is counted here: the wait statement names the slot's five destinations "+v" (form
+  // (ii) of cdna_hip_programming.md §5.7), and the steady-state loop has no branch between a load and
+  // its wait (the ISA carries no copy of a slot register in between: tests/test_isa_lint_cpu.py R4).
+  i32x4 R[D][NL];
+  const int klast = (int)(K / BK) - 1;
+  auto gload = [&](i32x4 (&r)[NL], int kt) {
+    const int64_t k0 = (int64_t)min(kt, klast) * BK;      // past the end: a harmless re-load
+#pragma unroll
+    for (int i = 0; i < NL; ++i) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[i]) : "v"(src[i] + k0) : "memory");
+  };
+  auto lstore = [&](const i32x4 (&r)[NL], int buf) {
+    bf16* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) *reinterpret_cast<i32x4*>(st + ldo[i]) = r[i];
+  };
+  auto wait_slot = [&](auto n_c, i32x4 (&r)[NL]) {      // at most N younger stages still in flight
+    constexpr int N = decltype(n_c)::value;
+    asm volatile("s_waitcnt vmcnt(%5)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) : "i"(N * NL) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, q = lane >> 4;
+  const int fo0 = r16 * BK + ((q ^ ((r16 >> 1) & 7)) * 8), fo1 = r16 * BK + (((4 + q) ^ ((r16 >> 1) & 7)) * 8);
+  const int ktiles = klast + 1;
+
+  // prologue: stages 0 .. D - 1 into the register slots; stage 0 to LDS slot 0; stage D into slot 0
+#pragma unroll
+  for (int d = 0; d < D; ++d) gload(R[d], d);
+  wait_slot(std::integral_constant<int, D - 1>{}, R[0]);
+  lstore(R[0], 0);
+  gload(R[0], D);
+  __syncthreads();
+
+  auto compute = [&](int buf) {
+    const bf16* As = smem + buf * STAGE;
+    const bf16* Ws = As + BM * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      s16x8 bfrag[FM], afrag[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + (h ? fo1 : fo0)]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + (h ? fo1 : fo0)]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
+    }
+  };
+  // K-step k with register slot S1 = (k + 1) % D holding stage k + 1 (in flight since step k + 1 - D);
+  // after the step the slot is reloaded with stage k + 1 + D.  At the last step the slot's data is a
+  // re-load nobody reads; the LDS write of it lands in the slot no later step reads.
+  auto step = [&](int k, auto s1_c) {
+    constexpr int S1 = decltype(s1_c)::value;
+    wait_slot(std::integral_constant<int, D - 1>{}, R[S1]);
+    lstore(R[S1], (k + 1) & 1);
+    gload(R[S1], k + 1 + D);
+    compute(k & 1);
+    __syncthreads();
+  };
+  for (int k = 0; k < ktiles; k += D) {
+    step(k, std::integral_constant<int, 1 % D>{});
+    step(k + 1, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 2) {
+      step(k + 2, std::integral_constant<int, 3 % D>{});
+      step(k + 3, std::integral_constant<int, 4 % D>{});
+    }
+  }
+  // drain the trailing re-loads before their registers can be reused
+#pragma unroll
+  for (int d = 0; d < D; ++d) wait_slot(std::integral_constant<int, 0>{}, R[d]);
   wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
 }
 
@@ -1109,11 +1308,24 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
   e.cvt_cout = g->cvt_cout;
   e.sa = nullptr; e.sw = nullptr;
-  e.pf = g_epi_prefetch;
+  e.pf = g_epi_prefetch | (g_wide_epi ? 2 : 0);
   return e;
 }
 
 int g_gemm4_group = 5;   // gemm4 tile order: G m-tiles per group (catseg_set_gemm4_group)
+
+template <typename TO, int BM, int BN, int D, int EPI>
+bool launch7(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->N % BN != 0 || g->K % 64 != 0 || (g->K / 64) % D != 0) return false;
+  const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
+  if (!ident) return false;
+  const EpiArgs e = make_epi(g);
+  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
+  auto kern = gemm7_kernel<TO, BM, BN, D, EPI>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A, g->lda, (const bf16*)g->W,
+                     g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm_group));
+  return true;
+}
 
 // KIND 4 = gemm4 (plain K-loop), 5 = gemm5 (ping-pong)
 template <typename TO, int BM, int BN, int S, int EPI, int KIND = 5, int ABL = 0>
@@ -1188,12 +1400,21 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     // (Earlier measurements: deeper rings S = 3 / 4 slower on fc2; a one-round 320x256 fc1 tile
     // 58.4 us vs 54.5; 288x256 102 us.)  The tile never changes the arithmetic: every variant
     // accumulates the full K of an output in the same k order.
+    // The ping-pong wide tiles (gemm6, v 50 / 51) need an identity A map and 32-bit buffer offsets.
+    // (round 6, tools/micro_gemm.py, one box: fc1 41.2 us vs 47.3 for 160x128 two per CU, QKV 31.4
+    // vs 33.3 for 224x256; weights from those ratios)
     struct Cand { int v, bm, bn, slots, bk; float w; };
     static const Cand cands[] = {{20, 224, 256, 1, 64, 1.0f}, {1, 256, 256, 1, 64, 0.95f}, {15, 160, 128, 1, 128, 0.95f},
-                                 {17, 160, 128, 2, 64, 0.9f}, {19, 128, 128, 2, 64, 0.85f}, {24, 96, 128, 1, 128, 0.85f}};
+                                 {17, 160, 128, 2, 64, 0.9f}, {19, 128, 128, 2, 64, 0.85f}, {24, 96, 128, 1, 128, 0.85f},
+                                 {50, 320, 256, 1, 64, 1.1f}, {51, 320, 192, 1, 64, 1.1f}};
+    const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
+    const bool lean = !g->add && !g->res2 && g->alpha == 1.f &&
+                      (g->act == ACT_NONE || (g->act == ACT_QUICKGELU && !g->res)) && g->store_mode == 0;
+    const bool wide_ok = ident && lean && g->M * g->lda * 2 < 0x7fffffffLL && g->N * g->ldw * 2 < 0x7fffffffLL;
     float best = 0.f;
     for (const Cand& c : cands) {
       if (g->N % c.bn != 0 || g->K % c.bk != 0) continue;
+      if (c.v >= 50 && !wide_ok) continue;
       const int64_t tiles = ((g->M + c.bm - 1) / c.bm) * (g->N / c.bn), slots = 256LL * c.slots;
       const int64_t rounds = (tiles + slots - 1) / slots;
       const float score = (float)tiles / (float)(rounds * slots) * c.w / (1.f + 0.15f * (float)(rounds - 1));
@@ -1226,7 +1447,7 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 2 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 2>(g, st);
   if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
   // wide tiles (lean epilogues only): 30-33 gemm4, 40-45 gemm5 (ping-pong)
-  if (v >= 30 && v < 60 && (epi == 1 || epi == 2)) {
+  if (v >= 30 && v < 70 && (epi == 1 || epi == 2)) {
     const bool e1 = epi == 1;
     switch (v) {
       case 30: return e1 ? launch4<TO, 320, 256, 4, 1, 4>(g, st) : launch4<TO, 320, 256, 4, 2, 4>(g, st);
@@ -1245,6 +1466,12 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
       case 52: return e1 ? launch4<TO, 256, 256, 2, 1, 6>(g, st) : launch4<TO, 256, 256, 2, 2, 6>(g, st);
       case 56: return launch4<TO, 256, 256, 2, 1, 6, 1>(g, st);   // ablation: no LDS-DMA (wrong output)
       case 57: return launch4<TO, 256, 256, 2, 1, 6, 2>(g, st);   // ablation: no MFMA (wrong output)
+      // gemm7 (register-prefetched staging)
+      case 62: return e1 ? launch7<TO, 160, 128, 2, 1>(g, st) : launch7<TO, 160, 128, 2, 2>(g, st);
+      case 63: return e1 ? launch7<TO, 160, 128, 4, 1>(g, st) : launch7<TO, 160, 128, 4, 2>(g, st);
+      case 58: return launch4<TO, 320, 256, 2, 2, 6, 1>(g, st);   // fc1 tile ablations (wrong output)
+      case 59: return launch4<TO, 320, 256, 2, 2, 6, 2>(g, st);
+      case 60: return launch4<TO, 320, 256, 2, 2, 6, 3>(g, st);
       default: return false;
     }
   }
@@ -1356,6 +1583,7 @@ CATSEG_KNOB(g_gemm_variant, "gemm_variant");
 CATSEG_KNOB(g_gemm_group, "gemm_group");
 CATSEG_KNOB(g_gemm4_group, "gemm4_group");
 CATSEG_KNOB(g_epi_prefetch, "epi_prefetch");
+CATSEG_KNOB(g_wide_epi, "wide_epi");
 CATSEG_KNOB(g_gemm_f8_variant, "gemm_fp8_variant");
 
 extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {

@@ -41,6 +41,9 @@ for name, (N, K, act, has_res) in shapes.items():
     def run():
         ops.gemm(A, W, out, bias=bias, act=act, res=R)
     def setv(v):
+        # 5000 + x: variant 2000 + x with the wide kernels' fp32-staged epilogue (tuning knob wide_epi 0)
+        L.tune("wide_epi", 0 if v >= 5000 else 1)
+        v = v - 3000 if v >= 5000 else v
         pf = v >= 2000                 # 2000 + v: variant v with the prefetching lean epilogue (epi_prefetch 1,
                                        # the library default); v < 2000 runs with epi_prefetch 0;
                                        # 3000 + g = 2000 + (1000 + g): the automatic tile, prefetching
