@@ -695,22 +695,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
 }
 
 // ------------------------------------------------------------------------------------
-// Wide tiles for the ViT GEMMs: BM = 320 (or 256) rows x BN = 256 / 192 columns, one 8-wave
+// Wide tiles for the ViT GEMMs (gemm6): BM = 320 rows x BN = 256 / 192 columns, one 8-wave
 // workgroup per CU.  At M = 4616 the 320-row tiles make ONE round on 240 CUs for fc1 (15 x 16 at
-// BN 256) and QKV (15 x 16 at BN 192), with half of gemm3's L2 -> LDS bytes per FLOP (142 FLOP
-// per byte at 320 x 256 vs 71 at 160 x 128).
-//   * ring: S stages of BK = 32 (64 bytes per row), filled by LDS-DMA (16 B per lane, lane-linear
-//     1 KB per wave-instruction = 16 rows); wave w issues instructions w, w + 8, ... of a stage
-//     (5 or 4 of the 36 of a 320 + 256 stage), counted per wave in vmcnt;
-//   * swizzle: the 16-byte chunk c of row r sits at slot c ^ g[(r >> 2) & 3], g = {0, 2, 3, 1}:
-//     the four lane groups of a ds_read_b128 fragment read (rows 0-15, chunk = lane >> 4) hit 16
-//     distinct bank slots each (tools/lds_bank_model.py), and the DMA writes are linear;
-//   * 8 waves as 2 (m) x 4 (n), a (BM / 2) x (BN / 4) wave tile: 160 x 64 = 14 fragment reads per
-//     40 MFMAs, 160 accumulator VGPRs;
-//   * epilogue through LDS in rounds of 64 rows (coalesced 16-byte stores of whole rows).
-// gemm4 is the plain K-loop (one barrier per K-step, all waves in step); gemm5 the ping-pong form.
-// Arithmetic per output = gemm3's (the same MFMA over the same k order, the same epilogue
-// expression), so the tile choice never changes a bit (batch invariance).
+// BN 256) and QKV (15 x 16 at BN 192), with half of gemm3's L2 -> LDS bytes per FLOP (142 FLOP per
+// byte at 320 x 256 vs 71 at 160 x 128): 8 waves as 2 (m) x 4 (n), a 160 x 64 (48) wave tile = 14
+// (13) fragment reads per 40 (30) MFMAs per k32, 160 (120) accumulator VGPRs.  Arithmetic per
+// output = gemm3's (the same MFMA over the same k order, the same epilogue expression), so the tile
+// choice never changes a bit (batch invariance).  Round-6 forms measured and removed (DESIGN.md
+// §11): BK = 32 stages (16 rows x 64 B per DMA instruction), in step or ping-pong; a register-
+// prefetched 160 x 128 tile for the narrow-N GEMMs.
 // ------------------------------------------------------------------------------------
 // 16-byte LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds): base and size are wave-
 // uniform, the lane's part is a 32-bit byte offset, `soff` a uniform byte offset (SGPR)
@@ -867,186 +860,15 @@ DEV void wide_epilogue_bf16(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, 
   }
 }
 
-// DMA plan of a wide stage: instruction i = wave + 8 j covers stage rows 16 i .. 16 i + 15 (A rows
-// first, then W rows); lane -> row 16 i + lane / 4, physical slot lane % 4, which holds logical
-// chunk (lane % 4) ^ g(row).  Rows past M read row M - 1 (masked in the epilogue).
-template <int BM, int BN>
-struct WideDma {
-  static constexpr int BK = 32, STAGE = (BM + BN) * BK, NI = (BM + BN) / 16, JMAX = (NI + 7) / 8;
-  static_assert(BM % 16 == 0 && BN % 16 == 0, "rows per DMA instruction");
-  const bf16* src[JMAX];
-  bool full;                                   // this wave issues JMAX instructions per stage (else JMAX - 1)
-  DEV WideDma(const bf16* A, int64_t lda, const bf16* W, int64_t ldw, int64_t M, int64_t m0, int64_t n0, int wave,
-              int lane) {
-    full = (wave + 8 * (JMAX - 1)) < NI;
-    const int dch = (lane & 3) ^ swz4(lane >> 2);
-#pragma unroll
-    for (int j = 0; j < JMAX; ++j) {
-      const int i = min(wave + 8 * j, NI - 1);
-      const int row = 16 * i + (lane >> 2);
-      if (row < BM) {
-        const int64_t m = min<int64_t>(m0 + row, M - 1);
-        src[j] = A + m * lda + dch * 8;
-      } else {
-        src[j] = W + (n0 + row - BM) * ldw + dch * 8;
-      }
-    }
-  }
-  DEV void issue(bf16* stage, int64_t k0, int wave) const {
-#pragma unroll
-    for (int j = 0; j < JMAX; ++j)
-      if (j < JMAX - 1 || full)
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[j] + k0), (lds_void_t*)(stage + (wave + 8 * j) * 512), 16, 0, 0);
-  }
-  // wait until at most `tiles` younger stages of this wave's DMA are outstanding
-  template <int TILES>
-  DEV void wait() const {
-    if (full) wait_vmcnt<TILES * JMAX>();
-    else wait_vmcnt<TILES * (JMAX - 1)>();
-  }
-};
-
-template <typename TO, int BM, int BN, int S, int EPI>
-__global__ __launch_bounds__(512) void gemm4_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
-                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
-                                                    int group_m) {
-  constexpr int BK = 32, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
-  using D = WideDma<BM, BN>;
-  __shared__ __attribute__((aligned(16))) bf16 smem[S * D::STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int tm_i, tn_i;
-  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
-  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
-  const int wm = (wave / 4) * WM, wn = (wave % 4) * WN;
-  const D dma(A, lda, W, ldw, M, m0, n0, wave, lane);
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int r16 = lane & 15;
-  const int foff = r16 * BK + (((lane >> 4) ^ swz4(r16)) * 8);
-  const int ktiles = (int)(K / BK);
-#pragma unroll
-  for (int t = 0; t < S - 1; ++t)
-    if (t < ktiles) dma.issue(smem + t * D::STAGE, (int64_t)t * BK, wave);
-  for (int kt = 0; kt < ktiles; ++kt) {
-    if (kt + S - 2 < ktiles) dma.template wait<S - 2>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();                 // stage kt visible; stage (kt - 1) % S free
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + S - 1 < ktiles) dma.issue(smem + ((kt + S - 1) % S) * D::STAGE, (int64_t)(kt + S - 1) * BK, wave);
-    const bf16* As = smem + (kt % S) * D::STAGE;
-    const bf16* Ws = As + BM * BK;
-    s16x8 bfrag[FM], afrag[FN];
-#pragma unroll
-    for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + foff]);
-#pragma unroll
-    for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + foff]);
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-      for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
-  }
-  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
-}
-
-// gemm5: the same tile as a PING-PONG loop (cdna_hip_programming.md §5, the staggered 8-wave
-// template).  Waves w and w + 4 share a SIMD; the waves of the second m-half (group 1 = waves 4-7)
-// run one barrier behind group 0, so between any two barriers one group issues its K-step's
-// fragment reads, LDS-DMA and counted waits (the LOAD segment) while the other issues its MFMAs
-// (the COMPUTE segment): each SIMD's matrix pipe is fed by one wave while its partner loads.
-// Per K-step t a wave: LOAD(t) = read all fragments of stage t, issue the DMA of stage t + S - 1
-// (into the slot of stage t - 1, whose reads every wave retired before the previous barrier),
-// lgkmcnt(0), wait its own DMA of stage t + 1, barrier; COMPUTE(t) = FM x FN MFMAs, barrier.
-// Barrier #k (B0 = the prologue's): group 0's LOAD(t) ends at #2t+1, COMPUTE(t) at #2t+2; group 1's
-// at #2t+2 / #2t+3.  RAW: stage t + 1 is read after #2t+2 (group 0) / #2t+3 (group 1), and every
-// wave waited its DMA of t + 1 before #2t+2.  WAR: stage t - 1's slot is refilled in LOAD(t), after
-// #2t (group 0) / #2t+1 (group 1); the last reads of t - 1 (group 1's LOAD(t - 1)) retired before #2t.
-template <typename TO, int BM, int BN, int S, int EPI, int ABL = 0>
-__global__ __launch_bounds__(512) void gemm5_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
-                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
-                                                    int group_m) {
-  constexpr int BK = 32, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
-  static_assert(S >= 3, "the ping-pong ring needs a stage beyond the two being read");
-  using D = WideDma<BM, BN>;
-  __shared__ __attribute__((aligned(16))) bf16 smem[S * D::STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // wave-uniform group (scalar branch for the stagger barrier)
-  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;
-  int tm_i, tn_i;
-  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
-  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
-  const int wm = grp * WM, wn = (wave % 4) * WN;
-  const D dma(A, lda, W, ldw, M, m0, n0, wave, lane);
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int r16 = lane & 15;
-  const int foff = r16 * BK + (((lane >> 4) ^ swz4(r16)) * 8);
-  const int ktiles = (int)(K / BK);
-#pragma unroll
-  for (int t = 0; t < S - 1; ++t)
-    if (t < ktiles) dma.issue(smem + t * D::STAGE, (int64_t)t * BK, wave);
-  if (S - 1 <= ktiles) dma.template wait<S - 2>();     // own stage 0 landed
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();                        // B0: stage 0 visible
-  if (grp == 1) __builtin_amdgcn_s_barrier();          // the stagger
-  __builtin_amdgcn_sched_barrier(0);
-  for (int kt = 0; kt < ktiles; ++kt) {
-    // ---- LOAD(kt) ----
-    const bf16* As = smem + (kt % S) * D::STAGE;
-    const bf16* Ws = As + BM * BK;
-    s16x8 bfrag[FM], afrag[FN];
-#pragma unroll
-    for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + foff]);
-#pragma unroll
-    for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + foff]);
-    if (ABL != 1 && kt + S - 1 < ktiles) dma.issue(smem + ((kt + S - 1) % S) * D::STAGE, (int64_t)(kt + S - 1) * BK, wave);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (ABL == 1) {
-    } else if (kt + S - 1 < ktiles) {
-      dma.template wait<S - 2>();   // own stage kt + 1 landed (kt + 2 .. kt + S - 1 in flight)
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- COMPUTE(kt) ----
-    __builtin_amdgcn_s_setprio(1);
-    if constexpr (ABL == 2) {
-      // ablation: no MFMAs (keep the fragments live)
-#pragma unroll
-      for (int j = 0; j < FM; ++j) asm volatile("" :: "v"(bfrag[j]));
-#pragma unroll
-      for (int i = 0; i < FN; ++i) asm volatile("" :: "v"(afrag[i]));
-    } else {
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-#pragma unroll
-        for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
-  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
-}
-
-// gemm6: gemm5's ping-pong with FULL-LINE staging.  The ablations of gemm5 at 8192^3 (256 x 256)
-// show the fill, not the MFMA loop, is its bound: without the LDS-DMA the loop runs at 0.71 of the
-// dense peak, without the MFMAs the loads alone take 724 of the 893 us.  gemm5's DMA moves 16 rows x
-// 64 B per wave-instruction (BK = 32: half a 128-B line per row), the fragment-shaped pattern the
-// guide prices at twice the TA work of whole lines.  gemm6 stages BK = 64 (8 rows x 128 B per
-// instruction) into S = 2 slots (2 x (BM + BN) x 128 B of LDS) and runs each K64 tile as two k32
-// phases, so the per-wave fragment registers stay those of one k32 step.
+// gemm6: the wide tile as a PING-PONG loop (cdna_hip_programming.md §5, the staggered 8-wave
+// template) with FULL-LINE staging.  Waves w and w + 4 share a SIMD; the waves of the second m-half
+// (group 1 = waves 4-7) run one barrier behind group 0, so between any two barriers one group issues
+// its fragment reads, LDS-DMA and counted waits (LOAD) while the other issues MFMAs (COMPUTE): each
+// SIMD's matrix pipe is fed by one wave while its partner loads.  The stages are BK = 64 (each DMA
+// wave-instruction moves 8 rows x 128 B, whole lines; the BK = 32 form's 16 rows x 64 B measured
+// 724 vs 683 us of fill alone at 8192^3) in S = 2 slots (2 x (BM + BN) x 128 B of LDS), each K64
+// tile run as two k32 phases so the per-wave fragment registers stay those of one k32 step.  The
+// DMA is buffer_load ... lds (one 32-bit lane offset, the K offset in soffset: no per-issue VALU).
 // Schedule (interval = the span between two barriers; group 1 one interval behind group 0):
 //   group 0: L(t,0) @4t, C(t,0) @4t+1, L(t,1) @4t+2, C(t,1) @4t+3;  group 1: each one later.
 //   L(t,0) issues the wave's share of tile t + 1's DMA (slot (t + 1) % 2 = (t - 1) % 2, whose last
@@ -1174,127 +996,6 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const bf16* __restrict__ A, 
   wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
 }
 
-// gemm7: REGISTER-prefetched staging for the narrow-N ViT GEMMs (out-proj, fc2: N = 1024, where a
-// one-round tile is at most ~160 x 128 and the per-CU fill -- (BM + BN) x K x 2 bytes, 2.36 MB per
-// CU for fc2 -- bounds the kernel).  The LDS-DMA ring holds at most one to three 36 KB stages in
-// flight in LDS; here each thread keeps the next D stages' chunks in VGPRs (D x 5 x 16 B: the 8-wave
-// 160 x 128 tile leaves ~150 VGPRs free), so D x 36 KB are in flight per CU beside a 2-slot LDS
-// double buffer, with full 128-B lines per row (8 lanes per row segment) and one cheap
-// global_load_dwordx4 per chunk instead of an LDS-DMA issue.  Per K-step k (BK = 64): wait for the
-// registers of stage k + 1 (counted vmcnt, D - 1 stages stay in flight), write them to LDS slot
-// (k + 1) % 2 (swizzled like gemm3: chunk c of row r at c ^ ((r / 2) % 8)), reload that register
-// slot with stage k + 1 + D, MFMA on slot k % 2, barrier.  Same MFMA and k order as gemm3.
-template <typename TO, int BM, int BN, int D, int EPI>
-__global__ __launch_bounds__(512) void gemm7_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ W,
-                                                    int64_t ldw, int64_t M, int64_t K, int tiles_n, EpiArgs e,
-                                                    int group_m) {
-  constexpr int NT = 512, BK = 64, BKC = 8, WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
-  constexpr int STAGE = (BM + BN) * BK, CH = (BM + BN) * BKC, NL = (CH + NT - 1) / NT;
-  static_assert(NL == 5, "the wait statements name five destinations");
-  static_assert(D == 2 || D == 4, "register slots: the host checks K / 64 % D == 0");
-  using SW = Swz<64>;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int tm_i, tn_i;
-  wide_tile(xcd_remap(blockIdx.x, gridDim.x), M, BM, tiles_n, group_m, tm_i, tn_i);
-  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
-  const int wm = (wave / 4) * WM, wn = (wave % 4) * WN;
-
-  // Every thread issues NL loads per stage (uniform counts: one wait statement, no branches between
-  // a load and its wait); a chunk index past the stage re-loads chunk c - NT into the same LDS
-  // slot as its owner (identical bytes, a benign duplicate write).
-  const bf16* src[NL];
-  int ldo[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    int c = tid + i * NT;
-    if (c >= CH) c -= NT;
-    const int row = c / BKC, ch = c % BKC;
-    if (row < BM) src[i] = A + min<int64_t>(m0 + row, M - 1) * lda + ch * 8;
-    else src[i] = W + (n0 + row - BM) * ldw + ch * 8;
-    ldo[i] = (row * BKC + SW::slot(row, ch)) * 8;
-  }
-  // The prefetch loads are inline asm: hipcc's waitcnt pass would drain every older load (vmcnt(0))
-  // before the first LDS write of a register slot, collapsing the D-stage prefetch to one.  Their
-  // completion is counted here: the wait statement names the slot's five destinations "+v" (form
-  // (ii) of cdna_hip_programming.md §5.7), and the steady-state loop has no branch between a load and
-  // its wait (the ISA carries no copy of a slot register in between: tests/test_isa_lint_cpu.py R4).
-  i32x4 R[D][NL];
-  const int klast = (int)(K / BK) - 1;
-  auto gload = [&](i32x4 (&r)[NL], int kt) {
-    const int64_t k0 = (int64_t)min(kt, klast) * BK;      // past the end: a harmless re-load
-#pragma unroll
-    for (int i = 0; i < NL; ++i) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[i]) : "v"(src[i] + k0) : "memory");
-  };
-  auto lstore = [&](const i32x4 (&r)[NL], int buf) {
-    bf16* st = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) *reinterpret_cast<i32x4*>(st + ldo[i]) = r[i];
-  };
-  auto wait_slot = [&](auto n_c, i32x4 (&r)[NL]) {      // at most N younger stages still in flight
-    constexpr int N = decltype(n_c)::value;
-    asm volatile("s_waitcnt vmcnt(%5)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) : "i"(N * NL) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int r16 = lane & 15, q = lane >> 4;
-  const int fo0 = r16 * BK + ((q ^ ((r16 >> 1) & 7)) * 8), fo1 = r16 * BK + (((4 + q) ^ ((r16 >> 1) & 7)) * 8);
-  const int ktiles = klast + 1;
-
-  // prologue: stages 0 .. D - 1 into the register slots; stage 0 to LDS slot 0; stage D into slot 0
-#pragma unroll
-  for (int d = 0; d < D; ++d) gload(R[d], d);
-  wait_slot(std::integral_constant<int, D - 1>{}, R[0]);
-  lstore(R[0], 0);
-  gload(R[0], D);
-  __syncthreads();
-
-  auto compute = [&](int buf) {
-    const bf16* As = smem + buf * STAGE;
-    const bf16* Ws = As + BM * BK;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      s16x8 bfrag[FM], afrag[FN];
-#pragma unroll
-      for (int i = 0; i < FN; ++i) afrag[i] = *reinterpret_cast<const s16x8*>(&Ws[(wn + 16 * i) * BK + (h ? fo1 : fo0)]);
-#pragma unroll
-      for (int j = 0; j < FM; ++j) bfrag[j] = *reinterpret_cast<const s16x8*>(&As[(wm + 16 * j) * BK + (h ? fo1 : fo0)]);
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-#pragma unroll
-        for (int i = 0; i < FN; ++i) acc[i][j] = mfma_bf16(afrag[i], bfrag[j], acc[i][j]);
-    }
-  };
-  // K-step k with register slot S1 = (k + 1) % D holding stage k + 1 (in flight since step k + 1 - D);
-  // after the step the slot is reloaded with stage k + 1 + D.  At the last step the slot's data is a
-  // re-load nobody reads; the LDS write of it lands in the slot no later step reads.
-  auto step = [&](int k, auto s1_c) {
-    constexpr int S1 = decltype(s1_c)::value;
-    wait_slot(std::integral_constant<int, D - 1>{}, R[S1]);
-    lstore(R[S1], (k + 1) & 1);
-    gload(R[S1], k + 1 + D);
-    compute(k & 1);
-    __syncthreads();
-  };
-  for (int k = 0; k < ktiles; k += D) {
-    step(k, std::integral_constant<int, 1 % D>{});
-    step(k + 1, std::integral_constant<int, 2 % D>{});
-    if constexpr (D > 2) {
-      step(k + 2, std::integral_constant<int, 3 % D>{});
-      step(k + 3, std::integral_constant<int, 4 % D>{});
-    }
-  }
-  // drain the trailing re-loads before their registers can be reused
-#pragma unroll
-  for (int d = 0; d < D; ++d) wait_slot(std::integral_constant<int, 0>{}, R[d]);
-  wide_epilogue<TO, BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
-}
-
 int g_gemm_group = 4;   // gemm3 tile order: 0 = row-major, G > 0 = G m-tiles per group (catseg_set_gemm_group); 4 measured best (fc2 48.6 -> 47.4 us)
 
 EpiArgs make_epi(const CatsegGemmArgs* g) {
@@ -1312,39 +1013,19 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   return e;
 }
 
-int g_gemm4_group = 5;   // gemm4 tile order: G m-tiles per group (catseg_set_gemm4_group)
+int g_gemm4_group = 5;   // gemm6 tile order: G m-tiles per group (catseg_set_gemm4_group)
 
-template <typename TO, int BM, int BN, int D, int EPI>
-bool launch7(const CatsegGemmArgs* g, hipStream_t st) {
-  if (g->N % BN != 0 || g->K % 64 != 0 || (g->K / 64) % D != 0) return false;
+// the wide ping-pong tiles (gemm6); ABL > 0: timing ablations (tools/micro_gemm.py 56-60, wrong outputs)
+template <typename TO, int BM, int BN, int EPI, int ABL = 0>
+bool launch6(const CatsegGemmArgs* g, hipStream_t st) {
+  if (g->N % BN != 0 || g->K % 64 != 0) return false;
   const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
   if (!ident) return false;
   const EpiArgs e = make_epi(g);
   const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
-  auto kern = gemm7_kernel<TO, BM, BN, D, EPI>;
+  auto kern = gemm6_kernel<TO, BM, BN, EPI, ABL>;
   hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A, g->lda, (const bf16*)g->W,
-                     g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm_group));
-  return true;
-}
-
-// KIND 4 = gemm4 (plain K-loop), 5 = gemm5 (ping-pong)
-template <typename TO, int BM, int BN, int S, int EPI, int KIND = 5, int ABL = 0>
-bool launch4(const CatsegGemmArgs* g, hipStream_t st) {
-  if (g->N % BN != 0 || g->K % (KIND == 6 ? 64 : 32) != 0) return false;
-  const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
-  if (!ident) return false;
-  const EpiArgs e = make_epi(g);
-  const int tm = (int)((g->M + BM - 1) / BM), tn = (int)(g->N / BN);
-  if constexpr (KIND == 6) {
-    auto kern = gemm6_kernel<TO, BM, BN, EPI, ABL>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A, g->lda, (const bf16*)g->W,
-                       g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
-  } else if constexpr (KIND == 4)
-    hipLaunchKernelGGL((gemm4_kernel<TO, BM, BN, S, EPI>), dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A,
-                       g->lda, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
-  else
-    hipLaunchKernelGGL((gemm5_kernel<TO, BM, BN, S, EPI, ABL>), dim3((unsigned)(tm * tn)), dim3(512), 0, st, (const bf16*)g->A,
-                       g->lda, (const bf16*)g->W, g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
+                     g->ldw, g->M, g->K, tn, e, std::max(1, g_gemm4_group));
   return true;
 }
 
@@ -1373,6 +1054,7 @@ bool launch3f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
   return true;
 }
 
+int g_gemm_wide = 1;      // 1 = the automatic choice includes the wide ping-pong tiles (gemm6); 0 = round-5 candidates
 int g_gemm_variant = 0;   // 0 = automatic; >0 forces one of the automatic gemm3 tiles (tests / tuning)
 
 // returns true when a gemm3 variant was launched
@@ -1410,7 +1092,7 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
     const bool ident = g->amap.d1 == 1 && g->amap.m1 >= g->M && g->amap.s1 == 1 && g->amap.m2 == 1 && g->amap.off == 0;
     const bool lean = !g->add && !g->res2 && g->alpha == 1.f &&
                       (g->act == ACT_NONE || (g->act == ACT_QUICKGELU && !g->res)) && g->store_mode == 0;
-    const bool wide_ok = ident && lean && g->M * g->lda * 2 < 0x7fffffffLL && g->N * g->ldw * 2 < 0x7fffffffLL;
+    const bool wide_ok = g_gemm_wide && ident && lean && g->M * g->lda * 2 < 0x7fffffffLL && g->N * g->ldw * 2 < 0x7fffffffLL;
     float best = 0.f;
     for (const Cand& c : cands) {
       if (g->N % c.bn != 0 || g->K % c.bk != 0) continue;
@@ -1446,32 +1128,18 @@ bool try_gemm3(const CatsegGemmArgs* g, hipStream_t st) {
   if (epi == 1 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 1>(g, st);
   if (epi == 2 && v == 22) return launch3<TO, 160, 128, 2, 4, 4, 64, false, 2>(g, st);
   if (epi == 2 && v == 24) return launch3<TO, 96, 128, 2, 4, 2, 128, false, 2>(g, st);
-  // wide tiles (lean epilogues only): 30-33 gemm4, 40-45 gemm5 (ping-pong)
-  if (v >= 30 && v < 70 && (epi == 1 || epi == 2)) {
+  // wide ping-pong tiles (gemm6, lean epilogues only); 56-60: timing ablations (wrong outputs)
+  if (v >= 50 && v < 70 && (epi == 1 || epi == 2)) {
     const bool e1 = epi == 1;
     switch (v) {
-      case 30: return e1 ? launch4<TO, 320, 256, 4, 1, 4>(g, st) : launch4<TO, 320, 256, 4, 2, 4>(g, st);
-      case 31: return e1 ? launch4<TO, 320, 192, 4, 1, 4>(g, st) : launch4<TO, 320, 192, 4, 2, 4>(g, st);
-      case 40: return e1 ? launch4<TO, 320, 256, 4, 1>(g, st) : launch4<TO, 320, 256, 4, 2>(g, st);
-      case 41: return e1 ? launch4<TO, 320, 192, 4, 1>(g, st) : launch4<TO, 320, 192, 4, 2>(g, st);
-      case 42: return e1 ? launch4<TO, 256, 256, 4, 1>(g, st) : launch4<TO, 256, 256, 4, 2>(g, st);
-      case 43: return e1 ? launch4<TO, 320, 256, 3, 1>(g, st) : launch4<TO, 320, 256, 3, 2>(g, st);
-      case 44: return e1 ? launch4<TO, 256, 192, 4, 1>(g, st) : launch4<TO, 256, 192, 4, 2>(g, st);
-      case 45: return e1 ? launch4<TO, 256, 128, 4, 1>(g, st) : launch4<TO, 256, 128, 4, 2>(g, st);
-      case 46: return launch4<TO, 256, 256, 4, 1, 5, 1>(g, st);   // ablation: no LDS-DMA (wrong output)
-      case 47: return launch4<TO, 256, 256, 4, 1, 5, 2>(g, st);   // ablation: no MFMA (wrong output)
-      // gemm6 (ping-pong, full-line BK = 64 staging)
-      case 50: return e1 ? launch4<TO, 320, 256, 2, 1, 6>(g, st) : launch4<TO, 320, 256, 2, 2, 6>(g, st);
-      case 51: return e1 ? launch4<TO, 320, 192, 2, 1, 6>(g, st) : launch4<TO, 320, 192, 2, 2, 6>(g, st);
-      case 52: return e1 ? launch4<TO, 256, 256, 2, 1, 6>(g, st) : launch4<TO, 256, 256, 2, 2, 6>(g, st);
-      case 56: return launch4<TO, 256, 256, 2, 1, 6, 1>(g, st);   // ablation: no LDS-DMA (wrong output)
-      case 57: return launch4<TO, 256, 256, 2, 1, 6, 2>(g, st);   // ablation: no MFMA (wrong output)
-      // gemm7 (register-prefetched staging)
-      case 62: return e1 ? launch7<TO, 160, 128, 2, 1>(g, st) : launch7<TO, 160, 128, 2, 2>(g, st);
-      case 63: return e1 ? launch7<TO, 160, 128, 4, 1>(g, st) : launch7<TO, 160, 128, 4, 2>(g, st);
-      case 58: return launch4<TO, 320, 256, 2, 2, 6, 1>(g, st);   // fc1 tile ablations (wrong output)
-      case 59: return launch4<TO, 320, 256, 2, 2, 6, 2>(g, st);
-      case 60: return launch4<TO, 320, 256, 2, 2, 6, 3>(g, st);
+      case 50: return e1 ? launch6<TO, 320, 256, 1>(g, st) : launch6<TO, 320, 256, 2>(g, st);
+      case 51: return e1 ? launch6<TO, 320, 192, 1>(g, st) : launch6<TO, 320, 192, 2>(g, st);
+      case 52: return e1 ? launch6<TO, 256, 256, 1>(g, st) : launch6<TO, 256, 256, 2>(g, st);
+      case 56: return launch6<TO, 256, 256, 1, 1>(g, st);   // no LDS-DMA
+      case 57: return launch6<TO, 256, 256, 1, 2>(g, st);   // no MFMA
+      case 58: return launch6<TO, 320, 256, 2, 1>(g, st);   // the fc1 tile: no LDS-DMA
+      case 59: return launch6<TO, 320, 256, 2, 2>(g, st);   //                no MFMA
+      case 60: return launch6<TO, 320, 256, 2, 3>(g, st);   //                no epilogue
       default: return false;
     }
   }
@@ -1580,6 +1248,7 @@ bool launch_f8(const CatsegGemmArgs* g, const float* sa, const float* sw, hipStr
 }  // namespace
 
 CATSEG_KNOB(g_gemm_variant, "gemm_variant");
+CATSEG_KNOB(g_gemm_wide, "gemm_wide");
 CATSEG_KNOB(g_gemm_group, "gemm_group");
 CATSEG_KNOB(g_gemm4_group, "gemm4_group");
 CATSEG_KNOB(g_epi_prefetch, "epi_prefetch");

@@ -96,26 +96,3 @@ def test_swin_opaque_dma_counted_waits(linted):
         assert v["opaque_dma"] >= 1 and v["counted_waits"] == 1, (k, v)
         assert v["min_younger_vmem"] >= 18, (k, v)
 
-
-def test_asm_prefetch_rule_fires():
-    """R4 flags a read of an in-flight asm load's destination and accepts it after a covering wait."""
-    ld = I.Insn(0, "global_load_dwordx4", "v[2:5], v[10:11], off")
-    ld2 = I.Insn(8, "global_load_dwordx4", "v[6:9], v[12:13], off")
-    f = I.Func("gemm7_kernel_synthetic", [ld, ld2, I.Insn(16, "v_mov_b32_e32", "v20, v3"), I.Insn(20, "s_endpgm", "")])
-    bad = I.check_prefetch(f)[0]
-    assert len(bad) == 1 and bad[0].rule == "R4"
-    # vmcnt(1) retires the older load (v[2:5]) only
-    f.insns.insert(2, I.Insn(12, "s_waitcnt", "vmcnt(1)"))
-    assert I.check_prefetch(f)[0] == []
-    f.insns.insert(4, I.Insn(18, "ds_write_b128", "v1, v[6:9]"))
-    assert len(I.check_prefetch(f)[0]) == 1
-
-
-def test_gemm7_register_prefetch_is_never_touched_in_flight(linted):
-    """gemm7's inline-asm prefetch loads (invisible to hipcc's waitcnt pass) are read only after the
-    counted wait that retires them: no compiler copy, spill or reuse in between (R4)."""
-    findings, report = linted
-    r4 = [str(x) for x in findings if x.rule == "R4"]
-    assert not r4, "\n".join(r4[:20])
-    g7 = {k: v for k, v in report.items() if "gemm7_kernel" in k}
-    assert g7 and all(v["prefetch_loads"] >= 20 for v in g7.values()), g7

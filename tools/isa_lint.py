@@ -17,12 +17,6 @@ instead of a GPU run.
       hand-counted `s_waitcnt vmcnt(N)` the kernel relies on is reached from every DMA only along
       paths that issue >= N younger vector-memory instructions (or pass a vmcnt(0)), so the wait
       retires every DMA.  Control-flow aware: basic blocks from the branch targets.
-  R4  asm register prefetch (gemm7_kernel: inline-asm `global_load_dwordx4` into VGPRs, invisible to
-      the waitcnt pass): along the kernel's instruction stream no instruction other than the next
-      load into the same registers reads or writes a destination register of an outstanding load
-      (a compiler copy, spill or reuse between a load and the counted `s_waitcnt vmcnt(N)` that
-      retires it would move garbage).  Outstanding = not yet retired by a vmcnt wait (loads retire
-      in order: vmcnt(N) retires all but the N youngest vector-memory instructions).
 
 Usage: python tools/isa_lint.py [objects...]   (default build/csrc/*.o); exits 1 on a violation.
 """
@@ -287,50 +281,6 @@ def check_dma(f: Func, counted: Iterable[int]) -> Tuple[List[Finding], Dict[str,
 COUNTED = {"swin_win5_kernel": (18,), "swin_win3_kernel": (8,)}
 
 
-# ---------------------------------------------------------------- R4: asm register prefetch
-ASM_PREFETCH = ("gemm7_kernel",)
-
-
-def _vregs(args: str) -> List[Tuple[str, int, int]]:
-    return [r for r in (regs(a) for a in split_operands(args)) if r[0]]
-
-
-def check_prefetch(f: Func) -> Tuple[List[Finding], Dict[str, int]]:
-    """R4 over the linear instruction stream (the steady-state loop body is straight-line code)."""
-    if not any(k in f.name for k in ASM_PREFETCH):
-        return [], {}
-    out: List[Finding] = []
-    pending: List[Tuple[int, Tuple[str, int, int]]] = []   # (index, destination) per outstanding VMEM op
-    loads = 0
-    for i, ins in enumerate(f.insns):
-        n = _vmcnt(ins)
-        if n is not None:
-            pending = pending[len(pending) - n:] if n < len(pending) else pending
-            if n == 0:
-                pending = []
-            continue
-        ops = _vregs(ins.args)
-        if VMEM.match(ins.op):
-            dst = ops[0] if ins.op.startswith(("global_load", "buffer_load")) and "lds" not in ins.args else ("", 0, -1)
-            # this instruction's operands must not touch an outstanding load's destination
-            srcs = ops[1:] if dst[0] else ops
-            for _, d in pending:
-                if any(r[0] == d[0] and max(r[1], d[1]) <= min(r[2], d[2]) for r in srcs):
-                    out.append(Finding("R4", f.name, ins.addr, f"reads an in-flight load destination: {ins.op} {ins.args}"))
-            if dst[0]:
-                pending = [(j, d) for j, d in pending if not (d == dst)]
-                loads += 1
-            pending.append((i, dst))
-            continue
-        for _, d in pending:
-            if not d[0]:
-                continue
-            if any(r[0] == d[0] and max(r[1], d[1]) <= min(r[2], d[2]) for r in ops):
-                out.append(Finding("R4", f.name, ins.addr, f"touches an in-flight load destination: {ins.op} {ins.args}"))
-                break
-    return out, {"prefetch_loads": loads}
-
-
 def lint(objs: List[str]):
     findings: List[Finding] = []
     report: Dict[str, Dict[str, int]] = {}
@@ -340,9 +290,8 @@ def lint(objs: List[str]):
                 fl, st = check_mfma(f)
                 counted = next((v for k, v in COUNTED.items() if k in f.name), ())
                 dl, ds = check_dma(f, counted)
-                pl, ps = check_prefetch(f)
-                findings += fl + dl + pl
-                report[f"{os.path.basename(obj)}:{f.name}"] = {**st, **ds, **ps}
+                findings += fl + dl
+                report[f"{os.path.basename(obj)}:{f.name}"] = {**st, **ds}
     return findings, report
 
 
