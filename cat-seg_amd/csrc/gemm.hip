@@ -987,7 +987,7 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const bf16* __restrict__ A, 
       for (int j = 0; j < FM; ++j) asm volatile("" :: "v"(acc[i][j]));
     return;
   }
-  if constexpr (sizeof(TO) == 2) {
+  if constexpr (sizeof(TO) == 2 && FM % 2 == 0) {
     if ((e.pf & 2) && !(EPI == 1 && e.res)) {
       wide_epilogue_bf16<BM, BN, EPI, FM, FN>(e, acc, smem, M, m0, n0);
       return;
