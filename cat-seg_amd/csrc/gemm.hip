@@ -438,6 +438,11 @@ struct Swz {
 // bias loaded once (same box, M = 4616: out-proj 20.8 -> 19.9 us, fc1 55.1 -> 52.7, fc2 48.3 -> 47.1;
 // bit-identical); 0 = one residual round trip per epilogue round
 int g_epi_prefetch = 1;
+int g_gemm3_store = 0;  // gemm3 lean fp32 epilogue stores: 0 = plain, 1 = nt (A/B knob)
+// gemm6 bf16 epilogue stores: 0 = plain, 1 = nt, 2 = sc1 write-through (default: the output leaves the
+// XCD's L2 as it is written instead of as dirty lines at the kernel boundary; same box, whole step,
+// tools/ab_knob.py: 9.309 / 9.286 / 9.234 ms)
+int g_wide_store = 2;
 int g_wide_epi = 1;   // gemm6 bf16 outputs: 1 = register-side epilogue (wide_epilogue_bf16), 0 = fp32 LDS staging
 template <typename TO, int BM, int BN, int WGM, int WGN, int S, int BK, bool F8 = false, bool SC = false,
           int EPI = 0>
@@ -652,6 +657,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm3_kernel(const bf16* __res
 #pragma unroll
               for (int r = 0; r < 8; ++r) v[r] += rc[k][r];
             }
+            if constexpr (sizeof(TO) == 4) {
+              if (e.pf & 16) {          // A/B knob gemm3_store 1: nt stores of the fp32 rows
+                float* p = reinterpret_cast<float*>(e.out) + m * e.ldo + n;
+                __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(p));
+                __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(p + 4));
+                continue;
+              }
+              if (e.pf & 32) {          // gemm3_store 2: sc1 write-through
+                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(e.out, (short)0, 0x7fffffff, 0x00020000);
+                const int off = (int)((m * e.ldo + n) * 4);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, f32x4{v[0], v[1], v[2], v[3]}), r, off, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, f32x4{v[4], v[5], v[6], v[7]}), r, off + 16, 0, 16);
+                continue;
+              }
+            }
             store8f(reinterpret_cast<TO*>(e.out) + m * e.ldo + n, v);
           }
         }
@@ -856,7 +876,15 @@ DEV void wide_epilogue_bf16(const EpiArgs& e, f32x4 (&acc)[FN][FM], bf16* smem, 
     }
 #pragma unroll
     for (int k = 0; k < IPT; ++k)
-      if (tid + k * NT4 < ITEMS && mr[k] < M) st16(reinterpret_cast<bf16*>(e.out) + mr[k] * e.ldo + n0 + cc[k], val[k]);
+      if (tid + k * NT4 < ITEMS && mr[k] < M) {
+        bf16* p = reinterpret_cast<bf16*>(e.out) + mr[k] * e.ldo + n0 + cc[k];
+        if (e.pf & 4) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, val[k]), reinterpret_cast<i32x4*>(p));
+        else if (e.pf & 8) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(e.out, (short)0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, val[k]), r,
+                                                 (int)((mr[k] * e.ldo + n0 + cc[k]) * 2), 0, 16);   // sc1 write-through
+        } else st16(p, val[k]);
+      }
   }
 }
 
@@ -1009,7 +1037,8 @@ EpiArgs make_epi(const CatsegGemmArgs* g) {
   e.store_mode = g->store_mode; e.cvt_k = g->cvt_k; e.cvt_hin = g->cvt_hin; e.cvt_win = g->cvt_win;
   e.cvt_cout = g->cvt_cout;
   e.sa = nullptr; e.sw = nullptr;
-  e.pf = g_epi_prefetch | (g_wide_epi ? 2 : 0);
+  e.pf = g_epi_prefetch | (g_wide_epi ? 2 : 0) | (g_wide_store == 1 ? 4 : g_wide_store == 2 ? 8 : 0) |
+         (g_gemm3_store == 1 ? 16 : g_gemm3_store == 2 ? 32 : 0);
   return e;
 }
 
@@ -1253,6 +1282,8 @@ CATSEG_KNOB(g_gemm_group, "gemm_group");
 CATSEG_KNOB(g_gemm4_group, "gemm4_group");
 CATSEG_KNOB(g_epi_prefetch, "epi_prefetch");
 CATSEG_KNOB(g_wide_epi, "wide_epi");
+CATSEG_KNOB(g_wide_store, "wide_store");
+CATSEG_KNOB(g_gemm3_store, "gemm3_store");
 CATSEG_KNOB(g_gemm_f8_variant, "gemm_fp8_variant");
 
 extern "C" int catseg_gemm_fp8(const CatsegGemmArgs* g, const float* scale_a, const float* scale_w, void* stream) {
