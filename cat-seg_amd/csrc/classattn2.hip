@@ -40,6 +40,7 @@ struct Cls2P {
   const float* k_pad; const float* v_pad; int n_pad; float attn_eps;
   bf16* y; int64_t ld_y;
   int64_t B; int T; int HW;
+  int wt;        // output rows through sc1 write-through stores (cls_store knob)
   int dbg;       // diagnostics (catseg_set_classattn_variant(16 + bits)): 1 = LN rows all row 0, 2 = stage-B rows all row 0
 };
 
@@ -333,7 +334,9 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
       const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
       if (t < T) {
         const uint4 w = (q & 1) ? make_uint4(got.x, got.y, yv[1].x, yv[1].y) : make_uint4(yv[0].x, yv[0].y, got.x, got.y);
-        *reinterpret_cast<uint4*>(yrow0 + ((a.dbg & 2) ? 0 : t) * ys + h * D + xcol) = w;
+        bf16* dst = yrow0 + ((a.dbg & 2) ? 0 : t) * ys + h * D + xcol;
+        if (a.wt) st16_wt(a.y, (dst - a.y) * 2, w);
+        else *reinterpret_cast<uint4*>(dst) = w;
       }
     };
     uint2 gqA[2], xrA[2], gqB[2], xrB[2];
@@ -356,6 +359,8 @@ __global__ __launch_bounds__(NT, 2) void classattn2_kernel(Cls2P a) {
 // >= 16: diagnostics (dbg = v - 16: LN / stage-B rows all row 0, phase stamps); 0 = default
 int g_classattn_variant = 0;
 CATSEG_KNOB(g_classattn_variant, "classattn_variant");
+int g_cls_store = 0;   // class attention output stores: 0 = plain, 1 = sc1 write-through (A/B knob; same box, whole step 9.250 -> 9.280 ms)
+CATSEG_KNOB(g_cls_store, "cls_store");
 
 extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream) {
   CATSEG_CHECK(a && a->x && a->w_qkv && a->b_qkv && a->ln_g && a->ln_b && a->tg && a->y && a->tgk_t,
@@ -383,6 +388,7 @@ extern "C" int catseg_class_attention(const CatsegClassAttnArgs* a, void* stream
   p.y = (bf16*)a->y; p.ld_y = a->ld_y;
   p.B = a->B; p.T = a->T; p.HW = a->HW;
   p.dbg = g_classattn_variant >= 16 ? g_classattn_variant - 16 : 0;
+  p.wt = g_cls_store && a->B * a->T * (int64_t)a->HW * a->ld_y * 2 < 0x7fffffffLL;
   const int cus = catseg_device_cus();
   const int64_t npix = a->B * a->HW;
   const unsigned grid = (unsigned)std::min<int64_t>(npix, 2LL * cus);

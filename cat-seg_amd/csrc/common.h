@@ -55,6 +55,16 @@ template <> struct Vec16<bf16> { static constexpr int N = 8; };
 
 DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 DEV void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+// sc1 write-through stores at a byte offset (< 2^31) from a wave-uniform base: the line leaves the
+// XCD's L2 as it is written, so the kernel-end writeback has no dirty lines of it left to flush
+DEV void st16_wt(void* base, int64_t byte_off, uint4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), r, (int)byte_off, 0, 16);
+}
+DEV void st8_wt(void* base, int64_t byte_off, uint2 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i32_t, v), r, (int)byte_off, 0, 16);
+}
 
 // load 4 consecutive elements as floats
 template <typename T> DEV void load4(const T* p, float out[4]);

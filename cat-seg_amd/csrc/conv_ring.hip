@@ -48,6 +48,7 @@ struct RingP {
   const float* add; int64_t add_ss; int64_t add_div;
   bf16* out; float* stats;
   int up_split;   // UP: output channels of a parity split over this many workgroups (1, 2 or 4)
+  int wt;         // output pixels through sc1 write-through stores (ring_store knob)
 };
 
 template <int C>
@@ -418,13 +419,17 @@ __global__ __launch_bounds__(NT, OCC) void conv_ring_kernel(RingP p) {
         const uint2 y1 = make_uint2(f2bf2(acc[1][j][0], acc[1][j][1]), f2bf2(acc[1][j][2], acc[1][j][3]));
         const uint2 give = (q & 1) ? y0 : y1;
         const uint2 got = make_uint2((unsigned)__shfl_xor((int)give.x, 16, 64), (unsigned)__shfl_xor((int)give.y, 16, 64));
-        st16(ob + ((q & 1) ? 12 + 4 * q : 4 * q),
-             (q & 1) ? make_uint4(got.x, got.y, y1.x, y1.y) : make_uint4(y0.x, y0.y, got.x, got.y));
+        bf16* dst = ob + ((q & 1) ? 12 + 4 * q : 4 * q);
+        const uint4 val = (q & 1) ? make_uint4(got.x, got.y, y1.x, y1.y) : make_uint4(y0.x, y0.y, got.x, got.y);
+        if (p.wt) st16_wt(p.out, (dst - p.out) * 2, val);
+        else st16(dst, val);
       } else {
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
-          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          store4<bf16>(ob + 16 * i + 4 * q, v);
+          bf16* dst = ob + 16 * i + 4 * q;
+          const uint2 val = make_uint2(f2bf2(acc[i][j][0], acc[i][j][1]), f2bf2(acc[i][j][2], acc[i][j][3]));
+          if (p.wt) st8_wt(p.out, (dst - p.out) * 2, val);
+          else *reinterpret_cast<uint2*>(dst) = val;
         }
       }
     };
@@ -791,6 +796,9 @@ static int ring_variant(const CatsegConvArgs* a, int* tile) {
   return v;
 }
 
+int g_ring_store = 0;   // conv ring output stores: 0 = plain, 1 = sc1 write-through (A/B knob; same box, whole step 9.251 -> 9.375 ms: slower)
+CATSEG_KNOB(g_ring_store, "ring_store");
+
 // Pixels per GroupNorm partial ("tile") of the conv catseg_conv3x3 would run for these args.
 int catseg_conv3x3_ring_tile(const CatsegConvArgs* a) {
   int t = 0;
@@ -810,6 +818,7 @@ int catseg_conv3x3_ring(const CatsegConvArgs* a, hipStream_t st) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
   p.out = (bf16*)a->out; p.stats = a->stats;
+  p.wt = g_ring_store && (int64_t)a->S * a->H * a->W * a->c_out * 2 < 0x7fffffffLL;
   // weights in registers: 9 taps x C/16 half-steps x COUT/WCO/16 fragments
   switch (v) {
     case 1: return launch_ring<64, 32, 4, 1, 156>(p, st);
@@ -946,6 +955,7 @@ extern "C" int catseg_upconv3x3(const CatsegConvArgs* a, void* stream) {
   p.gmean = a->gn_mean; p.grstd = a->gn_rstd; p.ggamma = a->gn_gamma; p.gbeta = a->gn_beta; p.gcpg = a->gn_cpg;
   p.add = a->addend; p.add_ss = a->addend_slice_stride; p.add_div = a->addend_div > 0 ? a->addend_div : 1;
   p.out = (bf16*)a->out; p.stats = a->stats;
+  p.wt = g_ring_store && (int64_t)a->S * a->H * a->W * a->c_out * 2 < 0x7fffffffLL;
   p.up_split = 1;
   hipStream_t st = (hipStream_t)stream;
   // 64-pixel chunks (a 48-wide chunk spans <= 3 rows: 5-row ring, <= 2 new rows = 104 positions):

@@ -39,7 +39,19 @@ struct PEpi {
   const bf16* res2; int64_t ld_res2;
   bf16* out; int64_t ldo;
   int cvt_k, cvt_hin, cvt_win, cvt_cout;
+  int wt;                        // 1: output rows leave through sc1 write-through stores (rows_store knob)
 };
+
+// one 16-byte output chunk at element offset `idx` of e.out: plain, or sc1 write-through (the rows
+// leave the XCD's L2 as they are written; the launch sets wt only when every byte offset fits 31 bits)
+DEV void st_out(const PEpi& e, int64_t idx, uint4 v) {
+  if (e.wt) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(e.out, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), r, (int)(idx * 2), 0, 16);
+  } else {
+    st16(e.out + idx, v);
+  }
+}
 
 // thread t holds chunk t of the tile: row t/16, columns (t%16)*8 .. +8
 DEV uint4 fetch_chunk(const bf16* X, int64_t ldx, int64_t m0, int64_t M) {
@@ -203,7 +215,7 @@ __global__ __launch_bounds__(NT, 2) void pgemm_kernel(const bf16* __restrict__ X
         } else {
           off = m * e.ldo + c;
         }
-        st16(e.out + off, pack8(v));
+        st_out(e, off, pack8(v));
       }
     }
     __syncthreads();
@@ -473,7 +485,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
       v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
       add8(v, y_raw);
       if constexpr (RES2) add8(v, r2_cur);
-      if (m < M) st16(e.out + m * e.ldo + ec, pack8(v));
+      if (m < M) st_out(e, m * e.ldo + ec, pack8(v));
     }
     __syncthreads();
   }
@@ -597,7 +609,7 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
     v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
     add8(v, *reinterpret_cast<const uint4*>(&yres[par][rofs]));
     if constexpr (RES2) add8(v, *reinterpret_cast<const uint4*>(&r2res[par][rofs]));
-    if (m < M) st16(e.out + m * e.ldo + ec, pack8(v));
+    if (m < M) st_out(e, m * e.ldo + ec, pack8(v));
   };
 
   int64_t t = blockIdx.x;
@@ -779,7 +791,7 @@ __global__ __launch_bounds__(NT4, 2) void pconvt64_kernel(const bf16* __restrict
       const uint32_t ky = (uint32_t)c / (2 * cout), rem = (uint32_t)c - ky * 2 * cout;
       const uint32_t kx = rem / cout, co = rem - kx * cout;
       const int64_t orow = ((int64_t)(sl * hin + y) * 2 + ky) * (2 * win) + x * 2 + kx;
-      st16(e.out + orow * cout + co, pack8(v));
+      st_out(e, orow * cout + co, pack8(v));
     }
   }
 }
@@ -792,6 +804,15 @@ PEpi make_pepi(const CatsegRowsEpi* p) {
   e.res = (const bf16*)p->res; e.ld_res = p->ld_res; e.res2 = (const bf16*)p->res2; e.ld_res2 = p->ld_res2;
   e.out = (bf16*)p->out; e.ldo = p->ldo;
   e.cvt_k = p->cvt_k; e.cvt_hin = p->cvt_hin; e.cvt_win = p->cvt_win; e.cvt_cout = p->cvt_cout;
+  e.wt = 0;
+  return e;
+}
+
+int g_rows_store = 0;   // output stores of the persistent row kernels: 0 = plain, 1 = sc1 write-through (A/B knob; same box, whole step 9.249 vs 9.249 ms: neutral)
+CATSEG_KNOB(g_rows_store, "rows_store");
+// e with the write-through flag of the rows_store knob, for an output spanning `out_elems` bf16
+PEpi with_wt(PEpi e, int64_t out_elems) {
+  e.wt = g_rows_store && out_elems * 2 < 0x7fffffffLL;
   return e;
 }
 
@@ -806,7 +827,8 @@ void launch_pgemm(const void* x, int64_t ld_x, int64_t M, const float* g, const 
                   const PEpi& e, hipStream_t st) {
   // NOUT=128 variants fit 3 workgroups per CU (<= 96 VGPRs, 25 KB LDS): more rows in flight
   hipLaunchKernelGGL((pgemm_kernel<NOUT, ADD, RES, SCATTER>), dim3(persist_grid(M, NOUT == 128 ? 3 : 1)), dim3(NT), 0, st,
-                     (const bf16*)x, ld_x, M, g, b, eps, (const bf16*)w, e);
+                     (const bf16*)x, ld_x, M, g, b, eps, (const bf16*)w,
+                     with_wt(e, SCATTER ? M * e.cvt_k * e.cvt_k * e.cvt_cout : M * e.ldo));
 }
 
 }  // namespace
@@ -839,7 +861,7 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
   CATSEG_CHECK(M < (1LL << 31), "convt64_gn: row count must fit 31 bits");
   const PEpi e = make_pepi(epi);
   hipLaunchKernelGGL((pconvt64_kernel<192>), dim3(persist_grid((M + 1) / 2, 2)), dim3(NT4), 0, (hipStream_t)stream,
-                     (const bf16*)x, M, HW, mean, rstd, gamma, beta, cpg, (const bf16*)w, e);
+                     (const bf16*)x, M, HW, mean, rstd, gamma, beta, cpg, (const bf16*)w, with_wt(e, M * 192));
   return catseg_launch_status("convt64_gn");
 }
 
@@ -847,9 +869,10 @@ int g_mlp_variant = 0;   // 0 = barrier-lean pmlp2_kernel (default), 1 = pmlp_ke
 CATSEG_KNOB(g_mlp_variant, "mlp_variant");
 
 int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
-                        const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e, bool res2,
+                        const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e0, bool res2,
                         hipStream_t st) {
   const dim3 grid(persist_grid(M)), blk(NT);
+  const PEpi e = with_wt(e0, M * e0.ldo);
   if (g_mlp_variant == 0) {
     if (act == ACT_GELU && !res2)
       hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
@@ -897,6 +920,7 @@ extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const voi
   CATSEG_CHECK(out == x ? ld_out == ld_x : true, "swin_proj_mlp: in place needs ld_out == ld_x");
   PEpi e{};
   e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
+  e = with_wt(e, M * ld_out);
   if (g_mlp_variant == 0)
     hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,

@@ -55,6 +55,7 @@ struct Swin3P {
   bf16* out; int64_t ld_out;
   int shift; float scale;
   int glin;     // gmap restricted to a slice is rowmap(slice * 576) + pixel
+  int wt;       // swin_win5: launch the sc1 write-through instance (swin_store knob)
 };
 
 // 16-byte chunk c of row r of a chunk-major image with ROWS rows, row XOR swizzle in the low 4 bits
@@ -347,7 +348,7 @@ DEV int local_region5(int wloc, int i, int shift) {   // region3 renumbered with
 // LayerNorm row read (one row x 16 chunks) touch 16 distinct 16-byte bank slots
 DEV int xs5(int c, int r) { return (r * 16 + (c ^ (r & 15))) * 8; }
 
-template <bool SWM, bool GLIN>
+template <bool SWM, bool GLIN, bool WT = false>
 __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_total) {
   __shared__ __attribute__((aligned(16))) bf16 Xn[L * C];               // LayerNorm'd window rows
   __shared__ __attribute__((aligned(16))) bf16 sWv[C * C];              // W_v (every head), chunk-major
@@ -573,11 +574,13 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
         osum = mfma_bf16(ones, pb, osum);
       }
       const float inv = 1.f / osum[0];
-      bf16* O = p.out + (int64_t)win_row3(slice, wl, rb + r16, p.shift) * p.ld_out + h * D;
+      const int64_t oe = (int64_t)win_row3(slice, wl, rb + r16, p.shift) * p.ld_out + h * D;
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-        *reinterpret_cast<uint2*>(O + dt * 16 + 4 * g) =
-            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+      for (int dt = 0; dt < 2; ++dt) {
+        const uint2 val = make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+        if constexpr (WT) st8_wt(p.out, (oe + dt * 16 + 4 * g) * 2, val);
+        else *reinterpret_cast<uint2*>(p.out + oe + dt * 16 + 4 * g) = val;
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     };
@@ -586,6 +589,9 @@ __global__ __launch_bounds__(NT5, 2) void swin_win5_kernel(Swin3P p, int nwin_to
 }
 
 }  // namespace
+
+int g_swin_store = 0;   // swin_win5 output stores: 0 = plain, 1 = sc1 write-through (A/B knob; same box, whole step 9.251 -> 9.356 ms: slower)
+CATSEG_KNOB(g_swin_store, "swin_store");
 
 // launched by catseg_swin_window_attention (swin_fused.hip) after its argument checks
 int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool glin) {
@@ -598,6 +604,7 @@ int swin_win3_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
   p.out = (bf16*)a->out; p.ld_out = a->ld_out;
   p.shift = a->shift; p.scale = a->scale;
+  p.wt = 0;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, n_cu));
   if (a->shift > 0) hipLaunchKernelGGL((swin_win3_kernel<true>), grid, dim3(NT), 0, st, p, nwin_total);
@@ -616,12 +623,18 @@ int swin_win5_launch(const CatsegSwinAttnArgs* a, int n_cu, hipStream_t st, bool
   p.gmap = RowMap{a->gmap.d1, a->gmap.m1, a->gmap.s1, a->gmap.d2, a->gmap.m2, a->gmap.s2, a->gmap.off};
   p.out = (bf16*)a->out; p.ld_out = a->ld_out;
   p.shift = a->shift; p.scale = a->scale;
+  p.wt = g_swin_store && a->S * 576 * a->ld_out * 2 < 0x7fffffffLL;
   const int nwin_total = (int)(a->S * NWIN);
   const dim3 grid((unsigned)std::min(nwin_total, (2 * n_cu) / NWIN * NWIN));
   // only for guidance rows that are one base + the pixel per slice (every engine call; the caller
   // sends other row maps to swin_win3).  The general-row-map instance spilled 19-23 VGPRs and gave
   // wrong shifted-window outputs on the box, so it is not instantiated.
   if (!glin) return -1;
+  if (p.wt) {
+    if (a->shift > 0) hipLaunchKernelGGL((swin_win5_kernel<true, true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
+    else hipLaunchKernelGGL((swin_win5_kernel<false, true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
+    return 0;
+  }
   if (a->shift > 0) hipLaunchKernelGGL((swin_win5_kernel<true, true>), grid, dim3(NT5), 0, st, p, nwin_total);
   else hipLaunchKernelGGL((swin_win5_kernel<false, true>), grid, dim3(NT5), 0, st, p, nwin_total);
   return 0;
