@@ -1,7 +1,8 @@
 """Same-process A/B of a tuning knob (catseg_tuning_set) on the headline step (L/14@336, T=150, bs=8, bf16):
 one engine, one hipGraph per knob value (the value is read at launch, so at capture), rounds
 interleaved; prints ms/step per value and whether the logits equal the first value's bit for bit.
-usage: python tools/ab_knob.py mlp_variant 0 1 [--steps N]"""
+usage: python tools/ab_knob.py mlp_variant 0 1
+       python tools/ab_knob.py wide_store,ln_store,attn_store 2,1,1 0,0,0   (several knobs set together)"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cat-seg_amd"), ROOT]
@@ -12,9 +13,14 @@ from cat_seg.arch import VIT_L14_336
 from cat_seg.engine import CatSegEngine
 from cat_seg.weights import synthesize_state_dict
 
-knob, values = sys.argv[1], [int(v) for v in sys.argv[2:]]
+knob, values = sys.argv[1], sys.argv[2:]
+knobs = knob.split(",")
 L.load()
-setter = lambda v: L.tune(knob, v)
+def setter(v):
+    vs = [int(x) for x in v.split(",")]
+    assert len(vs) == len(knobs), (knobs, v)
+    for k, x in zip(knobs, vs):
+        L.tune(k, x)
 arch = VIT_L14_336
 B, T, R = 8, 150, arch.clip_resolution
 eng = CatSegEngine(arch, synthesize_state_dict(arch, 0), dtype=torch.bfloat16)
