@@ -295,8 +295,65 @@ __device__ const float kGeluSeg[GSEG][4] = {
     {9.999986291e-01f, 2.075184739e-06f, -1.356016696e-06f, 3.768647900e-07f},
 };
 // (fit: R = 5, 32 cubic segments; max |GELU error| 4.3e-6 on [-12, 12], 1.7e-6 on [-4, 4])
+//
+// ACT_GELU7 (gelu_form knob 1): the same idea in 7 VALU per value (tools/gelu_x7_fit.py).  The segment
+// k = round(3.2 x + 16), clamped to [0, 32], comes without a float->int conversion: t = fma(x, 3.2,
+// 2^23 + 16) rounds to an integer whose fp32 bits are 0x4B000000 + k, med3 clamps it, and the bits
+// shifted left by 4 address the 16-byte coefficient row (one v_lshl_add_u32); the cubic is in x itself
+// (no in-segment coordinate, so no fract), the edge segments are the constants 0 and 1, so x * P stays
+// bounded for any x.  fma + med3 + lshl_add + LDS read + 3 fma + mul against gelu_seg's 9 VALU.
+constexpr int ACT_GELU7 = 91;      // internal activation id (not in the C ABI)
+constexpr int GSEG7 = 33;
+// 33 segments (k = round(3.2 x + 16), edges 0 / 1), cubic in x: max |GELU error| 3.287e-06 on [-12, 12] (1.547e-06 on [-4, 4])
+__device__ const float kGeluX7[GSEG7][4] = {
+    {0.000000000e+00f, 0.000000000e+00f, 0.000000000e+00f, 0.000000000e+00f},
+    {2.882618923e-03f, 1.753379707e-03f, 3.561640915e-04f, 2.415746530e-05f},
+    {8.511394262e-03f, 5.501359701e-03f, 1.188187511e-03f, 8.573576633e-05f},
+    {2.231834829e-02f, 1.537315361e-02f, 3.541412065e-03f, 2.727602259e-04f},
+    {5.184482783e-02f, 3.816473484e-02f, 9.407166392e-03f, 7.760967128e-04f},
+    {1.064083949e-01f, 8.392206579e-02f, 2.220178954e-02f, 1.968990080e-03f},
+    {1.924447566e-01f, 1.628885567e-01f, 4.636982083e-02f, 4.435458686e-03f},
+    {3.059913516e-01f, 2.779548168e-01f, 8.525618166e-02f, 8.817944676e-03f},
+    {4.273824394e-01f, 4.152130187e-01f, 1.370187402e-01f, 1.532850228e-02f},
+    {5.257804394e-01f, 5.409126878e-01f, 1.905829757e-01f, 2.294243686e-02f},
+    {5.756489635e-01f, 6.137913465e-01f, 2.261149138e-01f, 2.872194536e-02f},
+    {5.745609403e-01f, 6.108088493e-01f, 2.237454057e-01f, 2.813855931e-02f},
+    {5.451580286e-01f, 5.472433567e-01f, 1.778536141e-01f, 1.707486995e-02f},
+    {5.165857673e-01f, 4.688404500e-01f, 1.059021130e-01f, -5.007953849e-03f},
+    {5.029187202e-01f, 4.172078967e-01f, 4.047473893e-02f, -3.282082453e-02f},
+    {5.001025200e-01f, 4.003199339e-01f, 6.250044797e-03f, -5.630261824e-02f},
+    {5.000000000e-01f, 3.989397287e-01f, -2.000167085e-15f, -6.615200639e-02f},
+    {4.998974502e-01f, 4.003199339e-01f, -6.250044797e-03f, -5.630261824e-02f},
+    {4.970813096e-01f, 4.172078967e-01f, -4.047473893e-02f, -3.282082453e-02f},
+    {4.834142625e-01f, 4.688404500e-01f, -1.059021130e-01f, -5.007953849e-03f},
+    {4.548419714e-01f, 5.472433567e-01f, -1.778536141e-01f, 1.707486995e-02f},
+    {4.254390597e-01f, 6.108088493e-01f, -2.237454057e-01f, 2.813855931e-02f},
+    {4.243510365e-01f, 6.137913465e-01f, -2.261149138e-01f, 2.872194536e-02f},
+    {4.742195904e-01f, 5.409126878e-01f, -1.905829757e-01f, 2.294243686e-02f},
+    {5.726175308e-01f, 4.152130187e-01f, -1.370187402e-01f, 1.532850228e-02f},
+    {6.940086484e-01f, 2.779548168e-01f, -8.525618166e-02f, 8.817944676e-03f},
+    {8.075552583e-01f, 1.628885567e-01f, -4.636982083e-02f, 4.435458686e-03f},
+    {8.935915828e-01f, 8.392206579e-02f, -2.220178954e-02f, 1.968990080e-03f},
+    {9.481551647e-01f, 3.816473484e-02f, -9.407166392e-03f, 7.760967128e-04f},
+    {9.776816368e-01f, 1.537315361e-02f, -3.541412065e-03f, 2.727602259e-04f},
+    {9.914885759e-01f, 5.501359701e-03f, -1.188187511e-03f, 8.573576633e-05f},
+    {9.971174002e-01f, 1.753379707e-03f, -3.561640915e-04f, 2.415746530e-05f},
+    {1.000000000e+00f, 0.000000000e+00f, 0.000000000e+00f, 0.000000000e+00f},
+};
+constexpr int GTAB = GSEG7;        // float4 rows of the LDS table (either form)
+template <int ACT>
 DEV void stage_gelu_table(float4* sG) {
-  if (threadIdx.x < GSEG) sG[threadIdx.x] = *reinterpret_cast<const float4*>(kGeluSeg[threadIdx.x]);
+  if constexpr (ACT == ACT_GELU7) {
+    if (threadIdx.x < GSEG7) sG[threadIdx.x] = *reinterpret_cast<const float4*>(kGeluX7[threadIdx.x]);
+  } else {
+    if (threadIdx.x < GSEG) sG[threadIdx.x] = *reinterpret_cast<const float4*>(kGeluSeg[threadIdx.x]);
+  }
+}
+DEV float gelu_x7(float x, const float4* sG) {
+  const float t = __builtin_amdgcn_fmed3f(__builtin_fmaf(x, 3.2f, 8388624.0f), 8388608.0f, 8388640.0f);
+  const unsigned off = (__builtin_bit_cast(unsigned, t) << 4) - (0x4B000000u << 4);
+  const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sG) + off);
+  return x * __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, x, c.z), x, c.y), x, c.x);
 }
 DEV float gelu_seg(float x, const float4* sG) {
   const float u = __builtin_amdgcn_fmed3f(__builtin_fmaf(x, GSEG / 10.f, GSEG / 2.f), 0.f, GSEG - 0x1p-18f);
@@ -306,7 +363,8 @@ DEV float gelu_seg(float x, const float4* sG) {
 }
 template <int ACT>
 DEV float mlp_act(float v, const float4* sG) {
-  if constexpr (ACT == ACT_GELU) return GELU_SEG ? gelu_seg(v, sG) : gelu1(v);
+  if constexpr (ACT == ACT_GELU7) return gelu_x7(v, sG);
+  else if constexpr (ACT == ACT_GELU) return GELU_SEG ? gelu_seg(v, sG) : gelu1(v);
   else return act_t<ACT>(v);
 }
 
@@ -326,11 +384,11 @@ __global__ __launch_bounds__(NT, 2) void pmlp_kernel(const bf16* __restrict__ Y,
   __shared__ __attribute__((aligned(16))) float st[BM * SLD];
   // gamma / beta / b1 / b2 (/ bp) in LDS (see pgemm_kernel: no global loads behind the prefetch)
   __shared__ __attribute__((aligned(16))) float sPar[NPAR];
-  __shared__ __attribute__((aligned(16))) float4 sG[GSEG];
+  __shared__ __attribute__((aligned(16))) float4 sG[GTAB];
   for (int i = threadIdx.x; i < NPAR; i += NT)
     sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
             : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
-  stage_gelu_table(sG);
+  stage_gelu_table<ACT>(sG);
   __syncthreads();
   const float* sb1 = sPar + 2 * KD;
   const float* sb2 = sPar + 2 * KD + HID;
@@ -517,11 +575,11 @@ __global__ __launch_bounds__(NT, 2) void pmlp2_kernel(const bf16* __restrict__ Y
   __shared__ __attribute__((aligned(16))) bf16 r2res[RES2 ? 2 : 1][RES2 ? BM * KD : 8];
   __shared__ __attribute__((aligned(16))) bf16 xres[PROJ ? BM * KD : 8];       // PROJ: the x rows
   __shared__ __attribute__((aligned(16))) float sPar[NPAR];
-  __shared__ __attribute__((aligned(16))) float4 sG[GSEG];
+  __shared__ __attribute__((aligned(16))) float4 sG[GTAB];
   for (int i = threadIdx.x; i < NPAR; i += NT)
     sPar[i] = i < KD ? ln_g[i] : i < 2 * KD ? ln_b[i - KD] : i < 2 * KD + HID ? b1[i - 2 * KD]
             : i < 3 * KD + HID ? e.bias[i - 2 * KD - HID] : bp[i - 3 * KD - HID];
-  stage_gelu_table(sG);
+  stage_gelu_table<ACT>(sG);
   const float* sb1 = sPar + 2 * KD;
   const float* sb2 = sPar + 2 * KD + HID;
   const float* sbp = sPar + 3 * KD + HID;
@@ -867,6 +925,8 @@ extern "C" int catseg_convt64_gn(const void* x, int64_t M, int64_t HW, const flo
 
 int g_mlp_variant = 0;   // 0 = barrier-lean pmlp2_kernel (default), 1 = pmlp_kernel (A/B; bit-identical)
 CATSEG_KNOB(g_mlp_variant, "mlp_variant");
+int g_gelu_form = 1;     // GELU of pmlp2_kernel: 0 = gelu_seg (9 VALU), 1 = gelu_x7 (7 VALU; same box, whole step 9.675 -> 9.608 ms)
+CATSEG_KNOB(g_gelu_form, "gelu_form");
 
 int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g, const float* b, float eps,
                         const bf16* w1, const float* b1, int act, const bf16* w2, const PEpi& e0, bool res2,
@@ -874,7 +934,11 @@ int rows_mlp_persistent(const bf16* Yb, int64_t ld_y, int64_t M, const float* g,
   const dim3 grid(persist_grid(M)), blk(NT);
   const PEpi e = with_wt(e0, M * e0.ldo);
   if (g_mlp_variant == 0) {
-    if (act == ACT_GELU && !res2)
+    if (act == ACT_GELU && g_gelu_form == 1 && !res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU7, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else if (act == ACT_GELU && g_gelu_form == 1 && res2)
+      hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU7, true, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
+    else if (act == ACT_GELU && !res2)
       hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
     else if (act == ACT_RELU && res2)
       hipLaunchKernelGGL((pmlp2_kernel<ACT_RELU, true, false>), grid, blk, 0, st, Yb, ld_y, M, g, b, eps, w1, b1, w2, e);
@@ -921,7 +985,11 @@ extern "C" int catseg_swin_proj_mlp(const void* attn, int64_t ld_attn, const voi
   PEpi e{};
   e.bias = b2; e.out = (bf16*)out; e.ldo = ld_out;
   e = with_wt(e, M * ld_out);
-  if (g_mlp_variant == 0)
+  if (g_mlp_variant == 0 && g_gelu_form == 1)
+    hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU7, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
+                       (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);
+  else if (g_mlp_variant == 0)
     hipLaunchKernelGGL((pmlp2_kernel<ACT_GELU, false, true>), dim3(persist_grid(M)), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16*)attn, ld_attn, M, ln_gamma, ln_beta, eps, (const bf16*)w1, b1, (const bf16*)w2, e,
                        (const bf16*)x, ld_x, (const bf16*)w_proj, b_proj);

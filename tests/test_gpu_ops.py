@@ -1303,7 +1303,9 @@ def test_mlp_barrier_lean_bit_identical(act, M):
     """The barrier-lean persistent MLP (tuning knob mlp_variant 0, the default: the epilogue of one
     tile beside the first GEMM of the next, residual rows in LDS) equals pmlp_kernel (1) bit for
     bit -- the Swin MLP (GELU), the class MLP (ReLU, + res2), the fused Swin proj + MLP -- on ragged
-    M with one tile per workgroup (40 rows), a few, and many (> 2 tiles per workgroup)."""
+    M with one tile per workgroup (40 rows), a few, and many (> 2 tiles per workgroup).  pmlp_kernel
+    has the segment-table GELU only, so the comparison runs with gelu_form 0; the default 7-VALU form
+    is gated against fp64 in test_mlp_gelu_forms_vs_fp64."""
     C, Hd = 128, 512
     dt = torch.bfloat16
     y = (rnd(M, C, seed=130) * 2).to(dev, dt)
@@ -1313,6 +1315,8 @@ def test_mlp_barrier_lean_bit_identical(act, M):
     w2, b2 = (rnd(C, Hd, seed=136) / 22).to(dev, dt), rnd(C, seed=137).to(dev)
     wp, bp = (rnd(C, C, seed=138) / 11).to(dev, dt), rnd(C, seed=139).to(dev)
     outs = {}
+    form = L.tuning("gelu_form")
+    L.tune("gelu_form", 0)
     try:
         for v in (0, 1):
             L.tune("mlp_variant", v)
@@ -1325,5 +1329,45 @@ def test_mlp_barrier_lean_bit_identical(act, M):
             outs[v] = (o1, o2)
     finally:
         L.tune("mlp_variant", 0)
+        L.tune("gelu_form", form)
     assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0].float() - outs[1][0].float()).abs().max().item()
     assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1].float() - outs[1][1].float()).abs().max().item()
+
+
+@pytest.mark.parametrize("M", [300 * 32 + 17, 40])
+def test_mlp_gelu_forms_vs_fp64(M):
+    """Both GELU forms of the persistent MLPs (gelu_form 0: gelu_seg, 9 VALU; 1: gelu_x7, 7 VALU, the
+    default) against the fp64 composition of the Swin MLP and the fused Swin proj + MLP: each within the
+    same bf16 gate, and the two forms' outputs within a few bf16 ulps of each other."""
+    C, Hd = 128, 512
+    dt = torch.bfloat16
+    y = (rnd(M, C, seed=140) * 2).to(dev, dt)
+    x = rnd(M, C, seed=141).to(dev, dt)
+    g, b = (1 + rnd(C, seed=142) * 0.2).to(dev), (rnd(C, seed=143) * 0.1).to(dev)
+    w1, b1 = (rnd(Hd, C, seed=144) / 4).to(dev, dt), rnd(Hd, seed=145).to(dev)   # hidden spans the GELU range
+    w2, b2 = (rnd(C, Hd, seed=146) / 22).to(dev, dt), rnd(C, seed=147).to(dev)
+    wp, bp = (rnd(C, C, seed=148) / 11).to(dev, dt), rnd(C, seed=149).to(dev)
+    D = lambda t: t.double().cpu()
+    ref_mlp = D(y) + F.gelu(F.layer_norm(D(y), (C,), D(g), D(b), 1e-5) @ D(w1).T + D(b1)) @ D(w2).T + D(b2)
+    x1 = (D(x) + D(y) @ D(wp).T + D(bp)).to(dt).double()
+    ref_pm = x1 + F.gelu(F.layer_norm(x1, (C,), D(g), D(b), 1e-5) @ D(w1).T + D(b1)) @ D(w2).T + D(b2)
+    outs = {}
+    form = L.tuning("gelu_form")
+    try:
+        for f in (0, 1):
+            L.tune("gelu_form", f)
+            o1 = torch.empty_like(y)
+            ops.rows_mlp(y, w1, b1, w2, o1, ln=(g, b), b2=b2, act=L.ACT_GELU, res=y)
+            o2 = x.clone()
+            ops.swin_proj_mlp(y, o2, wp, bp, w1, b1, w2, b2, o2, ln=(g, b))
+            torch.cuda.synchronize()
+            outs[f] = (D(o1), D(o2))
+            e1 = (outs[f][0] - ref_mlp).abs().max().item()
+            e2 = (outs[f][1] - ref_pm).abs().max().item()
+            assert e1 < 0.1 and e2 < 0.1, (f, e1, e2)
+    finally:
+        L.tune("gelu_form", form)
+    for k in range(2):
+        d = (outs[0][k] - outs[1][k]).abs()
+        scale = ref_mlp.abs().max().item() if k == 0 else ref_pm.abs().max().item()
+        assert d.max().item() <= 2 ** -6 * scale, (k, d.max().item(), scale)
