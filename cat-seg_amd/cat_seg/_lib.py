@@ -94,6 +94,16 @@ class LinAttnArgs(C.Structure):
     ]
 
 
+class ClassSeqArgs(C.Structure):
+    _fields_ = [
+        ("qkv", vp), ("ld_qkv", i64), ("packed", vp), ("ld_packed", i64),
+        ("o", vp), ("ld_o", i64), ("x", vp), ("y", vp), ("ld_xy", i64),
+        ("B", i64), ("T", i32), ("HW", i32), ("C", i32),
+        ("n_pad", i32), ("k_pad", vp), ("v_pad", vp),
+        ("dtype", i32),
+    ]
+
+
 class RowsEpi(C.Structure):
     _fields_ = [
         ("bias", vp),
@@ -194,6 +204,8 @@ _SIGS = {
     "catseg_l2normalize": [vp, i64, RowMap, i32, vp, i64, i32, i64, i64, f32, vp],
     "catseg_attention": [C.POINTER(AttnArgs), vp],
     "catseg_linear_attention": [C.POINTER(LinAttnArgs), vp],
+    "catseg_class_seq_pack": [C.POINTER(ClassSeqArgs), vp],
+    "catseg_class_seq_unpack_add": [C.POINTER(ClassSeqArgs), vp],
     "catseg_conv3x3": [C.POINTER(ConvArgs), vp],
     "catseg_conv3x3_partial": [vp, i64, i32, i32, i32, vp, i32, vp, i32, vp],
     "catseg_upconv3x3": [C.POINTER(ConvArgs), vp],

@@ -48,6 +48,9 @@ class CatSegArch:
     decoder_guidance_proj_dims: Tuple[int, int] = (32, 16)
     prompt_channel: int = 1
     pad_len: int = 256
+    # ClassTransformerLayer attention (model.py:324-334): "linear" (LinearAttention, every shipped
+    # config) or "full" (FullAttention, softmax over the padded class axis)
+    attention_type: str = "linear"
     # ---- image preprocessing (config.py:36,67-68) ----
     size_divisibility: int = 32
     clip_pixel_mean: Tuple[float, float, float] = (122.7709383, 116.7460125, 104.09373615)
@@ -124,6 +127,7 @@ def arch_from_cfg(cfg) -> CatSegArch:
         pooling_size=tuple(int(p) for p in head.POOLING_SIZES),
         feature_resolution=tuple(int(p) for p in head.FEATURE_RESOLUTION),
         window_size=int(head.WINDOW_SIZES),
+        attention_type=str(getattr(head, "ATTENTION_TYPE", "linear")),
         text_guidance_proj_dim=int(head.TEXT_GUIDANCE_PROJ_DIM),
         appearance_guidance_proj_dim=int(head.APPEARANCE_GUIDANCE_PROJ_DIM),
         decoder_dims=tuple(head.DECODER_DIMS),

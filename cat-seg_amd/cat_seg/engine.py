@@ -54,6 +54,8 @@ class CatSegEngine:
         L.require_gpu()
         if arch.hidden_dim != 128 or arch.nheads != 4:
             raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
+        if arch.attention_type not in ("linear", "full"):     # AttentionLayer (model.py:331-336)
+            raise NotImplementedError(f"ATTENTION_TYPE {arch.attention_type!r}")
         self.arch = arch
         self.dt = dtype
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
@@ -280,6 +282,16 @@ class CatSegEngine:
         qkv = torch.empty(1, 3 * D, device=dev, dtype=_f32)
         ops.gemm(h, ca.wqkv, qkv, bias=ca.bqkv, add=tg, add_ncols=2 * D)
         return qkv[0, D:2 * D].contiguous(), qkv[0, 2 * D:].contiguous()
+
+    def _class_attn(self, qkv, X, Y, *, B, T, HW, n_pad, ca):
+        """Y = X + AttentionLayer's attention over the classes (model.py:331-334,352): LinearAttention or,
+        for ATTENTION_TYPE "full", FullAttention.  qkv: the fused [q | k | v] projection rows."""
+        a, D = self.arch, self.arch.hidden_dim
+        kw = dict(B=B, T=T, HW=HW, n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
+                  k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+        if a.attention_type == "full":
+            return ops.full_attention(qkv, X, Y, **kw)
+        return ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, **kw)
 
     # ------------------------------------------------------------------ shared transformer block
     class _Fp8Linear:
@@ -577,7 +589,8 @@ class CatSegEngine:
                       and a.nheads == 4 and D == 128)
         gmap = rowmap(d1=T * HW, s1=HW, d2=1, m2=HW, s2=1)     # (b, t, p) -> (b, p)
         # the fused class attention holds one pixel's T <= 256 class rows on chip (pad_len bounds T)
-        fused_class = self.fused_class and dt == torch.bfloat16 and a.nheads == 4 and D == 128 and T <= 256
+        fused_class = (self.fused_class and dt == torch.bfloat16 and a.nheads == 4 and D == 128 and T <= 256 and
+                       a.attention_type == "linear")
         n_pad = a.pad_len - T if a.pad_len > 0 and T < a.pad_len else 0
         for l, lay in enumerate(w.layers):
             ops.layernorm(G3, lay.gnw, lay.gnb, gn)           # guidance_norm, once per image
@@ -614,9 +627,7 @@ class CatSegEngine:
                 else:
                     ops.rows_gemm(X, ca.wqkv, qkv, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
                                   add_ncols=2 * D)
-                    ops.linear_attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], X, Y, B=B, T=T, HW=HW,
-                                         n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
-                                         k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                    self._class_attn(qkv, X, Y, B=B, T=T, HW=HW, n_pad=n_pad, ca=ca)
                 # x + (x_pool + MLP(norm2(x_pool)))  (model.py:413,423)
                 ops.rows_mlp(Y, ca.w0, ca.b0, ca.w2, X, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Y,
                              res2=X, ref_rows=B * HW * (T + n_pad))
@@ -632,9 +643,7 @@ class CatSegEngine:
                     qkvp = qkv[:Rp]
                     ops.rows_gemm(Xp, ca.wqkv, qkvp, ln=(ca.n1w, ca.n1b), bias=ca.bqkv, add=tgqk[l], addmap=tmap,
                                   add_ncols=2 * D)
-                    ops.linear_attention(qkvp[:, :D], qkvp[:, D:2 * D], qkvp[:, 2 * D:], Xp, Yp, B=B, T=T,
-                                         HW=HWc, n_heads=a.nheads, head_dim=D // a.nheads, n_pad=n_pad,
-                                         k_pad=ca.get("kpad"), v_pad=ca.get("vpad"))
+                    self._class_attn(qkvp, Xp, Yp, B=B, T=T, HW=HWc, n_pad=n_pad, ca=ca)
                 ops.rows_mlp(Yp, ca.w0, ca.b0, ca.w2, Yp, ln=(ca.n2w, ca.n2b), b2=ca.b2, act=L.ACT_RELU, res=Yp)
                 ops.upsample_add_rows(Yp, X, S=S, Hp=H_ // ph, Wp=W_ // pw, C=D, H=H_, W=W_)
         del qkv, o, Y, gn, gqk

@@ -47,9 +47,15 @@ class CATSegPredictor(nn.Module):
         self.class_texts = self._load_json(train_class_json)
         self.test_class_texts = self._load_json(test_class_json) or self.class_texts
         if prompt_ensemble_type != "single":
-            raise NotImplementedError("MI355X path: PROMPT_ENSEMBLE_TYPE 'single' (the configs' setting) only")
-        if attention_type != "linear":
-            raise NotImplementedError("MI355X path: ATTENTION_TYPE 'linear' only")
+            # the reference's own eval text path cannot run these: its (T, P, 77) token stack
+            # (cat_seg_predictor.py:196-208) reaches CLIP.encode_text's 3-d permute (model_vpt.py:428)
+            # and raises (tests/golden/prompt_ensemble_probe.json, made by running the reference)
+            raise NotImplementedError(
+                f"PROMPT_ENSEMBLE_TYPE {prompt_ensemble_type!r}: only 'single' (the shipped configs' setting); "
+                "the reference's multi-template path raises in CLIP.encode_text (model_vpt.py:428)")
+        if attention_type not in ("linear", "full"):       # AttentionLayer (model.py:331-336)
+            raise NotImplementedError(f"ATTENTION_TYPE {attention_type!r}")
+        self.attention_type = attention_type
         if prompt_depth or prompt_length:
             raise NotImplementedError("MI355X path: visual prompt tuning (PROMPT_DEPTH/LENGTH) not supported")
         self.prompt_templates = ["A photo of a {} in the scene"]

@@ -275,6 +275,35 @@ def linear_attention(q, k, v, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_p
     return y
 
 
+def full_attention(qkv, x, y, *, B, T, HW, n_heads, head_dim, n_pad=0, k_pad=None, v_pad=None):
+    """ATTENTION_TYPE "full" (FullAttention, model.py:300-320): y = x + softmax(q k^T / sqrt(d)) v over
+    every pixel's T classes plus the n_pad learned padding tokens (model.py:397-410).
+    qkv: class-major rows (b*T + t)*HW + p, [q | k | v].  catseg_class_seq_pack -> catseg_attention
+    (mode 0, the MFMA flash kernel) -> catseg_class_seq_unpack_add."""
+    C_ = n_heads * head_dim
+    Lp = T + n_pad
+    n_seq = B * HW
+    packed = torch.empty(n_seq * Lp, 3 * C_, device=qkv.device, dtype=qkv.dtype)
+    o = torch.empty(n_seq * Lp, C_, device=qkv.device, dtype=qkv.dtype)
+    a = L.ClassSeqArgs()
+    a.qkv, a.ld_qkv = qkv.data_ptr(), _ld(qkv)
+    a.packed, a.ld_packed = packed.data_ptr(), _ld(packed)
+    a.o, a.ld_o = o.data_ptr(), _ld(o)
+    a.x, a.y, a.ld_xy = x.data_ptr(), y.data_ptr(), _ld(x)
+    assert _ld(y) == a.ld_xy and x.dtype == y.dtype == qkv.dtype
+    a.B, a.T, a.HW, a.C = B, T, HW, C_
+    a.n_pad, a.k_pad, a.v_pad = n_pad, _p(k_pad), _p(v_pad)
+    a.dtype = _dt(qkv)
+    es = qkv.element_size()
+    with _rec("class_seq_pack", 0, es * (B * T * HW + n_seq * Lp) * 3 * C_):
+        call("catseg_class_seq_pack", a, _stream())
+    attention(packed[:, :C_], packed[:, C_:2 * C_], packed[:, 2 * C_:], o, n_seq=n_seq, seq_len=Lp,
+              n_heads=n_heads, head_dim=head_dim, scale=head_dim ** -0.5)
+    with _rec("class_seq_unpack_add", 0, es * 3 * B * T * HW * C_):
+        call("catseg_class_seq_unpack_add", a, _stream())
+    return y
+
+
 def _conv_args(src1, weight, out, S, H, W, c1, s1_slice_stride, s1_offset, src2, c2, s2_slice_stride, s2_offset,
                src2_div, bias, act, gn, stats, stats_cpg, addend, addend_div):
     a = L.ConvArgs()

@@ -941,6 +941,8 @@ def head_train_forward(arch: CatSegArch, P: Dict[str, torch.Tensor], feats: torc
     of the model); feats [B*(1+G^2)][C_o] dense CLIP tokens, hooks 2 x [B*(1+G^2)][W_v] (the forward
     hooks of cat_seg_model.py:84-87), text [T][C_o] class embeddings.  Returns logits [B][T][4G][4G]."""
     a = arch
+    if a.attention_type != "linear":
+        raise NotImplementedError("training step: ATTENTION_TYPE 'linear' only (the full-attention backward is not built)")
     G = a.grid
     HW = G * G
     B = feats.shape[0] // (HW + 1)

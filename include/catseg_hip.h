@@ -200,6 +200,26 @@ typedef struct {
 } CatsegLinAttnArgs;
 int catseg_linear_attention(const CatsegLinAttnArgs* args, void* stream);
 
+/* catseg_class_seq_pack / catseg_class_seq_unpack_add — ATTENTION_TYPE "full" (FullAttention,
+ * model.py:289-320, in AttentionLayer model.py:331-334 and ClassTransformerLayer :387-424).
+ * The softmax itself is catseg_attention (mode 0, head_dim 32) over sequence-major rows:
+ *   pack:       qkv rows (b*T + t)*HW + p ([q | k | v], C columns each) -> packed rows
+ *               (b*HW + p)*(T + n_pad) + t; pad rows t >= T get q = 0, k = k_pad, v = v_pad
+ *               (the learned padding's constant projections, fp32, model.py:397-410)
+ *   unpack_add: y[(b*T + t)*HW + p] = x[same] + o[(b*HW + p)*(T + n_pad) + t], t < T
+ *               (the pad rows' outputs are discarded as in model.py:419-421; x/y may alias) */
+typedef struct {
+  const void* qkv; int64_t ld_qkv;
+  void* packed; int64_t ld_packed;
+  const void* o; int64_t ld_o;
+  const void* x; void* y; int64_t ld_xy;
+  int64_t B; int T; int HW; int C;
+  int n_pad; const float* k_pad; const float* v_pad;
+  int dtype;
+} CatsegClassSeqArgs;
+int catseg_class_seq_pack(const CatsegClassSeqArgs* args, void* stream);
+int catseg_class_seq_unpack_add(const CatsegClassSeqArgs* args, void* stream);
+
 /* ---------------------------------------------------------------------------
  * catseg_conv3x3 — 3x3 / pad 1 convolution as an MFMA implicit GEMM over NHWC.
  * Replaces nn.Conv2d of model.py:528,531 (DoubleConv), 616, 627 (guidance

@@ -240,6 +240,13 @@ def linear_attention(q: Tensor, k: Tensor, v: Tensor, eps: float = 1e-6) -> Tens
     return torch.einsum("nlhd,nhdv,nlh->nlhv", Q, KV, Z) * S
 
 
+def full_attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+    """FullAttention.forward (model.py:300-320), no masks, no dropout at eval.  q,k,v: (N, L, H, D)."""
+    QK = torch.einsum("nlhd,nshd->nlsh", q, k)
+    A = torch.softmax(QK / q.size(3) ** .5, dim=2)
+    return torch.einsum("nlsh,nshd->nlhd", A, v)
+
+
 def class_layer(x: Tensor, tguid: Tensor, sd, p: str, arch) -> Tensor:
     """ClassTransformerLayer.forward (model.py:387-424).  x: (B,C,T,H,W), tguid (B,T,C')."""
     B, C, T, H, W = x.shape
@@ -263,7 +270,8 @@ def class_layer(x: Tensor, tguid: Tensor, sd, p: str, arch) -> Tensor:
     q = _lin(torch.cat([xn, g], -1), sd, ap + "q.").reshape(-1, L, nh, C // nh)
     k = _lin(torch.cat([xn, g], -1), sd, ap + "k.").reshape(-1, L, nh, C // nh)
     v = _lin(xn, sd, ap + "v.").reshape(-1, L, nh, C // nh)
-    xp = xp + linear_attention(q, k, v).reshape(-1, L, C)
+    attn = full_attention if getattr(arch, "attention_type", "linear") == "full" else linear_attention
+    xp = xp + attn(q, k, v).reshape(-1, L, C)           # AttentionLayer (model.py:331-334,352)
     h = F.relu(_lin(_ln(xp, sd, p + "norm2."), sd, p + "MLP.0."))
     xp = xp + _lin(h, sd, p + "MLP.2.")
     xp = xp.reshape(B, Hp, Wp, L, C).permute(0, 3, 4, 1, 2).reshape(B * L, C, Hp, Wp)

@@ -125,7 +125,7 @@ def build_reference(arch, sd, pad_len=256):
         decoder_guidance_proj_dims=list(arch.decoder_guidance_proj_dims),
         num_layers=arch.num_layers, nheads=arch.nheads, hidden_dim=arch.hidden_dim,
         pooling_size=list(arch.pooling_size), feature_resolution=list(arch.feature_resolution),
-        window_size=arch.window_size, attention_type="linear", prompt_channel=1, pad_len=pad_len)
+        window_size=arch.window_size, attention_type=arch.attention_type, prompt_channel=1, pad_len=pad_len)
     agg_sd = {k[len(AGG_P):]: v for k, v in sd.items() if k.startswith(AGG_P)}
     missing, unexpected = agg.load_state_dict(agg_sd, strict=False)
     # the only non-parameter entries are the SW-MSA mask buffers (model.py:183)
@@ -414,6 +414,31 @@ def train_case(name, arch, T, seed=3, n_sub=256):
     save(name, **kw)
 
 
+def prompt_ensemble_probe():
+    """PROMPT_ENSEMBLE_TYPE "imagenet" / "imagenet_select" (cat_seg_predictor.py:80-83): the eval text
+    path stacks each class's P template token rows to (T, P, 77) (:196-208; squeeze(1) only drops
+    P = 1) and hands that to CLIP.encode_text (:214), whose NLD -> LND permute (model_vpt.py:428) is
+    3-d.  Runs the reference's own encode_text on such a tensor and records what it raises."""
+    import json
+    arch = TINY
+    sd = synthesize_state_dict(arch, seed=0)
+    clip, _, _, _ = build_reference(arch, sd)
+    T, P = 3, 80                                      # IMAGENET_TEMPLATES has 80 templates
+    toks = np.stack([rand_tokens(9 + t, P, arch.context_length, arch.vocab_size) for t in range(T)])
+    tokens = torch.from_numpy(toks).squeeze(1)        # cat_seg_predictor.py:208
+    rec = {"tokens_shape": list(tokens.shape), "raised": None, "error": None}
+    try:
+        with torch.no_grad():
+            out = clip.encode_text(tokens)
+        rec["output_shape"] = list(out.shape)
+    except Exception as e:  # noqa: BLE001 - the failure is the result
+        rec["raised"], rec["error"] = type(e).__name__, str(e)
+    path = os.path.join(HERE, "prompt_ensemble_probe.json")
+    with open(path, "w") as f:
+        json.dump(rec, f, indent=1)
+    print("wrote", path, rec)
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "train":
         torch.set_num_threads(8)
@@ -430,6 +455,18 @@ def main():
         l14_case("e2e_l14_ade150", "ade150", [(336, 336), (300, 336)], seed=21)
         # config 4 class count: ade847 prompts -> top-256 + -100 scatter, one image
         l14_case("e2e_l14_ade847", "ade847", [(336, 336)], seed=22, sub=6)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "ensemble":
+        prompt_ensemble_probe()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "full":
+        torch.set_num_threads(8)
+        # ATTENTION_TYPE "full" (FullAttention, model.py:289-320): T=10 < pad_len=16 with pooling
+        # (2,2) (pad keys + pooled class attention), and T=20 with the eval pooling (1,1) padded to
+        # the default pad_len 256, B=2
+        full = TINY.replace(attention_type="full")
+        e2e_case("e2e_tiny_full_pad", full.replace(pooling_size=(2, 2)), 10, [(300, 352)], seed=7, pad_len=16)
+        e2e_case("e2e_tiny_full_eval", full, 20, [(384, 384), (352, 384)], seed=8)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "sliding":
         torch.set_num_threads(8)

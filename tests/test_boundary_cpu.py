@@ -38,6 +38,31 @@ def test_config_base_and_overrides():
     assert cfg.TEST.SLIDING_WINDOW is False
 
 
+def test_attention_type_config_key_reaches_the_arch():
+    """MODEL.SEM_SEG_HEAD.ATTENTION_TYPE (config.py:86) selects AttentionLayer's attention
+    (model.py:331-336): "linear" and "full" build; anything else fails as the reference does."""
+    from cat_seg.arch import arch_from_cfg
+    assert arch_from_cfg(tiny_cfg()).attention_type == "linear"
+    cfg = tiny_cfg(**{"MODEL.SEM_SEG_HEAD.ATTENTION_TYPE": "full"})
+    assert arch_from_cfg(cfg).attention_type == "full"
+    assert build_model(cfg).sem_seg_head.predictor.attention_type == "full"
+    with pytest.raises(NotImplementedError):
+        build_model(tiny_cfg(**{"MODEL.SEM_SEG_HEAD.ATTENTION_TYPE": "softmax"}))
+
+
+def test_prompt_ensemble_imagenet_refused_like_the_reference_fails():
+    """PROMPT_ENSEMBLE_TYPE "imagenet" (cat_seg_predictor.py:80-83): the reference's eval text path
+    raises in CLIP.encode_text on its (T, 80, 77) token stack (probe fixture made by running the
+    reference's encode_text, tests/golden/make_golden.py ensemble); the build refuses it up front."""
+    import json
+    from conftest import GOLDEN
+    rec = json.load(open(os.path.join(GOLDEN, "prompt_ensemble_probe.json")))
+    assert rec["tokens_shape"][1] == 80 and rec["raised"] == "RuntimeError"
+    for kind in ("imagenet", "imagenet_select"):
+        with pytest.raises(NotImplementedError, match="encode_text"):
+            build_model(tiny_cfg(**{"MODEL.PROMPT_ENSEMBLE_TYPE": kind}))
+
+
 def test_vit_fp8_config_key_reaches_the_model():
     assert build_model(tiny_cfg()).vit_fp8 is False
     m = build_model(tiny_cfg(**{"MODEL.CATSEG_HIP.DTYPE": "bf16", "MODEL.CATSEG_HIP.VIT_FP8": "True"}))

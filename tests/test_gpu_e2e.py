@@ -34,7 +34,10 @@ def batch_raw(imgs, div=32):
 # fp32 gate: 1e-3 (BASELINE.md parity gates); bf16 gate: max-abs 5e-2, mean-abs 5e-3
 CASES = {"e2e_tiny_pad": TINY, "e2e_tiny_eval": TINY, "e2e_tiny_topk": TINY,
          "e2e_tiny_topk_pool": TINY.replace(pooling_size=(2, 2)),          # POOLING [2,2] + top-k
-         "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2))}            # config 1 (yaml default pooling)
+         "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2)),            # config 1 (yaml default pooling)
+         # ATTENTION_TYPE "full" (FullAttention, model.py:289-320): pad keys + pooling, and pad_len 256
+         "e2e_tiny_full_pad": TINY.replace(attention_type="full", pooling_size=(2, 2)),
+         "e2e_tiny_full_eval": TINY.replace(attention_type="full")}
 
 
 @pytest.mark.parametrize("name", list(CASES))

@@ -497,6 +497,29 @@ def test_linear_attention(dt, T, n_pad):
     close(y, x.to(dt).double() + o, atol=2e-5 if dt == torch.float32 else 3e-2, what="linattn")
 
 
+# ----------------------------------------------------------------------------- full class attention
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T,n_pad", [(20, 236), (150, 106), (256, 0), (37, 0), (10, 6)])
+def test_full_class_attention(dt, T, n_pad):
+    """ATTENTION_TYPE "full": pack -> MFMA flash attention (mode 0, head_dim 32) -> unpack + residual,
+    against FullAttention (model.py:300-320) in fp64 over the padded class axis."""
+    B, HW, D = 2, 9, 128
+    qkv = rnd(B * T * HW, 3 * D, seed=24)
+    x = rnd(B * T * HW, D, seed=25)
+    kp, vp = rnd(D, seed=26), rnd(D, seed=27)
+    qd, xd = qkv.to(dev, dt), x.to(dev, dt)
+    y = torch.empty_like(xd)
+    ops.full_attention(qd, xd, y, B=B, T=T, HW=HW, n_heads=4, head_dim=32, n_pad=n_pad, k_pad=kp.to(dev),
+                       v_pad=vp.to(dev))
+    z = qkv.to(dt).double().reshape(B, T, HW, 3, 4, 32).permute(3, 0, 2, 1, 4, 5).reshape(3, B * HW, T, 4, 32)
+    q, k, v = z[0], z[1], z[2]
+    if n_pad:
+        k = torch.cat([k, kp.to(dt).double().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+        v = torch.cat([v, vp.to(dt).double().reshape(1, 1, 4, 32).expand(B * HW, n_pad, 4, 32)], 1)
+    o = O.full_attention(q, k, v).reshape(B, HW, T, D).permute(0, 2, 1, 3).reshape(-1, D)
+    close(y, x.to(dt).double() + o, atol=2e-5 if dt == torch.float32 else 3e-2, what="fullattn")
+
+
 @pytest.mark.parametrize("T,n_pad,per_image", [(150, 106, False), (20, 236, False), (256, 0, True), (37, 0, False),
                                                (33, 5, True)])
 def test_class_attention_fused(T, n_pad, per_image):

@@ -18,6 +18,9 @@ CASES = {
     "e2e_tiny_eval": TINY,
     "e2e_tiny_topk": TINY,
     "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2)),
+    # ATTENTION_TYPE "full" (FullAttention, model.py:289-320)
+    "e2e_tiny_full_pad": TINY.replace(attention_type="full", pooling_size=(2, 2)),
+    "e2e_tiny_full_eval": TINY.replace(attention_type="full"),
 }
 
 

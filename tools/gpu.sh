@@ -84,6 +84,7 @@ case "$CMD" in
   pmc) pmc "$@" ;;
   sq) sq "$@" ;;
   micro) micro "$@" ;;
+  smoke) smoke ;;
   final) tests && smoke && bench && configs && trace && pmc "$@" && sq ;;
   final1) tests && smoke && bench --cpu-images -1 && configs ;;
   final2) trace && pmc "$@" && sq && train ;;
