@@ -51,6 +51,10 @@ class CatSegArch:
     # ClassTransformerLayer attention (model.py:324-334): "linear" (LinearAttention, every shipped
     # config) or "full" (FullAttention, softmax over the padded class axis)
     attention_type: str = "linear"
+    # ---- visual prompt tuning (model_vpt.py:243-265): PROMPT_LENGTH learned tokens per layer joined
+    # after CLS for the first PROMPT_DEPTH vision blocks (cat_seg_predictor.py:76, clip.load) ----
+    prompt_depth: int = 0
+    prompt_length: int = 0
     # ---- image preprocessing (config.py:36,67-68) ----
     size_divisibility: int = 32
     clip_pixel_mean: Tuple[float, float, float] = (122.7709383, 116.7460125, 104.09373615)
@@ -77,6 +81,11 @@ class CatSegArch:
     @property
     def n_tokens(self) -> int:
         return self.grid * self.grid + 1
+
+    @property
+    def vpt(self) -> int:
+        """Prompt rows per vision sequence (0: no visual prompt tuning)."""
+        return self.prompt_length if self.prompt_length > 0 and self.prompt_depth > 0 else 0
 
     @property
     def text_guidance_dim(self) -> int:
@@ -128,6 +137,8 @@ def arch_from_cfg(cfg) -> CatSegArch:
         feature_resolution=tuple(int(p) for p in head.FEATURE_RESOLUTION),
         window_size=int(head.WINDOW_SIZES),
         attention_type=str(getattr(head, "ATTENTION_TYPE", "linear")),
+        prompt_depth=int(getattr(head, "PROMPT_DEPTH", 0)),
+        prompt_length=int(getattr(head, "PROMPT_LENGTH", 0)),
         text_guidance_proj_dim=int(head.TEXT_GUIDANCE_PROJ_DIM),
         appearance_guidance_proj_dim=int(head.APPEARANCE_GUIDANCE_PROJ_DIM),
         decoder_dims=tuple(head.DECODER_DIMS),

@@ -56,7 +56,13 @@ class CatSegEngine:
             raise NotImplementedError("HIP path: hidden_dim 128 / 4 heads only")
         if arch.attention_type not in ("linear", "full"):     # AttentionLayer (model.py:331-336)
             raise NotImplementedError(f"ATTENTION_TYPE {arch.attention_type!r}")
+        if arch.prompt_length > 0 and arch.prompt_depth < arch.vision_layers:
+            # every vision block drops PROMPT_LENGTH rows after CLS (model_vpt.py:213-214, 238-239) but only
+            # the first PROMPT_DEPTH insert them (:258-259): past the depth the reference drops patch tokens
+            raise NotImplementedError("visual prompt tuning needs PROMPT_DEPTH >= the vision layer count "
+                                      "(the reference's blocks past the depth drop patch tokens)")
         self.arch = arch
+        self._cache = {}
         self.dt = dtype
         self.fused_swin = True          # bf16: fused norm1 + q/k/v + window attention (A/B switch)
         self.fused_class = True         # bf16: fused norm1 + q/k/v + linear class attention (A/B switch)
@@ -193,6 +199,9 @@ class CatSegEngine:
                      for i in range(a.vision_layers)]
         w.ln_post = (self._F(sd[p + "ln_post.weight"]), self._F(sd[p + "ln_post.bias"]))
         w.proj_t = self._W(sd[p + "proj"].t())
+        # visual prompt tokens (model_vpt.py:252): one fp32 row of P*W per layer
+        w.vpt = (self._F(sd[p + "transformer.prompt_tokens"]).reshape(a.prompt_depth, -1).contiguous()
+                 if a.vpt else None)
         # ---------------- CLIP text ----------------
         w.tok_emb = self._F(sd[CLIP + "token_embedding.weight"])
         w.tpos = self._F(sd[CLIP + "positional_embedding"])
@@ -326,7 +335,8 @@ class CatSegEngine:
             return fp8_lin(a, blk["q8_" + name], out, **kw)
         return ops.gemm(a, blk[name], out, **kw)
 
-    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None, fp8=False, l2s=False):
+    def _resblocks(self, x, blocks, n_seq, seq_len, n_heads, causal, hooks_at=(), hooks=None, fp8=False, l2s=False,
+                   prompts=None):
         """ResidualAttentionBlock.forward over a stack (model_vpt.py:208-217, 256-266).  l2s: the blocks'
         q projections carry scale * log2(e) (_block heads > 0): attention mode 2."""
         M, width = x.shape
@@ -338,6 +348,8 @@ class CatSegEngine:
         f8 = self._Fp8Linear(M, width, dev) if fp8 else None
         fresh = False
         for i, blk in enumerate(blocks):
+            if prompts is not None and i < self.arch.prompt_depth:
+                prompts(i, x)                        # this block's visual prompt rows (model_vpt.py:258-259)
             self._ln_linear(f8, x, blk.ln1w, blk.ln1b, h, blk, "wqkv", qkv, bias=blk.bqkv)
             ops.attention(qkv[:, :width], qkv[:, width:2 * width], qkv[:, 2 * width:], o,
                           n_seq=n_seq, seq_len=seq_len, n_heads=n_heads, head_dim=width // n_heads,
@@ -428,6 +440,34 @@ class CatSegEngine:
         ops.vit_embed(patches, w.cls, w.pos, *w.ln_pre, x, B=B, G2=G2, width=W)
         return x
 
+    @property
+    def vision_seq_len(self) -> int:
+        """Rows per image of the vision residual stream: CLS + grid^2 tokens (+ the PROMPT_LENGTH visual
+        prompt rows, kept at the END of each sequence: the blocks mix tokens only through attention,
+        which is order-free over keys, so their position changes no result beyond summation order)."""
+        a = self.arch
+        return a.grid * a.grid + 1 + a.vpt
+
+    def _vpt_rows(self, x, B):
+        """Visual prompt tuning (model_vpt.py:255-265): the (B*(1+HW), W) embedded rows moved into a
+        (B*(1+HW+P), W) stream, and the prompt writer run before each block i < PROMPT_DEPTH (the
+        reference's cat after CLS + drop after the block; the rows of a block's prompts are rewritten
+        by the next block's, so nothing is dropped here).  Both copies are catseg_gather_rows."""
+        a, dev, W, P = self.arch, self.device, self.arch.vision_width, self.arch.vpt
+        L0 = a.grid * a.grid + 1
+        Ls = L0 + P
+        xs = torch.empty(B * Ls, W, device=dev, dtype=_f32)
+        key = ("vpt_idx", B)
+        if key not in self._cache:
+            self._cache[key] = (torch.arange(B, device=dev, dtype=torch.int32),
+                                torch.zeros(B, device=dev, dtype=torch.int32))
+        ar, zero = self._cache[key]
+        ops.gather_rows(x.view(B, L0 * W), ar, xs.view(B, Ls * W)[:, :L0 * W])
+
+        def write(i, stream_rows):
+            ops.gather_rows(self.w.vpt[i:i + 1], zero, stream_rows.view(B, Ls * W)[:, L0 * W:])
+        return xs, write
+
     def embed_text(self, tokens: torch.Tensor) -> torch.Tensor:
         """CLIP.encode_text up to the transformer (model_vpt.py:421-427): token + positional embedding.
         tokens (n, ctx) int32 on the device.  Returns fp32 (n*ctx, text_width) rows."""
@@ -441,12 +481,16 @@ class CatSegEngine:
         sizes (B,2) int32 valid (h, w).  Returns feats fp32 (B*L, C_o), [hook0, hook1] fp32 (B*L, W)."""
         a, dev, dt, w = self.arch, self.device, self.dt, self.w
         B = raw.shape[0]
-        Lt = a.grid * a.grid + 1
+        Lt = self.vision_seq_len
         W = a.vision_width
         x = self.embed_image(raw, sizes)
+        vpt = None
+        if a.vpt:
+            x, vpt = self._vpt_rows(x, B)
         hooks: List[torch.Tensor] = []
         x = self._resblocks(x, w.vblocks[:-1], B, Lt, a.vision_heads, False,
-                            hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8, l2s=self.vit_l2s)
+                            hooks_at=set(a.hook_layers), hooks=hooks, fp8=self.vit_fp8, l2s=self.vit_l2s,
+                            prompts=vpt)
         if a.vision_layers - 1 in a.hook_layers:
             raise NotImplementedError("hook on the dense block")
         # forward_dense (model_vpt.py:219-240)
@@ -491,8 +535,9 @@ class CatSegEngine:
         a, dev, dt, w = self.arch, self.device, self.dt, self.w
         G = a.grid
         HW = G * G
-        B = feats.shape[0] // (HW + 1)
-        drop_cls = rowmap(d1=HW, s1=HW + 1, d2=1, m2=HW, s2=1, off=1)
+        Ls = self.vision_seq_len
+        B = feats.shape[0] // Ls
+        drop_cls = rowmap(d1=HW, s1=Ls, d2=1, m2=HW, s2=1, off=1)
         res3 = torch.empty(B * HW, a.embed_dim, device=dev, dtype=dt)
         ops.convert(feats, res3, inmap=drop_cls)
         res45 = []
@@ -513,7 +558,7 @@ class CatSegEngine:
         a, dev, dt, w, tx = self.arch, self.device, self.dt, self.w, self._text
         G = a.grid
         HW = G * G
-        Lt = HW + 1
+        Lt = self.vision_seq_len
         B = feats.shape[0] // Lt
         D = a.hidden_dim
         Co = a.embed_dim

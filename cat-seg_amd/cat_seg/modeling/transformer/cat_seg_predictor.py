@@ -56,8 +56,9 @@ class CATSegPredictor(nn.Module):
         if attention_type not in ("linear", "full"):       # AttentionLayer (model.py:331-336)
             raise NotImplementedError(f"ATTENTION_TYPE {attention_type!r}")
         self.attention_type = attention_type
-        if prompt_depth or prompt_length:
-            raise NotImplementedError("MI355X path: visual prompt tuning (PROMPT_DEPTH/LENGTH) not supported")
+        # visual prompt tuning (PROMPT_DEPTH / PROMPT_LENGTH, model_vpt.py:243-265) reaches the engine through
+        # the arch (arch_from_cfg); CatSegEngine refuses a depth below the vision layer count
+        self.prompt_depth, self.prompt_length = int(prompt_depth), int(prompt_length)
         self.prompt_templates = ["A photo of a {} in the scene"]
         self.clip_pretrained = clip_pretrained
         self.bpe_vocab = bpe_vocab

@@ -899,6 +899,8 @@ def clip_image_train_forward(arch: CatSegArch, P: Dict[str, torch.Tensor], eng, 
     mode (cat_seg_model.py:58-75): the engine computes it without a graph.
     Returns feats [B*(1+G^2)][C_o] and the two hook outputs [B*(1+G^2)][W]."""
     from .weights import CLIP
+    if arch.vpt:
+        raise NotImplementedError("training step: visual prompt tuning (CLIP_FINETUNE 'prompt') is not built")
     B = raw.shape[0]
     L_ = arch.grid * arch.grid + 1
     x = eng.embed_image(raw, sizes)
@@ -941,6 +943,9 @@ def head_train_forward(arch: CatSegArch, P: Dict[str, torch.Tensor], feats: torc
     of the model); feats [B*(1+G^2)][C_o] dense CLIP tokens, hooks 2 x [B*(1+G^2)][W_v] (the forward
     hooks of cat_seg_model.py:84-87), text [T][C_o] class embeddings.  Returns logits [B][T][4G][4G]."""
     a = arch
+    if a.vpt:
+        raise NotImplementedError("training step: visual prompt tuning is not built (frozen-CLIP features "
+                                  "carry the prompt rows)")
     if a.attention_type != "linear":
         raise NotImplementedError("training step: ATTENTION_TYPE 'linear' only (the full-attention backward is not built)")
     G = a.grid

@@ -95,6 +95,8 @@ def synthesize_state_dict(arch: CatSegArch, seed: int = 0) -> Dict[str, torch.Te
     s.norm(CLIP + "visual.ln_pre.", W)
     for i in range(a.vision_layers):
         _clip_block(s, f"{CLIP}visual.transformer.resblocks.{i}.", W)
+    if a.prompt_length > 0:          # Transformer.prompt_tokens (model_vpt.py:252), VPT only
+        s.const_noise(CLIP + "visual.transformer.prompt_tokens", (a.prompt_depth, a.prompt_length, W), 0.0, 1.0)
     s.norm(CLIP + "visual.ln_post.", W)
     s.unit(CLIP + "visual.proj", (W, a.embed_dim), W)
     # ---------------- CLIP text (model_vpt.py:380-438) ----------------

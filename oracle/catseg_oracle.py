@@ -113,12 +113,18 @@ def encode_image_dense(arch, sd, img: Tensor) -> Tuple[Tensor, List[Tensor]]:
     x = _ln(x + pos, sd, p + "ln_pre.")
     x = x.permute(1, 0, 2)
     hooks = []
+    P = getattr(arch, "prompt_length", 0)
     for i in range(arch.vision_layers):
         bp = f"{p}transformer.resblocks.{i}."
+        if P > 0 and i < arch.prompt_depth:      # Transformer.forward (model_vpt.py:258-259): after CLS
+            pt = sd[p + "transformer.prompt_tokens"][i].unsqueeze(1).expand(P, x.shape[1], -1)
+            x = torch.cat([x[:1], pt, x[1:]], dim=0)
         if i == arch.vision_layers - 1:
             x = resblock_dense(x, sd, bp)
         else:
             x = resblock(x, sd, bp, arch.vision_heads)
+        if P > 0:                                # every block drops rows 1..P (model_vpt.py:213-214,238-239)
+            x = torch.cat([x[:1], x[P + 1:]], dim=0)
         if i in arch.hook_layers:
             hooks.append(x)
     x = _ln(x.permute(1, 0, 2), sd, p + "ln_post.")

@@ -114,7 +114,7 @@ def build_reference(arch, sd, pad_len=256):
     clip = model_vpt.CLIP(
         arch.embed_dim, arch.vision_pretrain_res, arch.vision_layers, arch.vision_width,
         arch.vision_patch, arch.context_length, arch.vocab_size, arch.text_width,
-        arch.text_heads, arch.text_layers)
+        arch.text_heads, arch.text_layers, prompt_depth=arch.prompt_depth, prompt_length=arch.prompt_length)
     clip_sd = {k[len(CLIP_P):]: v for k, v in sd.items() if k.startswith(CLIP_P)}
     clip.load_state_dict(clip_sd, strict=True)
     agg = agg_mod.Aggregator(
@@ -458,6 +458,13 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "ensemble":
         prompt_ensemble_probe()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "vpt":
+        torch.set_num_threads(8)
+        # visual prompt tuning (model_vpt.py:243-265): 3 prompt tokens in every one of TINY's 4 vision
+        # blocks (PROMPT_DEPTH = the layer count), T=10 < pad_len=16, two ragged images
+        vpt = TINY.replace(prompt_depth=4, prompt_length=3)
+        e2e_case("e2e_tiny_vpt", vpt, 10, [(300, 352), (320, 256)], seed=9, pad_len=16)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "full":
         torch.set_num_threads(8)

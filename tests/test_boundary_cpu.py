@@ -5,6 +5,8 @@ import re
 
 import numpy as np
 import pytest
+
+from cat_seg.weights import CLIP
 import torch
 
 from cat_seg import CATSeg, add_cat_seg_config, build_model, get_cfg
@@ -61,6 +63,23 @@ def test_prompt_ensemble_imagenet_refused_like_the_reference_fails():
     for kind in ("imagenet", "imagenet_select"):
         with pytest.raises(NotImplementedError, match="encode_text"):
             build_model(tiny_cfg(**{"MODEL.PROMPT_ENSEMBLE_TYPE": kind}))
+
+
+def test_visual_prompt_config_keys_reach_the_arch():
+    """MODEL.SEM_SEG_HEAD.PROMPT_DEPTH / PROMPT_LENGTH (config.py:88-89, clip.load prompt args,
+    model_vpt.py:243-265): the arch carries them, the synthesized state dict gets the reference's
+    visual.transformer.prompt_tokens (depth, length, width) parameter, and CLIP_FINETUNE 'prompt'
+    leaves exactly those trainable."""
+    from cat_seg.arch import arch_from_cfg
+    from cat_seg.weights import synthesize_state_dict
+    cfg = tiny_cfg(**{"MODEL.SEM_SEG_HEAD.PROMPT_DEPTH": "4", "MODEL.SEM_SEG_HEAD.PROMPT_LENGTH": "3"})
+    arch = arch_from_cfg(cfg)
+    assert (arch.prompt_depth, arch.prompt_length, arch.vpt) == (4, 3, 3)
+    assert arch_from_cfg(tiny_cfg()).vpt == 0
+    sd = synthesize_state_dict(arch)
+    assert sd[CLIP + "visual.transformer.prompt_tokens"].shape == (4, 3, arch.vision_width)
+    m = build_model(cfg)
+    assert m.sem_seg_head.predictor.prompt_length == 3
 
 
 def test_vit_fp8_config_key_reaches_the_model():

@@ -37,7 +37,10 @@ CASES = {"e2e_tiny_pad": TINY, "e2e_tiny_eval": TINY, "e2e_tiny_topk": TINY,
          "e2e_b16_voc20": VIT_B16.replace(pooling_size=(2, 2)),            # config 1 (yaml default pooling)
          # ATTENTION_TYPE "full" (FullAttention, model.py:289-320): pad keys + pooling, and pad_len 256
          "e2e_tiny_full_pad": TINY.replace(attention_type="full", pooling_size=(2, 2)),
-         "e2e_tiny_full_eval": TINY.replace(attention_type="full")}
+         "e2e_tiny_full_eval": TINY.replace(attention_type="full"),
+         # visual prompt tuning (model_vpt.py:243-265): 3 prompts in each of the 4 vision blocks; the
+         # fp32 gate (1e-3) is 13x below the prompts' effect on these logits (1.3e-2 without them)
+         "e2e_tiny_vpt": TINY.replace(prompt_depth=4, prompt_length=3)}
 
 
 @pytest.mark.parametrize("name", list(CASES))

@@ -21,6 +21,8 @@ CASES = {
     # ATTENTION_TYPE "full" (FullAttention, model.py:289-320)
     "e2e_tiny_full_pad": TINY.replace(attention_type="full", pooling_size=(2, 2)),
     "e2e_tiny_full_eval": TINY.replace(attention_type="full"),
+    # visual prompt tuning (model_vpt.py:243-265): 3 prompts in each of the 4 vision blocks
+    "e2e_tiny_vpt": TINY.replace(prompt_depth=4, prompt_length=3),
 }
 
 

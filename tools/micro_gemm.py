@@ -17,6 +17,7 @@ variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,5").spli
 M = 8 * 577
 shapes = {"qkv": (3072, 1024, L.ACT_NONE, False), "proj": (1024, 1024, L.ACT_NONE, True),
           "fc1": (4096, 1024, L.ACT_QUICKGELU, False), "fc2": (1024, 4096, L.ACT_NONE, True),
+          "fc2h": (1024, 2048, L.ACT_NONE, True),   # half of fc2's K (split-K probe: run at 2 M for 2 halves)
           "sq4k": (4096, 4096, L.ACT_NONE, False), "sq8k": (8192, 8192, L.ACT_NONE, False)}
 # MG_SHAPES=qkv,fc1,sq4k selects shapes (sq4k: M = N = K = 4096, the guide's reference size)
 sel = os.environ.get("MG_SHAPES", "qkv,proj,fc1,fc2").split(",")
