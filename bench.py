@@ -88,6 +88,10 @@ def parse():
                     help="seconds before a rendezvous or collective that has not completed fails the run (N > 1)")
     ap.add_argument("--vit-fp8", action="store_true",
                     help="e4m3 CLIP image-encoder GEMMs (config 5's setting) on another config")
+    ap.add_argument("--attention-type", default="linear", choices=["linear", "full"],
+                    help="MODEL.SEM_SEG_HEAD.ATTENTION_TYPE of the class aggregation (model.py:331-334)")
+    ap.add_argument("--prompt-length", type=int, default=0,
+                    help="visual prompt tuning: PROMPT_LENGTH tokens in every vision block (PROMPT_DEPTH = layers)")
     return ap.parse_args()
 
 
@@ -151,6 +155,14 @@ def main():
     cfg = CONFIGS[args.config]
     cfg5 = args.config == 5
     arch = cfg["arch"]
+    # the optional heads (not the reference configs' settings): a variant of the config, named in the line
+    variant = []
+    if args.attention_type != "linear":
+        arch = arch.replace(attention_type=args.attention_type)
+        variant.append(f"ATTENTION_TYPE {args.attention_type}")
+    if args.prompt_length:
+        arch = arch.replace(prompt_depth=arch.vision_layers, prompt_length=args.prompt_length)
+        variant.append(f"visual prompts {args.prompt_length} x {arch.vision_layers} layers")
     B = args.batch or cfg["B"]
     T = args.classes or cfg["T"]
     dname = args.dtype or cfg["dtype"]
@@ -264,7 +276,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     boundary = None
-    if rank == 0 and world == 1 and not cfg5 and not args.no_boundary and args.config == 3:
+    if rank == 0 and world == 1 and not cfg5 and not args.no_boundary and args.config == 3 and not variant:
         boundary = boundary_pass(cfg, B, S, T, args.steps, args.warmup, value)
     roofline, kernels = None, None
     if rank == 0 and not args.no_roofline:
@@ -291,7 +303,8 @@ def main():
                                     f"{5 * B} crops through ViT-L/14@336, T={T} (top-256 per crop), "
                                     "Fold/avg merge to 640² probabilities" if cfg5 else
                                     f"CATSeg eval forward {arch.name}, T={T} classes, bs={B}/GPU, "
-                                    f"POOLING [1,1], sigmoid upsampled to {R}x{R}"),
+                                    f"POOLING [1,1], sigmoid upsampled to {R}x{R}"
+                                    + "".join(f", {v}" for v in variant)),
                        "bench_config": args.config,
                        "global_batch": world * B, "classes": T, "resolution": R,
                        "parallelism": f"batch-shard x{world} + {backend} all-gather of logits" if world > 1 else "1 GPU",
@@ -301,7 +314,7 @@ def main():
             "boundary": boundary,
             # the whole path's fraction of the dtype's dense peak; None with fp8 ViT GEMMs (a mix of
             # fp8 and bf16 work has no single roof)
-            "path_roofline": None if vit_fp8 else {
+            "path_roofline": None if vit_fp8 or variant else {
                 "bound": "mfma", "achieved": round(path_tflops, 2), "peak": path_peak,
                 "unit": "TFLOP/s", "gf_per_image": cfg["gf"], "frac": round(path_tflops / path_peak, 4)},
             "cpu_baseline": cpu,
