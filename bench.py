@@ -404,13 +404,48 @@ def pmc_traffic(family, bench_config=3):
     return fam["traffic_bytes_per_launch"], os.path.relpath(f, ROOT), bool(same)
 
 
-def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
-    """One eager pass with HIP events around every wrapped launch (on the launch stream)."""
+def _queued_profile(step, stream):
+    """The eager step with HIP events around every wrapped launch, timed from a full queue.
+
+    Events around an eager launch also measure the host's time to enqueue it (Python + ctypes,
+    10-30 us) whenever the GPU runs ahead of the host -- a 10 us kernel can read 25 us.  So a first
+    pass measures the host's enqueue time of the whole step, and the recorded pass is enqueued behind
+    a spin kernel (torch.cuda._sleep) that holds the stream for about twice that long: the launches
+    then run back to back exactly as in the replayed graph, and every event pair brackets GPU time
+    only.  Returns (records, timing note, gap fraction: idle share of the recorded span)."""
     ops.PROFILE = []
     with torch.no_grad(), torch.cuda.stream(stream):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         step()
+        host_s = time.perf_counter() - t0
     torch.cuda.synchronize()
     recs, ops.PROFILE = ops.PROFILE, None
+    note = "eager, host-paced"
+    if hasattr(torch.cuda, "_sleep"):
+        with torch.cuda.stream(stream):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            torch.cuda._sleep(2_000_000)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        cyc_per_ms = 2_000_000 / max(e0.elapsed_time(e1), 1e-3)
+        ops.PROFILE = []
+        with torch.no_grad(), torch.cuda.stream(stream):
+            torch.cuda._sleep(int(cyc_per_ms * (2e3 * host_s + 20.0)))
+            step()
+        torch.cuda.synchronize()
+        recs, ops.PROFILE = ops.PROFILE, None
+        note = f"queued behind a {2e3 * host_s + 20:.0f} ms spin kernel (host enqueue {host_s * 1e3:.0f} ms)"
+    busy = sum(r["start"].elapsed_time(r["end"]) for r in recs)
+    span = recs[0]["start"].elapsed_time(recs[-1]["end"]) if recs else 0.0
+    return recs, note, (round(1.0 - busy / span, 4) if span > 0 else None)
+
+
+def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
+    """One eager pass with HIP events around every wrapped launch (on the launch stream), enqueued
+    behind a spin kernel so that the events bracket GPU time only (_queued_profile)."""
+    recs, timing, gap = _queued_profile(step, stream)
     agg = {}
     for r in recs:
         ms = r["start"].elapsed_time(r["end"])
@@ -425,7 +460,8 @@ def roofline_pass(step, stream, dtype, vit_fp8=False, bench_config=3):
     avg_s = a["ms"] / a["launches"] / 1e3
     traffic, tsrc, tsame = pmc_traffic(top, bench_config)
     common = {"launches": a["launches"], "avg_launch_us": round(avg_s * 1e6, 2), "traffic": traffic,
-              "traffic_source": tsrc, "traffic_same_build": tsame, "lib_sha16": lib_sha16()}
+              "traffic_source": tsrc, "traffic_same_build": tsame, "lib_sha16": lib_sha16(),
+              "timing": timing, "idle_frac_of_span": gap}
     if a["flops"] > 0:
         achieved = a["flops"] / a["launches"] / avg_s / 1e12
         peak = (PEAK_FP8_TFLOPS if top == "gemm_fp8" else
