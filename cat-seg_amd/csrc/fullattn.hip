@@ -11,7 +11,8 @@
 //                rows get k_pad / v_pad (their queries are zero: the reference discards the pad
 //                rows' outputs, :419-421, so their values never matter)
 //   unpack_add:  y[(b, t, p)] = x[(b, t, p)] + o[(b, p, t)] for t < T (the residual, :413)
-// One thread per 4 columns of a row; a wave covers whole rows, so both sides stay coalesced.
+// pack: one thread per 16-byte chunk of a row; unpack: one thread per 4 columns.  A wave covers whole
+// rows, so both sides stay coalesced.
 #include "common.h"
 #include "capi.h"
 
@@ -19,28 +20,29 @@ namespace {
 
 template <typename E>
 __global__ __launch_bounds__(256) void class_seq_pack_kernel(CatsegClassSeqArgs a, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int g3 = 3 * a.C / 4;                   // 4-column groups per [q | k | v] row
-  const int Lp = a.T + a.n_pad;
-  const int64_t pr = i / g3;
-  const int col = (int)(i % g3) * 4;
-  const int64_t seq = pr / Lp;
-  const int t = (int)(pr % Lp);
-  const int64_t b = seq / a.HW;
-  const int p = (int)(seq % a.HW);
-  float v[4];
+  // one 16-byte chunk per thread (8 bf16 / 4 fp32); 32-bit index math (host-checked n < 2^31)
+  constexpr int VN = 16 / sizeof(E);
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= (unsigned)n) return;
+  const unsigned g3 = 3u * (unsigned)a.C / VN;   // chunks per [q | k | v] row
+  const unsigned Lp = (unsigned)(a.T + a.n_pad);
+  const unsigned pr = i / g3;
+  const int col = (int)(i - pr * g3) * VN;
+  const unsigned seq = pr / Lp;
+  const int t = (int)(pr - seq * Lp);
+  const unsigned b = seq / (unsigned)a.HW;
+  const int p = (int)(seq - b * (unsigned)a.HW);
+  E* dst = reinterpret_cast<E*>(a.packed) + (int64_t)pr * a.ld_packed + col;
   if (t < a.T) {
-    load4<E>(reinterpret_cast<const E*>(a.qkv) + ((b * a.T + t) * a.HW + p) * a.ld_qkv + col, v);
+    const E* src = reinterpret_cast<const E*>(a.qkv) + (((int64_t)b * a.T + t) * a.HW + p) * a.ld_qkv + col;
+    st16(dst, ld16(src));
   } else if (col < a.C) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = 0.f;
+    st16(dst, make_uint4(0u, 0u, 0u, 0u));
   } else {
     const float* src = col < 2 * a.C ? a.k_pad + (col - a.C) : a.v_pad + (col - 2 * a.C);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = src[e];
+    for (int h = 0; h < VN / 4; ++h) store4<E>(dst + 4 * h, src + 4 * h);
   }
-  store4<E>(reinterpret_cast<E*>(a.packed) + pr * a.ld_packed + col, v);
 }
 
 template <typename E>
@@ -79,7 +81,10 @@ extern "C" int catseg_class_seq_pack(const CatsegClassSeqArgs* a, void* stream) 
   CATSEG_CHECK(a->ld_qkv >= 3 * a->C && a->ld_packed >= 3 * a->C, "class_seq_pack: row strides too small");
   CATSEG_CHECK(a->ld_qkv % 4 == 0 && a->ld_packed % 4 == 0 && (uintptr_t)a->qkv % 16 == 0 &&
                (uintptr_t)a->packed % 16 == 0, "class_seq_pack: rows must allow 4-element vector access");
-  const int64_t n = a->B * a->HW * (int64_t)(a->T + a->n_pad) * (3 * a->C / 4);
+  const int vn = a->dtype == CATSEG_BF16 ? 8 : 4;
+  CATSEG_CHECK(a->ld_qkv % vn == 0 && a->ld_packed % vn == 0, "class_seq_pack: rows must allow 16-byte chunks");
+  const int64_t n = a->B * a->HW * (int64_t)(a->T + a->n_pad) * (3 * a->C / vn);
+  CATSEG_CHECK(n < (1LL << 31), "class_seq_pack: too many chunks for 32-bit indexing");
   const unsigned grid = (unsigned)((n + 255) / 256);
   if (a->dtype == CATSEG_BF16)
     hipLaunchKernelGGL(class_seq_pack_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a, n);
