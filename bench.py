@@ -412,7 +412,8 @@ def _queued_profile(step, stream):
     pass measures the host's enqueue time of the whole step, and the recorded pass is enqueued behind
     a spin kernel (torch.cuda._sleep) that holds the stream for about twice that long: the launches
     then run back to back exactly as in the replayed graph, and every event pair brackets GPU time
-    only.  Returns (records, timing note, gap fraction: idle share of the recorded span)."""
+    only; one unrecorded step runs first, so the recorded one starts from full clocks and warm caches.
+    Returns (records, timing note, gap fraction: idle share of the recorded span)."""
     ops.PROFILE = []
     with torch.no_grad(), torch.cuda.stream(stream):
         torch.cuda.synchronize()
@@ -430,13 +431,18 @@ def _queued_profile(step, stream):
             e1.record(stream)
         torch.cuda.synchronize()
         cyc_per_ms = 2_000_000 / max(e0.elapsed_time(e1), 1e-3)
-        ops.PROFILE = []
+        # behind the spin: one unrecorded step (the GPU leaves the idle-ish spin at full clocks and warm
+        # caches, as in a run of back-to-back steps), then the recorded one
+        spin_ms = 4e3 * host_s + 20.0
         with torch.no_grad(), torch.cuda.stream(stream):
-            torch.cuda._sleep(int(cyc_per_ms * (2e3 * host_s + 20.0)))
+            torch.cuda._sleep(int(cyc_per_ms * spin_ms))
+            step()
+            ops.PROFILE = []
             step()
         torch.cuda.synchronize()
         recs, ops.PROFILE = ops.PROFILE, None
-        note = f"queued behind a {2e3 * host_s + 20:.0f} ms spin kernel (host enqueue {host_s * 1e3:.0f} ms)"
+        note = (f"queued behind a {spin_ms:.0f} ms spin kernel and one unrecorded step "
+                f"(host enqueue {host_s * 1e3:.0f} ms per step)")
     busy = sum(r["start"].elapsed_time(r["end"]) for r in recs)
     span = recs[0]["start"].elapsed_time(recs[-1]["end"]) if recs else 0.0
     return recs, note, (round(1.0 - busy / span, 4) if span > 0 else None)
