@@ -1,5 +1,3 @@
-cd $GRAFT_REPO_ROOT && O=gpurun_out/r06k && mkdir -p $O &&
-timeout -k 10 300 python -u tools/ab_knob.py gemm_group 4 2 8 4 > $O/ab_gemm_group.log 2>&1 &&
-timeout -k 10 300 python -u tools/ab_knob.py gemm4_group 5 3 8 5 > $O/ab_gemm4_group.log 2>&1 &&
-timeout -k 10 300 python -u tools/ab_knob.py ln_variant 0 2 3 0 > $O/ab_ln_variant.log 2>&1 &&
-timeout -k 10 300 python -u tools/ab_knob.py attn_tail_skip 0 1 0 > $O/ab_attn_tail.log 2>&1
+cd $GRAFT_REPO_ROOT && O=gpurun_out/r06l && mkdir -p $O &&
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bench.py tests/test_gpu_boundary.py -x -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
