@@ -95,6 +95,31 @@ def test_engine_b16_config2_vs_oracle(dtype):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("option", ["full", "vpt"])
+def test_engine_l14_options_vs_oracle(option):
+    """The round-6 options at the benchmarked geometry (ViT-L/14@336, T = 150 padded to 256, bf16):
+    ATTENTION_TYPE "full" (model.py:289-320) and 10 visual prompt tokens in all 24 vision blocks
+    (model_vpt.py:243-265), one image against the fp32 CPU oracle; gate as config 3's bf16 logits
+    (max-abs 5e-2, mean-abs 5e-3)."""
+    arch = (VIT_L14_336.replace(attention_type="full") if option == "full" else
+            VIT_L14_336.replace(prompt_depth=VIT_L14_336.vision_layers, prompt_length=10))
+    sd = synthesize_state_dict(arch, seed=0)
+    gen = torch.Generator().manual_seed(11)
+    text = torch.nn.functional.normalize(torch.randn(150, arch.embed_dim, generator=gen), dim=-1)
+    imgs = [torch.randint(0, 256, (3, 336, 336), generator=gen).float()]
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    clip_images, _ = O.preprocess(arch, imgs)
+    ref = O.head_logits(arch, sd, clip_images, text.unsqueeze(1))
+    eng = CatSegEngine(arch, sd, dtype=torch.bfloat16)
+    eng.set_text(text.cuda())
+    raw, sizes = batch_raw(imgs)
+    got = eng.head_logits(raw, sizes).cpu()
+    err = (got - ref).abs()
+    print(f"L/14 {option}: max {err.max().item():.3e} mean {err.mean().item():.3e}")
+    assert err.max().item() < 5e-2 and err.mean().item() < 5e-3
+
+
+@pytest.mark.timeout(600)
 def test_engine_l14_config5_fp8_sliding_vs_oracle():
     """Config 5 geometry: ViT-L/14 sliding-window 640² inference with fp8 (e4m3, per-row
     scales) CLIP image-encoder GEMMs, against the fp32 CPU oracle's sliding branch
